@@ -1,0 +1,247 @@
+"""Generate golden vectors by importing the pyABC 0.10.5 reference.
+
+Runs in the BUILD container only (needs /root/reference); the outputs are
+small .npz/.json fixtures committed next to this script.  Nothing here is
+imported by the product or shipped to the GPU box.
+
+    PYTHONDONTWRITEBYTECODE=1 OMP_NUM_THREADS=1 \
+      PYTHONPATH=/root/reference:tests/golden python tests/golden/make_golden.py [--e2e]
+
+Each fixture stores its inputs, seed and the reference outputs.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import pandas as pd
+
+import stub_env  # noqa: F401  (must precede pyabc)
+import pyabc
+from pyabc.transition import MultivariateNormalTransition, LocalTransition
+from pyabc.distance import PNormDistance, AdaptivePNormDistance
+from pyabc.distance.scale import (standard_deviation,
+                                  median_absolute_deviation)
+from pyabc.weighted_statistics import weighted_quantile
+from pyabc.epsilon import QuantileEpsilon
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def names(d):
+    return [f"p{k:02d}" for k in range(d)]
+
+
+def mvn_case(tag, X, w, x, scaling=1.0):
+    d = X.shape[1]
+    cols = names(d)
+    Xdf = pd.DataFrame(X, columns=cols)
+    t = MultivariateNormalTransition(scaling=scaling)
+    wref = w.copy()
+    t.fit(Xdf, wref)
+    xdf = pd.DataFrame(x, columns=cols)
+    pdf = np.atleast_1d(t.pdf(xdf))
+    np.savez_compressed(os.path.join(HERE, f"mvn_{tag}.npz"), X=X, w=w, x=x,
+                        scaling=scaling, cov=t.cov, w_fit=wref, pdf=pdf)
+    print("mvn", tag, X.shape, pdf[:3])
+
+
+def gen_mvn():
+    rng = np.random.default_rng(12345)
+    for d, N in [(1, 1000), (2, 500), (10, 4096)]:
+        X = rng.normal(0.5, 1.0, size=(N, d)) * (1 + np.arange(d))
+        w = np.exp(0.5 * rng.standard_normal(N))
+        w /= w.sum()
+        par = rng.integers(0, N, size=256)
+        x = X[par] + 0.3 * rng.standard_normal((256, d)) * (1 + np.arange(d))
+        mvn_case(f"d{d}_n{N}", X, w, x)
+    # un-normalised weights (fit normalises in place) and scaling != 1
+    X = rng.normal(size=(300, 3))
+    w = rng.uniform(0.5, 2.0, size=300)
+    x = X[:64] + 0.1 * rng.standard_normal((64, 3))
+    mvn_case("d3_unnorm_scaled", X, w, x, scaling=0.5)
+    # singular: last coordinate constant -> rank 2 of 3
+    X = rng.normal(size=(200, 3))
+    X[:, 2] = 1.25
+    w = np.full(200, 1 / 200)
+    x = X[:40] + np.c_[0.2 * rng.standard_normal((40, 2)), np.zeros(40)]
+    x[::4, 2] += 0.5     # every 4th candidate leaves the support
+    mvn_case("singular", X, w, x)
+    # single particle: diag(|x0|) covariance
+    X = np.array([[0.7, -1.3]])
+    w = np.array([1.0])
+    x = X + 0.2 * rng.standard_normal((16, 2))
+    mvn_case("n1", X, w, x)
+
+
+def gen_local():
+    rng = np.random.default_rng(99)
+    N, d = 400, 5
+    comp = rng.integers(0, 2, size=N)
+    A = np.tril(rng.normal(size=(d, d))) * 0.3 + np.eye(d) * 0.5
+    X = rng.standard_normal((N, d)) @ A.T + comp[:, None] * 2.0
+    w = np.exp(0.5 * rng.standard_normal(N))
+    w /= w.sum()
+    x = X[rng.integers(0, N, 64)] + 0.2 * rng.standard_normal((64, d))
+    cols = names(d)
+    for tag, kw in [("k50", dict(k=50, k_fraction=None)),
+                    ("default", dict())]:
+        t = LocalTransition(**kw)
+        t.fit(pd.DataFrame(X, columns=cols), w.copy())
+        pdf = np.atleast_1d(t.pdf(pd.DataFrame(x, columns=cols)))
+        np.savez_compressed(os.path.join(HERE, f"local_{tag}.npz"), X=X, w=w,
+                            x=x, k=t.k, covs=t.covs, inv_covs=t.inv_covs,
+                            dets=t.determinants,
+                            normalization=t.normalization, pdf=pdf)
+        print("local", tag, t.k, pdf[:3])
+
+
+def gen_distance():
+    rng = np.random.default_rng(7)
+    out = {}
+    for S in (1, 10, 256):
+        keys = [f"s{k:03d}" for k in range(S)][::-1]   # non-sorted key order
+        x0 = {k: float(v) for k, v in zip(keys, rng.normal(size=S))}
+        xs = rng.normal(size=(50, S)) * rng.uniform(0.1, 5, size=S)
+        wts = {k: float(v) for k, v in zip(keys, rng.uniform(0.2, 3, size=S))}
+        fac = {k: float(v) for k, v in zip(keys, rng.uniform(0.5, 2, size=S))}
+        for p in (1, 2, np.inf):
+            dist = PNormDistance(p=p, weights=wts, factors=fac)
+            dist.initialize(0, lambda: [], x0)
+            dv = [dist({k: float(v) for k, v in zip(keys, row)}, x0, 0)
+                  for row in xs]
+            ptag = "inf" if p == np.inf else str(p)
+            out[f"S{S}_p{ptag}"] = dict(
+                x=xs, x0=np.array([x0[k] for k in keys]),
+                w=np.array([wts[k] for k in keys]),
+                f=np.array([fac[k] for k in keys]), p=float(p),
+                d=np.array(dv))
+    np.savez_compressed(os.path.join(HERE, "pnorm.npz"),
+                        **{f"{c}__{f}": v for c, dct in out.items()
+                           for f, v in dct.items()})
+    print("pnorm", list(out))
+    # adaptive weights
+    res = {}
+    for R in (101, 100):
+        S = 12
+        keys = [f"y{k}" for k in range(S)]
+        data = rng.normal(size=(R, S)) * 10.0 ** rng.uniform(-2, 2, size=S)
+        data[:, 3] = 4.2          # zero-scale key -> weight 0
+        data[:, 5] = np.round(data[:, 5])  # ties for the MAD
+        x0 = {k: 0.0 for k in keys}
+        ss = [{k: float(v) for k, v in zip(keys, row)} for row in data]
+        for sname, sf in [("std", standard_deviation),
+                          ("mad", median_absolute_deviation)]:
+            for ratio in (None, 5.0):
+                dist = AdaptivePNormDistance(scale_function=sf,
+                                             max_weight_ratio=ratio)
+                dist.initialize(0, lambda: ss, x0)
+                wv = np.array([dist.weights[0][k] for k in keys])
+                tag = f"R{R}_{sname}_r{ratio}"
+                res[tag + "__data"] = data
+                res[tag + "__w"] = wv
+                res[tag + "__ratio"] = np.nan if ratio is None else ratio
+    np.savez_compressed(os.path.join(HERE, "adaptive.npz"), **res)
+    print("adaptive", len(res) // 3)
+
+
+def gen_quantile():
+    rng = np.random.default_rng(3)
+    res = {}
+    cases = {
+        "n10k": (rng.exponential(size=10000), rng.uniform(0, 1, size=10000)),
+        "ties": (np.repeat(rng.normal(size=50), 7),
+                 rng.uniform(0, 1, size=350)),
+        "zerow": (rng.normal(size=500),
+                  np.where(rng.uniform(size=500) < 0.3, 0.0,
+                           rng.uniform(size=500))),
+        "n1": (np.array([3.5]), np.array([1.0])),
+    }
+    for name, (pts, w) in cases.items():
+        w = w / w.sum()
+        for a in (0.2, 0.5, 0.9, 1.0):
+            q = weighted_quantile(pts, w, alpha=a)
+            res[f"{name}__a{a}__q"] = q
+        res[f"{name}__points"] = pts
+        res[f"{name}__w"] = w
+        # QuantileEpsilon update path, weighted and not, multiplier
+        for weighted in (True, False):
+            eps = QuantileEpsilon(alpha=0.3, quantile_multiplier=1.1,
+                                  weighted=weighted)
+            df = pd.DataFrame({"distance": pts, "w": w * 2.0})
+            eps.initialize(0, lambda: df, None, 10, None)
+            res[f"{name}__eps_w{int(weighted)}"] = eps(0)
+    np.savez_compressed(os.path.join(HERE, "quantile.npz"), **res)
+    print("quantile", len(cases))
+
+
+def gen_step():
+    """Fixed-input generation step: population, weights, candidates, eps ->
+    distances, accept mask, importance weights (smc.py:768-811)."""
+    rng = np.random.default_rng(2024)
+    d, N, M = 4, 800, 512
+    cols = names(d)
+    X = rng.normal(0.5, 0.5, size=(N, d))
+    w = np.exp(0.3 * rng.standard_normal(N))
+    w /= w.sum()
+    prior = pyabc.Distribution(**{c: pyabc.RV("norm", 0, 1) for c in cols})
+    t = MultivariateNormalTransition()
+    t.fit(pd.DataFrame(X, columns=cols), w.copy())
+    theta = X[rng.integers(0, N, M)] + 0.4 * rng.standard_normal((M, d))
+    noise = rng.standard_normal((M, d))
+    xsim = theta + 0.5 * noise
+    x0 = {f"y{k}": 1.0 for k in range(d)}
+    dist = PNormDistance(p=2)
+    dist.initialize(1, lambda: [], x0)
+    dv = np.array([dist({f"y{k}": row[k] for k in range(d)}, x0, 1)
+                   for row in xsim])
+    eps = float(np.quantile(dv, 0.4))
+    acc = dv <= eps
+    prior_pd = np.array([prior.pdf(pyabc.Parameter(
+        **{c: v for c, v in zip(cols, row)})) for row in theta])
+    trans_pd = np.atleast_1d(t.pdf(pd.DataFrame(theta, columns=cols)))
+    weight = np.where(acc, prior_pd / trans_pd, 0.0)
+    np.savez_compressed(os.path.join(HERE, "step.npz"), X=X, w=w,
+                        theta=theta, xsim=xsim, x0=np.ones(d), eps=eps,
+                        d=dv, accept=acc, prior_pd=prior_pd,
+                        trans_pd=trans_pd, weight=weight)
+    print("step", acc.sum(), "accepted of", M)
+
+
+def gen_e2e(seeds=(0, 1, 2, 3)):
+    """End-to-end reference moments (statistical parity targets)."""
+    out = {}
+    for s in seeds:
+        np.random.seed(s)
+        t0 = time.time()
+
+        def model(p):
+            return {"y": p["x"] + 0.5 * np.random.randn()}
+        abc = pyabc.ABCSMC(model, pyabc.Distribution(x=pyabc.RV("norm", 0, 1)),
+                           pyabc.PNormDistance(), population_size=1000,
+                           sampler=pyabc.SingleCoreSampler())
+        abc.new("sqlite://", {"y": 2.0})
+        h = abc.run(max_nr_populations=8)
+        df, w = h.get_distribution(0, h.max_t)
+        pops = h.get_all_populations()
+        out[f"c1_seed{s}"] = dict(
+            mean=float((df["x"].values * w).sum()),
+            sd=float(np.sqrt((w * (df["x"].values
+                                   - (df["x"].values * w).sum()) ** 2).sum())),
+            eps=[float(e) for e in pops["epsilon"].values],
+            samples=[int(n) for n in pops["samples"].values],
+            seconds=time.time() - t0)
+        print("e2e c1 seed", s, out[f"c1_seed{s}"])
+    with open(os.path.join(HERE, "e2e_reference.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    gen_mvn()
+    gen_local()
+    gen_distance()
+    gen_quantile()
+    gen_step()
+    if "--e2e" in sys.argv:
+        gen_e2e()

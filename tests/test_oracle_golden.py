@@ -1,0 +1,137 @@
+"""Pin the CPU oracle: reference known-answer tests + golden vectors.
+
+The known answers are the ones pyABC's own tests hold:
+test_weighted_statistics.py:10-39, test_epsilon.py:25-47,
+test_distance_function.py:80-96 and :137-155.  The golden vectors were made
+by importing the reference (tests/golden/make_golden.py).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+# ---- reference known-answer tests, restated -----------------------------
+
+def test_kat_weighted_quantile():
+    # test_weighted_statistics.py:10-39
+    pts = np.array([1, 2, 3, 4.])
+    w = np.array([.25, .25, .25, .25])
+    assert oracle.weighted_quantile(pts, w, alpha=.5) == 2.5
+    w = np.array([.1, .2, .3, .4])
+    assert 3 <= oracle.weighted_quantile(pts, w, alpha=.5) <= 4
+    assert oracle.weighted_quantile(pts, np.array([.1, .2, .3, .4]), 1) == 4
+    assert oracle.weighted_quantile(pts, None, 0.2) == 1.3
+
+
+def test_kat_quantile_epsilon():
+    # test_epsilon.py:25-47: unweighted median of [1,2,3,4] * 1.1
+    e = oracle.quantile_epsilon([1, 2, 3, 4], [1, 1, 1, 1], alpha=.5,
+                                multiplier=1.1, weighted=False)
+    assert e == pytest.approx(2.5 * 1.1)
+    e = oracle.quantile_epsilon([1, 2, 3, 4], [.1, .2, .3, .4], alpha=.9)
+    assert 3 <= e <= 4
+
+
+def test_kat_pnorm():
+    # test_distance_function.py:80-96: |(1,2)|_2 weighted -> sqrt(5)
+    d = oracle.pnorm([[1, 2]], [0, 0], w=[1, 1], p=2)
+    assert d[0] == pytest.approx(np.sqrt(5))
+    # test_distance_function.py:137-155: initial weights (1, 2) -> sqrt(2^2+6^2)
+    d = oracle.pnorm([[2, 3]], [0, 0], w=[1, 2], p=2)
+    assert d[0] == pytest.approx(np.sqrt(2 ** 2 + 6 ** 2))
+
+
+# ---- golden vectors from the imported reference --------------------------
+
+MVN = ["d1_n1000", "d2_n500", "d10_n4096", "d3_unnorm_scaled", "singular",
+       "n1"]
+
+
+@pytest.mark.parametrize("tag", MVN)
+def test_mvn_fit_and_pdf(tag):
+    g = load(f"mvn_{tag}.npz")
+    cov, wn = oracle.mvn_fit(g["X"], g["w"], scaling=float(g["scaling"]))
+    np.testing.assert_allclose(cov, g["cov"], rtol=1e-10, atol=1e-14)
+    np.testing.assert_allclose(wn, g["w_fit"], rtol=1e-13)
+    pdf = oracle.mvn_pdf(g["x"], g["X"], wn, cov)
+    np.testing.assert_allclose(pdf, g["pdf"], rtol=1e-9, atol=0)
+
+
+@pytest.mark.parametrize("tag", ["k50", "default"])
+def test_local_fit_and_pdf(tag):
+    g = load(f"local_{tag}.npz")
+    kw = dict(k=50, k_fraction=None) if tag == "k50" else {}
+    fit = oracle.local_fit(g["X"], g["w"], **kw)
+    assert fit["k"] == int(g["k"])
+    np.testing.assert_allclose(fit["covs"], g["covs"], rtol=1e-9, atol=1e-13)
+    np.testing.assert_allclose(fit["dets"], g["dets"], rtol=1e-8)
+    pdf = oracle.local_pdf(g["x"], g["X"], fit)
+    np.testing.assert_allclose(pdf, g["pdf"], rtol=1e-9)
+
+
+def test_pnorm_golden():
+    g = load("pnorm.npz")
+    cases = sorted({k.split("__")[0] for k in g.files})
+    assert len(cases) == 9
+    for c in cases:
+        d = oracle.pnorm(g[c + "__x"], g[c + "__x0"], g[c + "__w"],
+                         g[c + "__f"], float(g[c + "__p"]))
+        np.testing.assert_allclose(d, g[c + "__d"], rtol=1e-12, err_msg=c)
+
+
+def test_adaptive_golden():
+    g = load("adaptive.npz")
+    tags = sorted({k.split("__")[0] for k in g.files})
+    assert len(tags) == 8
+    for t in tags:
+        sf = "std" if "_std_" in t else "mad"
+        ratio = float(g[t + "__ratio"])
+        w = oracle.adaptive_weights(g[t + "__data"], sf,
+                                    max_weight_ratio=None if np.isnan(ratio)
+                                    else ratio)
+        np.testing.assert_allclose(w, g[t + "__w"], rtol=1e-12, err_msg=t)
+
+
+def test_quantile_golden():
+    g = load("quantile.npz")
+    for name in ("n10k", "ties", "zerow", "n1"):
+        pts, w = g[f"{name}__points"], g[f"{name}__w"]
+        for a in (0.2, 0.5, 0.9, 1.0):
+            q = oracle.weighted_quantile(pts, w, a)
+            assert q == pytest.approx(float(g[f"{name}__a{a}__q"]),
+                                      rel=1e-13), (name, a)
+        for weighted in (True, False):
+            e = oracle.quantile_epsilon(pts, w * 2.0, 0.3, 1.1, weighted)
+            assert e == pytest.approx(float(g[f"{name}__eps_w{int(weighted)}"]),
+                                      rel=1e-13)
+
+
+def test_step_golden():
+    g = load("step.npz")
+    cov, wn = oracle.mvn_fit(g["X"], g["w"])
+    tp = oracle.mvn_pdf(g["theta"], g["X"], wn, cov)
+    np.testing.assert_allclose(tp, g["trans_pd"], rtol=1e-10)
+    d = oracle.pnorm(g["xsim"], g["x0"], p=2)
+    np.testing.assert_allclose(d, g["d"], rtol=1e-13)
+    acc = d <= float(g["eps"])
+    np.testing.assert_array_equal(acc, g["accept"])
+    from scipy.stats import norm
+    prior = norm.pdf(g["theta"]).prod(1)
+    np.testing.assert_allclose(prior, g["prior_pd"], rtol=1e-13)
+    wt = np.where(acc, oracle.importance_weights(prior, tp), 0.0)
+    np.testing.assert_allclose(wt, g["weight"], rtol=1e-10)
+
+
+def test_philox_known_answer():
+    # Random123 KAT: philox4x32_10(ctr=0, key=0)
+    r = oracle.philox4x32_10(np.zeros(1, np.uint64), 0, 0, 0)[0]
+    assert [int(v) for v in r] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c,
+                                   0x9b00dbd8]
