@@ -1,0 +1,205 @@
+/*
+ * libabcgpu -- C ABI of the MI355X (gfx950) batched ABC-SMC generation engine.
+ *
+ * Drop-in boundary for pyABC 0.10.5's hot path.  pyABC has no FFI of its own
+ * (it is pure Python); these entry points are what its plugin
+ * classes bind through ctypes (INTEGRATION.md shows the binding).  Each group
+ * cites the reference interface it replaces.
+ *
+ * Conventions
+ *   - Every pointer is DEVICE memory owned by the caller (torch tensors in the
+ *     Python layer), except where a parameter says "host".
+ *   - Parameters are row-major [rows x d] float64, columns in the reference's
+ *     order (sorted parameter names, pyabc/storage/history.py:307); summary
+ *     statistics in x_0 key order (pyabc/distance/distance.py:113-125).
+ *   - `stream` is a hipStream_t (NULL = default stream).  Calls are
+ *     stream-ordered and asynchronous unless stated; nothing allocates device
+ *     memory inside a call: scratch comes from a caller workspace whose size
+ *     the matching *_workspace() query returns.
+ *   - Return 0 on success, a negative ABC_ERR_* code otherwise; the message is
+ *     in abc_last_error() (thread-local).  No C++ exception crosses the ABI.
+ */
+#ifndef ABCGPU_H
+#define ABCGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ABC_OK 0
+#define ABC_ERR_INVALID (-1)
+#define ABC_ERR_HIP (-2)
+#define ABC_ERR_WORKSPACE (-3)
+#define ABC_ERR_NOT_ENOUGH_PARTICLES (-4)
+#define ABC_ERR_UNSUPPORTED (-5)
+
+/* Precision of the transition-density kernel. */
+#define ABC_PREC_F64 0 /* f64 MFMA cross term: parity mode (default)   */
+#define ABC_PREC_F32 1 /* f32 MFMA cross term: fast mode (~3e-5 rel.)  */
+
+/* Prior distribution kinds (scipy.stats names, loc/scale convention). */
+#define ABC_PRIOR_FLAT (-1)  /* no prior: density 1 everywhere (plain rvs) */
+#define ABC_PRIOR_NORM 0    /* params: loc, scale                       */
+#define ABC_PRIOR_UNIFORM 1 /* params: loc, scale -> U[loc, loc+scale]  */
+#define ABC_PRIOR_EXPON 2   /* params: loc, scale                       */
+#define ABC_PRIOR_LAPLACE 3 /* params: loc, scale                       */
+#define ABC_PRIOR_LOGNORM 4 /* params: s, loc, scale                    */
+#define ABC_PRIOR_GAMMA 5   /* params: a, loc, scale                    */
+#define ABC_PRIOR_BETA 6    /* params: a, b, loc, scale                 */
+
+const char* abc_last_error(void);
+int abc_version(void);
+
+/* ---- reductions used by the fits ------------------------------------------
+ * Replaces the numpy work in MultivariateNormalTransition.fit
+ * (pyabc/transition/multivariatenormal.py:72-83, smart_cov util.py:4-16):
+ * out[0] = sum w, out[1] = sum w^2, out[2 .. 2+d) = weighted mean
+ * (sum w x / sum w), out[2+d .. 2+d+d*d) = sum w (x-mean)(x-mean)^T / sum w.
+ * Deterministic two-pass fp64 (per-block partials, fixed-order combine). */
+size_t abc_weighted_moments_workspace(int64_t N, int d);
+int abc_weighted_moments(const double* X, const double* w, int64_t N, int d,
+                         double* out, void* ws, size_t ws_bytes, void* stream);
+
+/* Inclusive prefix sum (fp64), the cumulative weights behind
+ * np.random.choice(p=w) in MultivariateNormalTransition.rvs
+ * (multivariatenormal.py:85-91). */
+size_t abc_scan_workspace(int64_t N);
+int abc_inclusive_scan_f64(const double* in, double* out, int64_t N, void* ws,
+                           size_t ws_bytes, void* stream);
+
+/* ---- MultivariateNormalTransition.pdf (multivariatenormal.py:99-113) -----
+ * density(x_i) = sum_j w_j N(x_i - X_j; 0, Sigma).  Host supplies the fp64
+ * eigen-whitening of Sigma (scipy _PSD semantics): U [d x r], mean mu [d].
+ * pack: builds the MFMA A-operand image of the population once per fit:
+ *   y_j = (X_j - mu) U,  c_j = log(w_j) + log_w_shift - |y_j|^2 / 2.
+ * logpdf: out[i] = log(sum_j w_j exp(-|(x_i - X_j) U|^2 / 2)) + log_const,
+ *   with log_const = -(r log 2pi + log pdet)/2 - log_w_shift supplied by the
+ *   host.  prec selects the f64- or f32-MFMA kernel (ABC_PREC_*).  r <= 60. */
+size_t abc_mvn_packed_bytes(int64_t N, int r, int prec);
+int abc_mvn_pack_population(const double* X, const double* w, int64_t N, int d,
+                            const double* mu, const double* U, int r,
+                            double log_w_shift, int prec, void* packed,
+                            void* stream);
+size_t abc_mvn_logpdf_workspace(int64_t M, int64_t N, int r, int prec);
+int abc_mvn_logpdf(const double* x, int64_t M, int d, const void* packed,
+                   int64_t N, const double* mu, const double* U, int r,
+                   int prec, double log_const, double* out, void* ws,
+                   size_t ws_bytes, void* stream);
+/* Direct-difference fp64 VALU path: any r, and scipy's singular-covariance
+ * support mask (pairs with |(x_i - X_j) V| >= support_tol get density 0;
+ * V [d x nv] null-space basis, nv = d - r). */
+int abc_mvn_logpdf_direct(const double* x, int64_t M, const double* X,
+                          const double* w, int64_t N, int d, const double* U,
+                          int r, const double* V, int nv, double support_tol,
+                          double log_const, double* out, void* stream);
+
+/* ---- proposal: Transition.rvs + prior support (smc.py:610-662) ----------
+ * Candidate g (global index idx0 .. idx0+B-1) draws, from Philox4x32-10 keyed
+ * by (seed, generation, g, slot), an ancestor j ~ Cat(w) by inverse CDF over
+ * `cdf` (inclusive prefix of w) and theta = X_j + L n, n ~ N(0, I_d)
+ * (L: any square root of Sigma, [d x d] row-major).  It re-draws while the
+ * prior density is 0 (smc.py:654-656; at most max_attempts), and writes
+ * theta [B x d], prior log-density [B], ancestor [B] and attempts used [B]
+ * (attempts > max_attempts means "gave up").  With X == NULL it samples the
+ * prior itself (t = 0, smc.py:631-634).
+ * Prior: per dimension kind[k] (ABC_PRIOR_*) and params[4k .. 4k+4). */
+int abc_propose(const double* X, const double* cdf, int64_t N, int d,
+                const double* L, const int32_t* prior_kind,
+                const double* prior_params, uint64_t seed, uint32_t generation,
+                int64_t idx0, int64_t B, int max_attempts, double* theta,
+                double* prior_logpdf, int64_t* ancestor, int32_t* attempts,
+                void* stream);
+/* Prior log-density of given parameters (Distribution.pdf,
+ * pyabc/random_variables.py:425-452), product over dimensions. */
+int abc_prior_logpdf(const double* theta, int64_t B, int d,
+                     const int32_t* prior_kind, const double* prior_params,
+                     double* out, void* stream);
+
+/* ---- vectorised synthetic simulator (the Model.sample boundary,
+ * pyabc/model.py:89-116): x[b,k] = a[k] * theta[b, src[k]] + sigma[k] * e,
+ * e ~ N(0,1) from Philox slot 0x40000000 + k/2 of candidate idx0+b. */
+int abc_simulate_linear_gaussian(const double* theta, int64_t B, int d, int S,
+                                 const int32_t* src, const double* a,
+                                 const double* sigma, uint64_t seed,
+                                 uint32_t generation, int64_t idx0, double* x,
+                                 void* stream);
+
+/* ---- PNormDistance.__call__ (pyabc/distance/distance.py:79-105) ----------
+ * d[b] = (sum_k |wf[k] (x[b,k] - x0[k])|^p)^(1/p); p = +inf -> max.
+ * wf = weights * factors, in x_0 key order. */
+int abc_pnorm(const double* x, int64_t B, int S, const double* x0,
+              const double* wf, double p, double* d, void* stream);
+
+/* ---- UniformAcceptor (acceptor.py:235-244) + order-preserving compaction -
+ * accept[b] = d[b] <= eps.  Writes the positions of accepted rows in
+ * increasing order to idx and their number to *count (device int64). */
+size_t abc_compact_workspace(int64_t B);
+int abc_accept_compact(const double* d, int64_t B, double eps, int64_t* idx,
+                       int64_t* count, void* ws, size_t ws_bytes,
+                       void* stream);
+/* Gather rows: out[i, :] = in[idx[i], :] (row width `cols` doubles). */
+int abc_gather_rows(const double* in, const int64_t* idx, int64_t n, int cols,
+                    double* out, void* stream);
+
+/* ---- importance weight (smc.py:768-811, single model) --------------------
+ * w[i] = exp(prior_logpdf[i] - trans_logpdf[i]) * scale  (t > 0). */
+int abc_importance_weights(const double* prior_logpdf,
+                           const double* trans_logpdf, int64_t A, double scale,
+                           double* w, void* stream);
+
+/* ---- QuantileEpsilon (epsilon.py:202-228 -> weighted_statistics.py:27-43)
+ * Stable LSD radix sort of fp64 keys carrying fp64 values, then
+ * q = interp(alpha, cumsum(w) - w/2, sorted keys) with w normalised by its
+ * sum.  Result written to *q (device double). */
+size_t abc_sort_pairs_workspace(int64_t N);
+int abc_sort_pairs_f64(const double* keys, const double* vals, int64_t N,
+                       double* keys_out, double* vals_out, void* ws,
+                       size_t ws_bytes, void* stream);
+size_t abc_weighted_quantile_workspace(int64_t N);
+int abc_weighted_quantile(const double* points, const double* w, int64_t N,
+                          double alpha, double* q, void* ws, size_t ws_bytes,
+                          void* stream);
+
+/* ---- AdaptivePNormDistance._update scales (distance.py:263-307,
+ * scale.py:38-65) over recorded sum stats X [R x S] (row-major):
+ * std: np.std (ddof 0); mad: median(|x - median(x)|), even R averaging the
+ * two middle order statistics like np.median. */
+size_t abc_column_stats_workspace(int64_t R, int S);
+int abc_column_std(const double* X, int64_t R, int S, double* out, void* ws,
+                   size_t ws_bytes, void* stream);
+int abc_column_mad(const double* X, int64_t R, int S, double* out, void* ws,
+                   size_t ws_bytes, void* stream);
+
+/* ---- LocalTransition (pyabc/transition/local_transition.py:77-145) -------
+ * fit: per particle n, the k nearest other particles (ties by index),
+ * weighted covariance of their offsets (weights renormalised, unbiased
+ * 1/(1 - sum a^2)), all-zero -> diag(|X[0]|), times scaling, then
+ * "while det <= 0: cov += eps I".  Writes covs, inverse covs, dets,
+ * Cholesky factors (for rvs) and log normalisation
+ * log sqrt((2 pi)^d det) per particle.  d <= 8. */
+size_t abc_local_fit_workspace(int64_t N, int d);
+int abc_local_fit(const double* X, const double* w, int64_t N, int d,
+                  int64_t k, double scaling, double eps, double* covs,
+                  double* inv_covs, double* dets, double* chol,
+                  double* log_norm, void* ws, size_t ws_bytes, void* stream);
+/* pdf: out[i] = log( sum_j w_j exp(-d_ij^T inv_j d_ij / 2 - log_norm_j)
+ * / sum_j w_j ), d_ij = X_j - x_i. */
+int abc_local_logpdf(const double* x, int64_t M, const double* X,
+                     const double* w, int64_t N, int d, const double* inv_covs,
+                     const double* log_norm, double* out, void* stream);
+/* rvs: ancestor j ~ Cat(w) (cdf), theta = X_j + chol_j n; same Philox keying
+ * and prior re-draw loop as abc_propose. */
+int abc_local_propose(const double* X, const double* cdf, int64_t N, int d,
+                      const double* chol, const int32_t* prior_kind,
+                      const double* prior_params, uint64_t seed,
+                      uint32_t generation, int64_t idx0, int64_t B,
+                      int max_attempts, double* theta, double* prior_logpdf,
+                      int64_t* ancestor, int32_t* attempts, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ABCGPU_H */

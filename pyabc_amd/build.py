@@ -1,0 +1,70 @@
+"""Build libabcgpu.so (gfx950) in-tree with hipcc.
+
+    python -m pyabc_amd.build          # incremental
+    python -m pyabc_amd.build --force
+
+The shared library lands next to this file so that it travels with the repo
+snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+"""
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+ROOT = os.path.dirname(HERE)
+OBJ = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "libabcgpu.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}",
+         "-I", os.path.join(ROOT, "include"), "-Wno-unused-result"]
+
+
+def _sources():
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
+                  if f.endswith((".hip", ".cpp")))
+
+
+def _headers():
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hs.append(os.path.join(ROOT, "include", "abcgpu.h"))
+    return hs
+
+
+def _compile(src):
+    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    newest_dep = max([os.path.getmtime(src)] +
+                     [os.path.getmtime(h) for h in _headers()])
+    if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
+        return obj, False
+    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+    return obj, True
+
+
+def build(force=False, verbose=True):
+    os.makedirs(OBJ, exist_ok=True)
+    if force:
+        for f in os.listdir(OBJ):
+            os.remove(os.path.join(OBJ, f))
+    srcs = _sources()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        results = list(ex.map(_compile, srcs))
+    objs = [o for o, _ in results]
+    changed = any(c for _, c in results) or not os.path.exists(LIB)
+    if changed:
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+    if verbose:
+        print(f"libabcgpu: {LIB} ({'rebuilt' if changed else 'up to date'})")
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,283 @@
+// Deterministic fp64 reductions and scans for the fits and the sampler.
+//
+// abc_weighted_moments: the numpy work inside
+//   MultivariateNormalTransition.fit (pyabc/transition/multivariatenormal.py:72-83)
+//   -> smart_cov (pyabc/transition/util.py:4-16) = np.cov(X, aweights=w).
+// abc_inclusive_scan_f64: cumulative weights for the ancestor draw of
+//   MultivariateNormalTransition.rvs (multivariatenormal.py:85-91).
+// All reductions use a fixed block count and a fixed combine order, so the
+// results are bitwise reproducible run to run (no float atomics).
+#include "abc_common.h"
+
+namespace abc {
+namespace {
+
+constexpr int MOM_BLOCKS = 256;
+constexpr int MOM_ROWS = 64;  // rows staged in LDS per step
+
+// pass 1: columns (w, w^2, w x_0 .. w x_{d-1})
+__global__ __launch_bounds__(256) void moments1_kernel(
+    const double* __restrict__ X, const double* __restrict__ w, int64_t N,
+    int d, double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* xs = lds;                    // [MOM_ROWS][d]
+  double* ws = lds + MOM_ROWS * d;     // [MOM_ROWS]
+  const int ncol = 2 + d;
+  double acc[2] = {0.0, 0.0};          // this thread's columns c0, c0+256
+  for (int64_t r0 = (int64_t)blockIdx.x * MOM_ROWS; r0 < N;
+       r0 += (int64_t)gridDim.x * MOM_ROWS) {
+    const int nr = (int)((N - r0) < MOM_ROWS ? (N - r0) : MOM_ROWS);
+    __syncthreads();
+    for (int e = threadIdx.x; e < nr * d; e += blockDim.x) xs[e] = X[r0 * d + e];
+    for (int e = threadIdx.x; e < nr; e += blockDim.x) ws[e] = w[r0 + e];
+    __syncthreads();
+    for (int h = 0; h < 2; ++h) {
+      const int c = threadIdx.x + 256 * h;
+      if (c >= ncol) continue;
+      double s = 0.0;
+      for (int r = 0; r < nr; ++r) {
+        const double wr = ws[r];
+        s += (c == 0) ? wr : (c == 1 ? wr * wr : wr * xs[r * d + (c - 2)]);
+      }
+      acc[h] += s;
+    }
+  }
+  for (int h = 0; h < 2; ++h) {
+    const int c = threadIdx.x + 256 * h;
+    if (c < ncol) part[(int64_t)blockIdx.x * ncol + c] = acc[h];
+  }
+}
+
+__global__ void moments1_final(const double* __restrict__ part, int nblk,
+                               int d, double* __restrict__ out) {
+  const int ncol = 2 + d;
+  for (int c = threadIdx.x; c < ncol; c += blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * ncol + c];
+    out[c] = s;  // 0: sum w, 1: sum w^2, 2+q: sum w x_q (mean fixed below)
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double sw = out[0];
+    for (int q = 0; q < d; ++q) out[2 + q] = out[2 + q] / sw;
+  }
+}
+
+// pass 2: sum w (x - mean)(x - mean)^T, one (a, b) entry per thread slot
+__global__ __launch_bounds__(256) void moments2_kernel(
+    const double* __restrict__ X, const double* __restrict__ w, int64_t N,
+    int d, const double* __restrict__ mom, double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  double* xs = lds;                    // centred rows
+  double* ws = lds + MOM_ROWS * d;
+  const double* mean = mom + 2;
+  const int npair = d * d;
+  double acc[16];
+  for (int h = 0; h < 16; ++h) acc[h] = 0.0;
+  for (int64_t r0 = (int64_t)blockIdx.x * MOM_ROWS; r0 < N;
+       r0 += (int64_t)gridDim.x * MOM_ROWS) {
+    const int nr = (int)((N - r0) < MOM_ROWS ? (N - r0) : MOM_ROWS);
+    __syncthreads();
+    for (int e = threadIdx.x; e < nr * d; e += blockDim.x)
+      xs[e] = X[r0 * d + e] - mean[e % d];
+    for (int e = threadIdx.x; e < nr; e += blockDim.x) ws[e] = w[r0 + e];
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+      const int pidx = threadIdx.x + 256 * h;
+      if (pidx >= npair) break;
+      const int a = pidx / d, b = pidx % d;
+      double s = 0.0;
+      for (int r = 0; r < nr; ++r) s += ws[r] * xs[r * d + a] * xs[r * d + b];
+      acc[h] += s;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 16; ++h) {
+    const int pidx = threadIdx.x + 256 * h;
+    if (pidx < npair) part[(int64_t)blockIdx.x * npair + pidx] = acc[h];
+  }
+}
+
+__global__ void moments2_final(const double* __restrict__ part, int nblk,
+                               int d, double* __restrict__ out) {
+  const int npair = d * d;
+  const double sw = out[0];
+  for (int c = threadIdx.x; c < npair; c += blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * npair + c];
+    out[2 + d + c] = s / sw;
+  }
+}
+
+// ---- scan -------------------------------------------------------------------
+constexpr int SCAN_T = 256, SCAN_I = 8, SCAN_TILE = SCAN_T * SCAN_I;
+
+__device__ double block_exclusive_scan(double v, double* sh, double& total) {
+  // Hillis-Steele over 256 threads in LDS (fixed order -> deterministic).
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int o = 1; o < SCAN_T; o <<= 1) {
+    double add = (t >= o) ? sh[t - o] : 0.0;
+    __syncthreads();
+    sh[t] += add;
+    __syncthreads();
+  }
+  total = sh[SCAN_T - 1];
+  double incl = sh[t];
+  __syncthreads();
+  return incl - v;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_tile_sums(
+    const double* __restrict__ in, int64_t N, double* __restrict__ sums) {
+  __shared__ double sh[SCAN_T];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_I;
+  double s = 0.0;
+  for (int k = 0; k < SCAN_I; ++k)
+    if (base + k < N) s += in[base + k];
+  double tot;
+  block_exclusive_scan(s, sh, tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_sums(double* __restrict__ sums,
+                                                    int64_t n) {
+  // exclusive scan of n tile sums, sequential chunks per thread
+  __shared__ double sh[SCAN_T];
+  const int64_t per = (n + SCAN_T - 1) / SCAN_T;
+  const int64_t b0 = threadIdx.x * per;
+  double s = 0.0;
+  for (int64_t k = 0; k < per; ++k)
+    if (b0 + k < n) s += sums[b0 + k];
+  double tot;
+  double off = block_exclusive_scan(s, sh, tot);
+  for (int64_t k = 0; k < per; ++k) {
+    if (b0 + k < n) {
+      double v = sums[b0 + k];
+      sums[b0 + k] = off;
+      off += v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(SCAN_T) void scan_apply(
+    const double* __restrict__ in, int64_t N, const double* __restrict__ sums,
+    double* __restrict__ out) {
+  __shared__ double sh[SCAN_T];
+  const int64_t base = (int64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_I;
+  double v[SCAN_I];
+  double s = 0.0;
+  for (int k = 0; k < SCAN_I; ++k) {
+    v[k] = (base + k < N) ? in[base + k] : 0.0;
+    s += v[k];
+  }
+  double tot;
+  double run = block_exclusive_scan(s, sh, tot) + sums[blockIdx.x];
+  for (int k = 0; k < SCAN_I; ++k) {
+    run += v[k];
+    if (base + k < N) out[base + k] = run;
+  }
+}
+
+__global__ void gather_rows_kernel(const double* __restrict__ in,
+                                   const int64_t* __restrict__ idx, int64_t n,
+                                   int cols, double* __restrict__ out) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * cols) return;
+  int64_t i = e / cols;
+  int c = (int)(e % cols);
+  out[e] = in[idx[i] * cols + c];
+}
+
+__global__ void importance_weights_kernel(const double* __restrict__ lp,
+                                          const double* __restrict__ lt,
+                                          int64_t A, double scale,
+                                          double* __restrict__ w) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < A) w[i] = exp(lp[i] - lt[i]) * scale;
+}
+
+}  // namespace
+}  // namespace abc
+
+using namespace abc;
+
+extern "C" size_t abc_weighted_moments_workspace(int64_t N, int d) {
+  (void)N;
+  size_t off = 0;
+  size_only<double>(off, (size_t)MOM_BLOCKS * (2 + d));
+  size_only<double>(off, (size_t)MOM_BLOCKS * d * d);
+  return off + 256;
+}
+
+extern "C" int abc_weighted_moments(const double* X, const double* w,
+                                    int64_t N, int d, double* out, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  ABC_CHECK_ARG(N >= 1 && d >= 1 && d <= 64, "moments: bad N=%lld d=%d", (long long)N, d);
+  ABC_CHECK_ARG(X && w && out && ws, "moments: null pointer");
+  if (ws_bytes < abc_weighted_moments_workspace(N, d))
+    return set_error(ABC_ERR_WORKSPACE, "moments: workspace too small");
+  Carver cv(ws, ws_bytes);
+  double* p1 = cv.take<double>((size_t)MOM_BLOCKS * (2 + d));
+  double* p2 = cv.take<double>((size_t)MOM_BLOCKS * d * d);
+  hipStream_t s = as_stream(stream);
+  const int nblk = (int)(ceil_div(N, MOM_ROWS) < MOM_BLOCKS ? ceil_div(N, MOM_ROWS) : MOM_BLOCKS);
+  const size_t lds = sizeof(double) * (MOM_ROWS * d + MOM_ROWS);
+  hipLaunchKernelGGL(moments1_kernel, dim3(nblk), dim3(256), lds, s, X, w, N, d, p1);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(moments1_final, dim3(1), dim3(256), 0, s, p1, nblk, d, out);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(moments2_kernel, dim3(nblk), dim3(256), lds, s, X, w, N, d, out, p2);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(moments2_final, dim3(1), dim3(256), 0, s, p2, nblk, d, out);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
+extern "C" size_t abc_scan_workspace(int64_t N) {
+  return align_up(sizeof(double) * (size_t)(ceil_div(N > 0 ? N : 1, SCAN_TILE)), 256) + 256;
+}
+
+extern "C" int abc_inclusive_scan_f64(const double* in, double* out, int64_t N,
+                                      void* ws, size_t ws_bytes, void* stream) {
+  ABC_CHECK_ARG(N >= 0, "scan: N < 0");
+  if (N == 0) return ABC_OK;
+  ABC_CHECK_ARG(in && out && ws, "scan: null pointer");
+  if (ws_bytes < abc_scan_workspace(N))
+    return set_error(ABC_ERR_WORKSPACE, "scan: workspace too small");
+  const int64_t ntile = ceil_div(N, SCAN_TILE);
+  double* sums = static_cast<double*>(ws);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(scan_tile_sums, dim3((unsigned)ntile), dim3(SCAN_T), 0, s, in, N, sums);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(scan_sums, dim3(1), dim3(SCAN_T), 0, s, sums, ntile);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(scan_apply, dim3((unsigned)ntile), dim3(SCAN_T), 0, s, in, N, sums, out);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
+extern "C" int abc_gather_rows(const double* in, const int64_t* idx, int64_t n,
+                               int cols, double* out, void* stream) {
+  ABC_CHECK_ARG(n >= 0 && cols >= 1, "gather: bad n/cols");
+  if (n == 0) return ABC_OK;
+  ABC_CHECK_ARG(in && idx && out, "gather: null pointer");
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)ceil_div(n * cols, 256)), dim3(256),
+                     0, as_stream(stream), in, idx, n, cols, out);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
+extern "C" int abc_importance_weights(const double* prior_logpdf,
+                                      const double* trans_logpdf, int64_t A,
+                                      double scale, double* w, void* stream) {
+  ABC_CHECK_ARG(A >= 0, "weights: A < 0");
+  if (A == 0) return ABC_OK;
+  ABC_CHECK_ARG(prior_logpdf && trans_logpdf && w, "weights: null pointer");
+  hipLaunchKernelGGL(importance_weights_kernel, dim3((unsigned)ceil_div(A, 256)), dim3(256),
+                     0, as_stream(stream), prior_logpdf, trans_logpdf, A, scale, w);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}

@@ -1,0 +1,277 @@
+"""Torch-plumbing wrappers over the libabcgpu C ABI.
+
+PyTorch is used only to own device memory and to name the HIP stream; every
+computation below is a hand-written HIP kernel reached through
+``pyabc_amd._native``.  All tensors are float64 / int64 on the current
+device unless stated.
+"""
+import math
+
+import numpy as np
+
+from . import _native as nat
+
+try:
+    import torch
+except ImportError:  # pragma: no cover - torch is part of the image
+    torch = None
+
+F64 = None if torch is None else torch.float64
+I64 = None if torch is None else torch.int64
+
+
+class NoDeviceError(RuntimeError):
+    pass
+
+
+def require_device():
+    """The GPU path needs a HIP device and the native library: fail loudly."""
+    if torch is None or not torch.cuda.is_available():
+        raise NoDeviceError("pyabc_amd GPU path needs an MI355X (HIP device)")
+    nat.load()
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_ptr():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def p(t):
+    """Raw device pointer of a contiguous tensor (or None)."""
+    if t is None:
+        return None
+    assert t.is_contiguous(), "kernels take contiguous tensors"
+    return t.data_ptr()
+
+
+_ws = {}
+
+
+def workspace(nbytes, slot="main"):
+    """A cached device scratch buffer of at least nbytes (per device/slot)."""
+    dev = torch.cuda.current_device()
+    key = (dev, slot)
+    buf = _ws.get(key)
+    nbytes = max(int(nbytes), 256)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(int(nbytes * 1.25) + 256, dtype=torch.uint8,
+                          device=f"cuda:{dev}")
+        _ws[key] = buf
+    return buf
+
+
+def as_dev(a, dtype=None, device=None):
+    """numpy / list / tensor -> contiguous device tensor."""
+    dtype = dtype or F64
+    device = device or require_device()
+    if isinstance(a, torch.Tensor):
+        return a.to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype,
+                           device=device).contiguous()
+
+
+# ---- reductions -----------------------------------------------------------
+
+def weighted_moments(X, w):
+    """(sum w, sum w^2, mean [d], cov_biased [d, d]) as float64 numpy."""
+    N, d = X.shape
+    out = torch.empty(2 + d + d * d, dtype=F64, device=X.device)
+    nb = nat.query("abc_weighted_moments_workspace", N, d)
+    ws = workspace(nb)
+    nat.call("abc_weighted_moments", p(X), p(w), N, d, p(out), p(ws), ws.numel(),
+             stream_ptr())
+    o = out.cpu().numpy()
+    return o[0], o[1], o[2:2 + d].copy(), o[2 + d:].reshape(d, d).copy()
+
+
+def inclusive_scan(x, out=None):
+    n = x.numel()
+    out = torch.empty_like(x) if out is None else out
+    nb = nat.query("abc_scan_workspace", n)
+    ws = workspace(nb, "scan")
+    nat.call("abc_inclusive_scan_f64", p(x), p(out), n, p(ws), ws.numel(),
+             stream_ptr())
+    return out
+
+
+# ---- MultivariateNormalTransition -----------------------------------------
+
+def mvn_pack(X, w, mu, U, shift, prec):
+    N, d = X.shape
+    r = U.shape[1]
+    nb = nat.query("abc_mvn_packed_bytes", N, r, prec)
+    packed = torch.empty(nb, dtype=torch.uint8, device=X.device)
+    nat.call("abc_mvn_pack_population", p(X), p(w), N, d, p(mu), p(U), r,
+             float(shift), prec, p(packed), stream_ptr())
+    return packed
+
+
+def mvn_logpdf(x, packed, N, mu, U, prec, log_const, out=None):
+    M, d = x.shape
+    r = U.shape[1]
+    out = torch.empty(M, dtype=F64, device=x.device) if out is None else out
+    if M == 0:
+        return out
+    nb = nat.query("abc_mvn_logpdf_workspace", M, N, r, prec)
+    ws = workspace(nb, "mvn")
+    nat.call("abc_mvn_logpdf", p(x), M, d, p(packed), N, p(mu), p(U), r, prec,
+             float(log_const), p(out), p(ws), ws.numel(), stream_ptr())
+    return out
+
+
+def mvn_logpdf_direct(x, X, w, U, V, support_tol, log_const, out=None):
+    M, d = x.shape
+    N = X.shape[0]
+    r = 0 if U is None else U.shape[1]
+    nv = 0 if V is None else V.shape[1]
+    out = torch.empty(M, dtype=F64, device=x.device) if out is None else out
+    if M == 0:
+        return out
+    nat.call("abc_mvn_logpdf_direct", p(x), M, p(X), p(w), N, d,
+             p(U) if r else None, r, p(V) if nv else None, nv,
+             float(support_tol), float(log_const), p(out), stream_ptr())
+    return out
+
+
+# ---- proposal / prior / simulator / distance / acceptance ----------------
+
+def propose(X, cdf, L, prior_kind, prior_params, seed, generation, idx0, B,
+            max_attempts, d, per_particle_L=False):
+    dev = prior_params.device
+    theta = torch.empty((B, d), dtype=F64, device=dev)
+    lp = torch.empty(B, dtype=F64, device=dev)
+    anc = torch.empty(B, dtype=I64, device=dev)
+    att = torch.empty(B, dtype=torch.int32, device=dev)
+    N = 0 if X is None else X.shape[0]
+    fn = "abc_local_propose" if per_particle_L else "abc_propose"
+    nat.call(fn, p(X), p(cdf), N, d, p(L), p(prior_kind), p(prior_params),
+             int(seed) & (2 ** 64 - 1), int(generation) & 0xFFFFFFFF, int(idx0),
+             int(B), int(max_attempts), p(theta), p(lp), p(anc), p(att),
+             stream_ptr())
+    return theta, lp, anc, att
+
+
+def prior_logpdf(theta, prior_kind, prior_params, out=None):
+    B, d = theta.shape
+    out = torch.empty(B, dtype=F64, device=theta.device) if out is None else out
+    nat.call("abc_prior_logpdf", p(theta), B, d, p(prior_kind), p(prior_params),
+             p(out), stream_ptr())
+    return out
+
+
+def simulate_linear_gaussian(theta, src, a, sigma, seed, generation, idx0,
+                             out=None):
+    B, d = theta.shape
+    S = src.numel()
+    out = torch.empty((B, S), dtype=F64, device=theta.device) if out is None else out
+    nat.call("abc_simulate_linear_gaussian", p(theta), B, d, S, p(src), p(a),
+             p(sigma), int(seed) & (2 ** 64 - 1), int(generation) & 0xFFFFFFFF,
+             int(idx0), p(out), stream_ptr())
+    return out
+
+
+def pnorm(x, x0, wf, pval, out=None):
+    B, S = x.shape
+    out = torch.empty(B, dtype=F64, device=x.device) if out is None else out
+    nat.call("abc_pnorm", p(x), B, S, p(x0), p(wf), float(pval), p(out),
+             stream_ptr())
+    return out
+
+
+def accept_compact(d, eps, idx_out=None, count_out=None):
+    B = d.numel()
+    idx = torch.empty(max(B, 1), dtype=I64, device=d.device) if idx_out is None else idx_out
+    cnt = torch.empty(1, dtype=I64, device=d.device) if count_out is None else count_out
+    nb = nat.query("abc_compact_workspace", B)
+    ws = workspace(nb, "compact")
+    nat.call("abc_accept_compact", p(d), B, float(eps), p(idx), p(cnt), p(ws),
+             ws.numel(), stream_ptr())
+    return idx, cnt
+
+
+def gather_rows(x, idx, n=None):
+    n = idx.numel() if n is None else n
+    cols = 1 if x.dim() == 1 else x.shape[1]
+    out = torch.empty((n, cols) if x.dim() > 1 else (n,), dtype=F64,
+                      device=x.device)
+    nat.call("abc_gather_rows", p(x), p(idx), n, cols, p(out), stream_ptr())
+    return out
+
+
+def importance_weights(prior_lp, trans_lp, scale=1.0):
+    A = prior_lp.numel()
+    w = torch.empty(A, dtype=F64, device=prior_lp.device)
+    nat.call("abc_importance_weights", p(prior_lp), p(trans_lp), A,
+             float(scale), p(w), stream_ptr())
+    return w
+
+
+# ---- sort / quantile / column statistics ---------------------------------
+
+def sort_pairs(keys, vals):
+    N = keys.numel()
+    ko = torch.empty_like(keys)
+    vo = torch.empty_like(vals)
+    nb = nat.query("abc_sort_pairs_workspace", N)
+    ws = workspace(nb, "sort")
+    nat.call("abc_sort_pairs_f64", p(keys), p(vals), N, p(ko), p(vo), p(ws),
+             ws.numel(), stream_ptr())
+    return ko, vo
+
+
+def weighted_quantile(points, w, alpha):
+    N = points.numel()
+    q = torch.empty(1, dtype=F64, device=points.device)
+    nb = nat.query("abc_weighted_quantile_workspace", N)
+    ws = workspace(nb, "sort")
+    nat.call("abc_weighted_quantile", p(points), p(w), N, float(alpha), p(q),
+             p(ws), ws.numel(), stream_ptr())
+    return q
+
+
+def column_std(X):
+    R, S = X.shape
+    out = torch.empty(S, dtype=F64, device=X.device)
+    nb = nat.query("abc_column_stats_workspace", R, S)
+    ws = workspace(nb, "colstats")
+    nat.call("abc_column_std", p(X), R, S, p(out), p(ws), ws.numel(), stream_ptr())
+    return out
+
+
+def column_mad(X):
+    R, S = X.shape
+    out = torch.empty(S, dtype=F64, device=X.device)
+    nb = nat.query("abc_column_stats_workspace", R, S)
+    ws = workspace(nb, "colstats")
+    nat.call("abc_column_mad", p(X), R, S, p(out), p(ws), ws.numel(), stream_ptr())
+    return out
+
+
+# ---- LocalTransition -------------------------------------------------------
+
+def local_fit(X, w, k, scaling, eps):
+    N, d = X.shape
+    dev = X.device
+    covs = torch.empty((N, d, d), dtype=F64, device=dev)
+    inv = torch.empty_like(covs)
+    chol = torch.empty_like(covs)
+    dets = torch.empty(N, dtype=F64, device=dev)
+    lnorm = torch.empty(N, dtype=F64, device=dev)
+    nat.call("abc_local_fit", p(X), p(w), N, d, int(k), float(scaling),
+             float(eps), p(covs), p(inv), p(dets), p(chol), p(lnorm), None, 0,
+             stream_ptr())
+    return covs, inv, dets, chol, lnorm
+
+
+def local_logpdf(x, X, w, inv, lnorm, out=None):
+    M, d = x.shape
+    N = X.shape[0]
+    out = torch.empty(M, dtype=F64, device=x.device) if out is None else out
+    if M == 0:
+        return out
+    nat.call("abc_local_logpdf", p(x), M, p(X), p(w), N, d, p(inv), p(lnorm),
+             p(out), stream_ptr())
+    return out
+
+
+LOG_2PI = math.log(2 * math.pi)

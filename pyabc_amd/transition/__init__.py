@@ -1,0 +1,11 @@
+"""Transitions (pyabc/transition/__init__.py): GPU-backed perturbation
+kernels behind the reference's Transition API."""
+from .base import Transition, DiscreteTransition
+from .exceptions import NotEnoughParticles
+from .multivariatenormal import (MultivariateNormalTransition,
+                                 silverman_rule_of_thumb, scott_rule_of_thumb)
+from .local_transition import LocalTransition
+
+__all__ = ["Transition", "DiscreteTransition", "NotEnoughParticles",
+           "MultivariateNormalTransition", "LocalTransition",
+           "silverman_rule_of_thumb", "scott_rule_of_thumb"]

@@ -1,0 +1,43 @@
+"""The C ABI library loads and exports every symbol include/abcgpu.h declares
+(no compute calls: this runs on the CPU-only build host)."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "abcgpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(abc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_matches_binding_table():
+    from pyabc_amd import _native
+    assert sorted(_native.SIGNATURES) == declared_symbols()
+
+
+def test_library_exports_all_symbols():
+    from pyabc_amd import _native
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    _native.load()
+    assert _native.load().abc_version() == 1
+
+
+def test_size_queries_are_pure_host():
+    from pyabc_amd import _native as nat
+    assert nat.query("abc_mvn_packed_bytes", 1000, 10, nat.ABC_PREC_F64) == \
+        63 * 64 * 3 * 8
+    assert nat.query("abc_mvn_logpdf_workspace", 4096, 4096, 10, 0) > 0
+    assert nat.query("abc_sort_pairs_workspace", 10 ** 6) > 32 * 10 ** 6
+
+
+def test_invalid_arguments_raise_without_device():
+    import pytest
+    from pyabc_amd import _native as nat
+    with pytest.raises(ValueError):
+        nat.call("abc_pnorm", None, 10, 0, None, None, 2.0, None, None)
+    assert "pnorm" in nat.load().abc_last_error().decode()

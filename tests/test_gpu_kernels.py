@@ -1,0 +1,298 @@
+"""GPU parity: every kernel, through the C ABI, against the CPU oracle and the
+reference golden vectors (tests/golden).  Tolerances are stated per test:
+integer / index / accept-mask work is exact; fp64 arithmetic 1e-10..1e-12;
+the transition density 2e-6 relative in the f64-MFMA mode (exp2 of the
+shifted exponent is fp32) and 1e-4 in the f32-MFMA fast mode.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import oracle.sampler as osamp
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from pyabc_amd import gpu
+    return gpu.require_device()
+
+
+def g(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def T(a, dtype=None):
+    from pyabc_amd import gpu
+    return gpu.as_dev(a, dtype=dtype)
+
+
+MVN = ["d1_n1000", "d2_n500", "d10_n4096", "d3_unnorm_scaled"]
+
+
+@pytest.mark.parametrize("tag", MVN)
+@pytest.mark.parametrize("precision,rtol", [("f64", 2e-6), ("f32", 1e-4)])
+def test_mvn_pdf_golden(dev, tag, precision, rtol):
+    import pandas as pd
+    from pyabc_amd.transition import MultivariateNormalTransition
+    gg = g(f"mvn_{tag}.npz")
+    d = gg["X"].shape[1]
+    cols = [f"p{k:02d}" for k in range(d)]
+    t = MultivariateNormalTransition(scaling=float(gg["scaling"]),
+                                     precision=precision)
+    w = gg["w"].copy()
+    t.fit(pd.DataFrame(gg["X"], columns=cols), w)
+    np.testing.assert_allclose(w, gg["w_fit"], rtol=1e-13)
+    np.testing.assert_allclose(t.cov, gg["cov"], rtol=1e-10, atol=1e-14)
+    assert t._mfma
+    pdf = t.pdf(pd.DataFrame(gg["x"], columns=cols))
+    np.testing.assert_allclose(pdf, gg["pdf"], rtol=rtol, atol=0)
+
+
+@pytest.mark.parametrize("tag", ["singular", "n1"])
+def test_mvn_pdf_direct_golden(dev, tag):
+    import pandas as pd
+    from pyabc_amd.transition import MultivariateNormalTransition
+    gg = g(f"mvn_{tag}.npz")
+    d = gg["X"].shape[1]
+    cols = [f"p{k:02d}" for k in range(d)]
+    t = MultivariateNormalTransition()
+    t.fit(pd.DataFrame(gg["X"], columns=cols), gg["w"].copy())
+    np.testing.assert_allclose(t.cov, gg["cov"], rtol=1e-10, atol=1e-14)
+    pdf = np.atleast_1d(t.pdf(pd.DataFrame(gg["x"], columns=cols)))
+    # singular -> direct fp64 kernel (1e-10); n1 is full rank -> f64 MFMA
+    np.testing.assert_allclose(pdf, gg["pdf"], rtol=2e-6 if t._mfma else 1e-10,
+                               atol=1e-300)
+    if tag == "singular":
+        assert not t._mfma
+        assert (pdf[::4] == 0).all() and (pdf[1::4] > 0).all()
+
+
+def test_mvn_pdf_large_vs_oracle(dev):
+    """N = 1e5, d = 10 (the c2 shape): subset of candidates vs the oracle."""
+    import pandas as pd
+    from pyabc_amd.transition import MultivariateNormalTransition
+    rng = np.random.default_rng(5)
+    N, d = 100_000, 10
+    X = 0.8 + np.sqrt(0.2) * rng.standard_normal((N, d))
+    w = np.exp(0.5 * rng.standard_normal(N))
+    w /= w.sum()
+    cols = [f"p{k}" for k in range(d)]
+    t = MultivariateNormalTransition()
+    t.fit(pd.DataFrame(X, columns=cols), w.copy())
+    cand = t.rvs(4096).values
+    ref = oracle.mvn_logpdf(cand[:200], X, w, t.cov)
+    lp = t.logpdf_device(T(cand)).cpu().numpy()
+    np.testing.assert_allclose(np.exp(lp[:200] - ref), 1.0, rtol=2e-6)
+    t32 = MultivariateNormalTransition(precision="f32")
+    t32.fit(pd.DataFrame(X, columns=cols), w.copy())
+    lp32 = t32.logpdf_device(T(cand)).cpu().numpy()
+    np.testing.assert_allclose(np.exp(lp32 - lp), 1.0, rtol=1e-4)
+
+
+@pytest.mark.parametrize("tag,kw", [("k50", dict(k=50, k_fraction=None)),
+                                    ("default", dict())])
+def test_local_golden(dev, tag, kw):
+    import pandas as pd
+    from pyabc_amd.transition import LocalTransition
+    gg = g(f"local_{tag}.npz")
+    d = gg["X"].shape[1]
+    cols = [f"p{k:02d}" for k in range(d)]
+    t = LocalTransition(**kw)
+    t.fit(pd.DataFrame(gg["X"], columns=cols), gg["w"].copy())
+    assert t.k == int(gg["k"])
+    np.testing.assert_allclose(t.covs, gg["covs"], rtol=1e-9, atol=1e-13)
+    np.testing.assert_allclose(t.determinants, gg["dets"], rtol=1e-8)
+    np.testing.assert_allclose(t.inv_covs, gg["inv_covs"], rtol=1e-8, atol=1e-10)
+    pdf = t.pdf(pd.DataFrame(gg["x"], columns=cols))
+    np.testing.assert_allclose(pdf, gg["pdf"], rtol=1e-9)
+
+
+def test_pnorm_golden(dev):
+    from pyabc_amd import gpu
+    gg = g("pnorm.npz")
+    for c in sorted({k.split("__")[0] for k in gg.files}):
+        wf = gg[c + "__w"] * gg[c + "__f"]
+        dd = gpu.pnorm(T(gg[c + "__x"]), T(gg[c + "__x0"]), T(wf),
+                       float(gg[c + "__p"])).cpu().numpy()
+        np.testing.assert_allclose(dd, gg[c + "__d"], rtol=1e-12, err_msg=c)
+
+
+def test_weighted_quantile_golden(dev):
+    from pyabc_amd import gpu
+    gg = g("quantile.npz")
+    for name in ("n10k", "ties", "zerow", "n1"):
+        pts, w = gg[f"{name}__points"], gg[f"{name}__w"]
+        for a in (0.2, 0.5, 0.9, 1.0):
+            q = float(gpu.weighted_quantile(T(pts), T(w), a).cpu())
+            ref = oracle.weighted_quantile(pts, w, a, kind="stable")
+            assert q == pytest.approx(ref, rel=1e-12, abs=1e-15), (name, a)
+            if name != "ties":
+                assert q == pytest.approx(float(gg[f"{name}__a{a}__q"]),
+                                          rel=1e-12), (name, a)
+
+
+def test_sort_pairs(dev):
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(1)
+    for n in (1, 7, 2048, 2049, 100_003):
+        k = rng.standard_normal(n) * 10 ** rng.uniform(-5, 5, n)
+        k[::13] = 0.0
+        k[::17] = -0.0 if n > 17 else k[::17]
+        k[1::7] = k[::7][:len(k[1::7])]        # ties
+        v = np.arange(n, dtype=np.float64)
+        ko, vo = gpu.sort_pairs(T(k), T(v))
+        order = np.argsort(k, kind="stable")
+        np.testing.assert_array_equal(ko.cpu().numpy(), k[order])
+        np.testing.assert_array_equal(vo.cpu().numpy(), v[order])
+
+
+def test_column_stats_golden(dev):
+    from pyabc_amd import gpu
+    gg = g("adaptive.npz")
+    for R in (101, 100):
+        data = gg[f"R{R}_std_rNone__data"]
+        sd = gpu.column_std(T(data)).cpu().numpy()
+        np.testing.assert_allclose(sd, oracle.standard_deviation(data),
+                                   rtol=1e-12, atol=1e-15)
+        mad = gpu.column_mad(T(data)).cpu().numpy()
+        np.testing.assert_array_equal(mad, oracle.median_absolute_deviation(data))
+
+
+def test_column_mad_large(dev):
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(2)
+    for R, S in ((4097, 3), (20000, 256)):
+        X = rng.standard_normal((R, S)) * 10 ** rng.uniform(-2, 2, S)
+        X[:, 0] = np.round(X[:, 0])
+        mad = gpu.column_mad(T(X)).cpu().numpy()
+        np.testing.assert_array_equal(mad, oracle.median_absolute_deviation(X))
+
+
+def test_weighted_moments(dev):
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((10_001, 7)) + 5
+    w = rng.uniform(size=10_001)
+    sw, sw2, mean, cov_b = gpu.weighted_moments(T(X), T(w))
+    assert sw == pytest.approx(w.sum(), rel=1e-13)
+    assert sw2 == pytest.approx((w ** 2).sum(), rel=1e-13)
+    np.testing.assert_allclose(mean, w @ X / w.sum(), rtol=1e-13)
+    wn = w / w.sum()
+    cov_ref = np.cov(X, aweights=w, rowvar=False)
+    np.testing.assert_allclose(cov_b * sw / (sw - sw2 / sw), cov_ref, rtol=1e-11)
+
+
+def test_scan(dev):
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(4)
+    for n in (1, 5, 2048, 2049, 1_000_001):
+        x = rng.uniform(size=n)
+        c = gpu.inclusive_scan(T(x)).cpu().numpy()
+        np.testing.assert_allclose(c, np.cumsum(x), rtol=1e-12)
+
+
+def test_propose_replay(dev):
+    """Philox draws bit-compatible with the oracle replay; prior re-draws."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(6)
+    N, d = 1000, 3
+    X = rng.standard_normal((N, d))
+    w = rng.uniform(size=N)
+    w /= w.sum()
+    L = np.linalg.cholesky(np.array([[1, .3, 0], [.3, 1, .2], [0, .2, .5]])) * .4
+    kinds = ["uniform", "norm", "expon"]
+    params = np.array([[-1.0, 2.0, 0, 0], [0.0, 1.0, 0, 0], [-0.5, 1.0, 0, 0]])
+    ref = osamp.propose_mvn(X, w, L, 123, 4, 1000, 5000, kinds, params)
+    th, lp, anc, att = gpu.propose(
+        T(X), gpu.inclusive_scan(T(w)), T(L),
+        T([osamp.KIND[k] for k in kinds], dtype=torch.int32), T(params.ravel()),
+        123, 4, 1000, 5000, 1000, d)
+    np.testing.assert_array_equal(anc.cpu().numpy(), ref[2])
+    np.testing.assert_array_equal(att.cpu().numpy(), ref[3])
+    np.testing.assert_allclose(th.cpu().numpy(), ref[0], rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(lp.cpu().numpy(), ref[1], rtol=1e-12)
+    assert (att.cpu().numpy() > 1).any()     # re-draws happened
+
+
+def test_prior_sampling_moments(dev):
+    """t = 0 draws from the prior itself: moments of every supported kind."""
+    from pyabc_amd import gpu
+    from scipy import stats
+    kinds = ["norm", "uniform", "expon", "laplace", "lognorm", "gamma", "beta"]
+    params = np.array([[1, 2, 0, 0], [-1, 3, 0, 0], [0.5, 2, 0, 0],
+                       [0, 1, 0, 0], [0.5, 0, 1, 0], [2.5, 0, 1, 0],
+                       [2, 3, 0, 1]], dtype=float)
+    B = 200_000
+    th, lp, _, att = gpu.propose(None, None, None,
+                                 T([osamp.KIND[k] for k in kinds], dtype=torch.int32),
+                                 T(params.ravel()), 9, 0, 0, B, 10, len(kinds))
+    th = th.cpu().numpy()
+    dists = [stats.norm(1, 2), stats.uniform(-1, 3), stats.expon(0.5, 2),
+             stats.laplace(0, 1), stats.lognorm(0.5, 0, 1), stats.gamma(2.5, 0, 1),
+             stats.beta(2, 3, 0, 1)]
+    for k, dist in enumerate(dists):
+        ks = stats.kstest(th[:, k], dist.cdf).statistic
+        assert ks < 0.01, (kinds[k], ks)
+    ref_lp = osamp.prior_logpdf(th[:1000], kinds, params)
+    np.testing.assert_allclose(lp.cpu().numpy()[:1000], ref_lp, rtol=1e-10)
+
+
+def test_simulate_replay(dev):
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(7)
+    th = rng.standard_normal((777, 4))
+    S = 13
+    src = np.arange(S) % 4
+    a = rng.uniform(0.5, 2, S)
+    sig = 10 ** rng.uniform(-2, 2, S)
+    x = gpu.simulate_linear_gaussian(T(th), T(src, dtype=torch.int32), T(a), T(sig),
+                                     55, 3, 10).cpu().numpy()
+    ref = osamp.simulate_linear_gaussian(th, src, a, sig, 55, 3, 10)
+    np.testing.assert_allclose(x, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_accept_compact(dev):
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(8)
+    for B in (1, 100, 2048, 2049, 300_001):
+        dd = rng.uniform(size=B)
+        eps = 0.37
+        idx, cnt = gpu.accept_compact(T(dd), eps)
+        n = int(cnt.cpu())
+        ref = np.nonzero(dd <= eps)[0]
+        assert n == len(ref)
+        np.testing.assert_array_equal(idx.cpu().numpy()[:n], ref)
+
+
+def test_step_golden(dev):
+    """Fixed-input generation step (tests/golden/step.npz): distances,
+    accept mask and importance weights against the reference."""
+    import pandas as pd
+    from pyabc_amd import gpu
+    from pyabc_amd.transition import MultivariateNormalTransition
+    gg = g("step.npz")
+    d = gg["X"].shape[1]
+    cols = [f"p{k:02d}" for k in range(d)]
+    t = MultivariateNormalTransition()
+    t.fit(pd.DataFrame(gg["X"], columns=cols), gg["w"].copy())
+    dd = gpu.pnorm(T(gg["xsim"]), T(gg["x0"]), T(np.ones(d)), 2.0)
+    np.testing.assert_allclose(dd.cpu().numpy(), gg["d"], rtol=1e-13)
+    idx, cnt = gpu.accept_compact(dd, float(gg["eps"]))
+    n = int(cnt.cpu())
+    acc = np.zeros(len(gg["d"]), bool)
+    acc[idx.cpu().numpy()[:n]] = True
+    np.testing.assert_array_equal(acc, gg["accept"])
+    theta = T(gg["theta"])
+    kind = T([0] * d, dtype=torch.int32)
+    params = T(np.tile([0.0, 1.0, 0, 0], d))
+    lp = gpu.prior_logpdf(theta, kind, params)
+    lt = t.logpdf_device(theta)
+    wts = gpu.importance_weights(lp, lt).cpu().numpy()
+    np.testing.assert_allclose(wts[acc], gg["weight"][acc], rtol=2e-6)
