@@ -70,6 +70,14 @@ size_t abc_scan_workspace(int64_t N);
 int abc_inclusive_scan_f64(const double* in, double* out, int64_t N, void* ws,
                            size_t ws_bytes, void* stream);
 
+/* Population._normalize_weights (pyabc/population.py:123-145, one model) and
+ * effective_sample_size (pyabc/weighted_statistics.py:73-83): w /= sum w in
+ * place; stats[0] = sum w (before), stats[1] = ESS = (sum w)^2 / sum w^2,
+ * stats[2] = sum w^2 (before). */
+size_t abc_normalize_weights_workspace(int64_t N);
+int abc_normalize_weights(double* w, int64_t N, double* stats, void* ws,
+                          size_t ws_bytes, void* stream);
+
 /* ---- MultivariateNormalTransition.pdf (multivariatenormal.py:99-113) -----
  * density(x_i) = sum_j w_j N(x_i - X_j; 0, Sigma).  Host supplies the fp64
  * eigen-whitening of Sigma (scipy _PSD semantics): U [d x r], mean mu [d].
@@ -120,7 +128,8 @@ int abc_prior_logpdf(const double* theta, int64_t B, int d,
 
 /* ---- vectorised synthetic simulator (the Model.sample boundary,
  * pyabc/model.py:89-116): x[b,k] = a[k] * theta[b, src[k]] + sigma[k] * e,
- * e ~ N(0,1) from Philox slot 0x40000000 + k/2 of candidate idx0+b. */
+ * e ~ N(0,1): normal k of candidate idx0+b's stream (Philox slot
+ * 0x40000000 + k/4, four Box-Muller normals per slot). */
 int abc_simulate_linear_gaussian(const double* theta, int64_t B, int d, int S,
                                  const int32_t* src, const double* a,
                                  const double* sigma, uint64_t seed,

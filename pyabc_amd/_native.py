@@ -27,6 +27,8 @@ SIGNATURES = {
     "abc_weighted_moments": (I32, [P, P, I64, I32, P, P, SZ, P]),
     "abc_scan_workspace": (SZ, [I64]),
     "abc_inclusive_scan_f64": (I32, [P, P, I64, P, SZ, P]),
+    "abc_normalize_weights_workspace": (SZ, [I64]),
+    "abc_normalize_weights": (I32, [P, I64, P, P, SZ, P]),
     "abc_mvn_packed_bytes": (SZ, [I64, I32, I32]),
     "abc_mvn_pack_population": (I32, [P, P, I64, I32, P, P, I32, D, I32, P, P]),
     "abc_mvn_logpdf_workspace": (SZ, [I64, I64, I32, I32]),

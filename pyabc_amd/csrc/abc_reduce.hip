@@ -199,6 +199,42 @@ __global__ void importance_weights_kernel(const double* __restrict__ lp,
   if (i < A) w[i] = exp(lp[i] - lt[i]) * scale;
 }
 
+
+// ---- Population._normalize_weights + effective_sample_size ---------------
+constexpr int NW_BLOCKS = 256;
+__global__ __launch_bounds__(256) void wsum_kernel(const double* __restrict__ w,
+                                                   int64_t N,
+                                                   double* __restrict__ part) {
+  double s = 0.0, s2 = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < N;
+       i += (int64_t)gridDim.x * 256) {
+    const double v = w[i];
+    s += v; s2 += v * v;
+  }
+  __shared__ double sh[2][4];
+  s = wave_sum(s); s2 = wave_sum(s2);
+  if ((threadIdx.x & 63) == 0) { sh[0][threadIdx.x >> 6] = s; sh[1][threadIdx.x >> 6] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = ((sh[0][0] + sh[0][1]) + sh[0][2]) + sh[0][3];
+    part[2 * blockIdx.x + 1] = ((sh[1][0] + sh[1][1]) + sh[1][2]) + sh[1][3];
+  }
+}
+__global__ void wsum_final(const double* __restrict__ part, int nblk,
+                           double* __restrict__ stats) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0, s2 = 0.0;
+  for (int b = 0; b < nblk; ++b) { s += part[2 * b]; s2 += part[2 * b + 1]; }
+  stats[0] = s;             // sum w
+  stats[1] = s * s / s2;    // ESS (weighted_statistics.py:73-83)
+  stats[2] = s2;
+}
+__global__ void wscale_kernel(double* __restrict__ w, int64_t N,
+                              const double* __restrict__ stats) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < N) w[i] = w[i] / stats[0];
+}
+
 }  // namespace
 }  // namespace abc
 
@@ -278,6 +314,29 @@ extern "C" int abc_importance_weights(const double* prior_logpdf,
   ABC_CHECK_ARG(prior_logpdf && trans_logpdf && w, "weights: null pointer");
   hipLaunchKernelGGL(importance_weights_kernel, dim3((unsigned)ceil_div(A, 256)), dim3(256),
                      0, as_stream(stream), prior_logpdf, trans_logpdf, A, scale, w);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
+extern "C" size_t abc_normalize_weights_workspace(int64_t N) {
+  (void)N;
+  return sizeof(double) * 2 * NW_BLOCKS + 256;
+}
+
+extern "C" int abc_normalize_weights(double* w, int64_t N, double* stats,
+                                     void* ws, size_t ws_bytes, void* stream) {
+  ABC_CHECK_ARG(N >= 1, "normalize: N < 1");
+  ABC_CHECK_ARG(w && stats && ws, "normalize: null pointer");
+  if (ws_bytes < abc_normalize_weights_workspace(N))
+    return set_error(ABC_ERR_WORKSPACE, "normalize: workspace too small");
+  hipStream_t s = as_stream(stream);
+  const int nblk = (int)(ceil_div(N, 256) < NW_BLOCKS ? ceil_div(N, 256) : NW_BLOCKS);
+  double* part = static_cast<double*>(ws);
+  hipLaunchKernelGGL(wsum_kernel, dim3(nblk), dim3(256), 0, s, w, N, part);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(wsum_final, dim3(1), dim3(64), 0, s, part, nblk, stats);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(wscale_kernel, dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s, w, N, stats);
   ABC_LAUNCHED();
   return ABC_OK;
 }

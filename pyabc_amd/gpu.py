@@ -94,6 +94,17 @@ def inclusive_scan(x, out=None):
     return out
 
 
+def normalize_weights(w):
+    """In-place w /= sum(w); returns device stats [sum, ESS, sum w^2]."""
+    n = w.numel()
+    stats = torch.empty(3, dtype=F64, device=w.device)
+    nb = nat.query("abc_normalize_weights_workspace", n)
+    ws = workspace(nb, "norm")
+    nat.call("abc_normalize_weights", p(w), n, p(stats), p(ws), ws.numel(),
+             stream_ptr())
+    return stats
+
+
 # ---- MultivariateNormalTransition -----------------------------------------
 
 def mvn_pack(X, w, mu, U, shift, prec):

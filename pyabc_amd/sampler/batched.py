@@ -1,0 +1,255 @@
+"""BatchedGPUSampler: one ABC-SMC generation as a few large kernel launches.
+
+Reference loop: pyabc/sampler/singlecore.py:20-38 and
+multicore_evaluation_parallel.py:14-150 call the per-candidate closure
+(smc.py:588-724) until n particles are accepted, keep the first n by
+evaluation id and count every evaluation.  Here a round of B candidates per
+rank runs as
+
+  propose (abc_propose / abc_local_propose, prior re-draw loop inside)
+  -> simulate (VectorizedModel, e.g. abc_simulate_linear_gaussian)
+  -> distance (abc_pnorm) -> accept + order-preserving compaction
+     (abc_accept_compact)
+
+with one host read of the accept count per round.  Once n are accepted the
+importance weights prior / transition (smc.py:768-811) are computed for the
+accepted rows only -- the N_acc x N_pop transition density on MFMA
+(abc_mvn_logpdf) -- and the accepted rows are gathered across ranks.
+
+Semantics vs. the reference: the accepted set is the first n accepted in
+global candidate-index order (deterministic for any rank count), and
+``nr_evaluations_`` = global index of the n-th accepted + 1, i.e. no
+overshoot is counted (the reference's MulticoreEval counts its overshoot,
+multicore_evaluation_parallel.py:138).  Recorded sum stats (record_rejected)
+are all candidates up to that cutoff, in index order (SingleCore semantics).
+"""
+import math
+
+import numpy as np
+
+from .. import gpu
+from ..distance.distance import SumStatMatrix
+from ..population import ColumnarParticles, Particle, Population
+from ..parameters import Parameter
+from . import distributed as dd
+from .base import Sampler
+
+
+class ColumnarSample:
+    """Sample of the batched sampler (device columns, see Sample)."""
+
+    def __init__(self, columns, recorded, recorded_keys, record_rejected, ok,
+                 accepted_flags=None):
+        self._cols = columns
+        self._recorded = recorded            # [R, S] device or None
+        self._recorded_keys = recorded_keys
+        self._accepted_flags = accepted_flags
+        self.record_rejected = record_rejected
+        self.ok = ok
+
+    @property
+    def n_accepted(self):
+        return 0 if self._cols is None else len(self._cols)
+
+    def get_accepted_population(self):
+        return Population.from_columns(self._cols)
+
+    def first_m_sum_stats(self, m):
+        rec = self._recorded
+        if rec is None:
+            return []
+        if m is not None and np.isfinite(m) and m < rec.shape[0]:
+            rec = rec[: int(m)].contiguous()
+        return SumStatMatrix(rec, self._recorded_keys)
+
+    @property
+    def all_sum_stats(self):
+        return self.first_m_sum_stats(np.inf)
+
+    def first_m_particles(self, m):
+        c = self._cols
+        th = c.theta.cpu().numpy()
+        w = c.weights.cpu().numpy()
+        d = c.distances.cpu().numpy()
+        ss = c.sum_stats.cpu().numpy()
+        parts = [Particle(m=c.m, parameter=Parameter(dict(zip(c.param_names, th[i]))),
+                          weight=float(w[i]),
+                          accepted_sum_stats=[dict(zip(c.sum_stat_keys, ss[i]))],
+                          accepted_distances=[float(d[i])])
+                 for i in range(len(c))]
+        m = len(parts) if m is None or not np.isfinite(m) else int(m)
+        return parts[:m]
+
+
+class BatchedGPUSampler(Sampler):
+    """Batched, device-resident sampler (single model, nr_samples_per_param 1).
+
+    Parameters
+    ----------
+    batch_size: candidates per rank and round (None: adapt to the measured
+        acceptance rate).
+    max_batch_size: cap on the adaptive batch.
+    seed: base seed of the counter-based RNG (None: drawn from numpy's global
+        RNG on rank 0 and broadcast).
+    max_attempts: prior re-draws per candidate before giving up
+        (the reference loops forever and warns at 1000, smc.py:658-662).
+    """
+
+    def __init__(self, batch_size=None, max_batch_size=1 << 22, seed=None,
+                 max_attempts=10000):
+        super().__init__()
+        self.batch_size = batch_size
+        self.max_batch_size = max_batch_size
+        self.seed = seed
+        self.max_attempts = max_attempts
+        self._acc_rate = None
+        self.last_stats = {}
+
+    def _base_seed(self, device):
+        if self.seed is None:
+            self.seed = dd.broadcast_int(np.random.randint(0, 2 ** 62), device)
+        return self.seed
+
+    def _round_size(self, needed, ws):
+        if self.batch_size is not None:
+            return int(self.batch_size)
+        rate = self._acc_rate if self._acc_rate else 0.5
+        b = int(math.ceil(needed / max(rate, 1e-4) * 1.15 / ws)) + 256
+        return int(min(max(b, 4096), self.max_batch_size))
+
+    def sample_until_n_accepted(self, n, simulate_one, max_eval=np.inf,
+                                all_accepted=False, show_progress=False):
+        spec = simulate_one
+        if not getattr(spec, "batched_capable", False):
+            raise TypeError(
+                "BatchedGPUSampler needs the GenerationSpec built by "
+                "pyabc_amd.ABCSMC with a VectorizedModel, a device-capable "
+                "prior and transition, and a PNormDistance; got "
+                f"{type(spec).__name__}: {getattr(spec, 'why_not', '')}")
+        dev = gpu.require_device()
+        rank, ws = dd.world()
+        seed = self._base_seed(dev)
+        gen = spec.t & 0xFFFFFFFF
+        record = self.sample_factory.record_rejected
+        d = len(spec.param_names)
+
+        acc_theta, acc_lp, acc_d, acc_x = [], [], [], []
+        rec_x = []
+        n_acc = 0
+        base = 0
+        n_eval = 0
+        ok = True
+        rounds = 0
+        while n_acc < n:
+            if n_eval >= max_eval:
+                ok = False
+                break
+            B = self._round_size(n - n_acc, ws)
+            lo, _ = dd.rank_range(base, B, rank)
+            theta, lp = self._propose(spec, B, seed, gen, lo, d)
+            x = spec.model.simulate_batch(theta, seed, gen, lo)
+            if all_accepted or spec.distance is None:
+                dist = gpu.torch.full((B,), np.inf, dtype=gpu.F64, device=dev)
+                idx = gpu.torch.arange(B, dtype=gpu.I64, device=dev)
+                cnt_local = B
+            else:
+                dist = spec.distance.device_call(x, spec.x0vec, spec.t,
+                                                 spec.sum_stat_keys)
+                idx, cnt = gpu.accept_compact(dist, spec.eps)
+                cnt_local = int(cnt.item())
+            counts = dd.allgather_counts(cnt_local, dev)
+            keep = dd.cutoff(counts, n - n_acc)
+            total_keep = int(keep.sum())
+            k_mine = int(keep[rank])
+            # evaluations up to the cutoff (global order)
+            if n_acc + total_keep >= n:
+                c_rank = int(np.nonzero(keep)[0][-1])
+                pos = self._local_cutoff_pos(idx, keep[c_rank]) if rank == c_rank else -1
+                pos = dd.allgather_counts(pos, dev)[c_rank]
+                evaluated = c_rank * B + pos + 1
+                if rank < c_rank:
+                    rec_rows = B
+                elif rank == c_rank:
+                    rec_rows = pos + 1
+                else:
+                    rec_rows = 0
+            else:
+                evaluated = ws * B
+                rec_rows = B
+            if k_mine:
+                sel = idx[:k_mine]
+                acc_theta.append(gpu.gather_rows(theta, sel))
+                acc_lp.append(gpu.gather_rows(lp, sel))
+                acc_d.append(gpu.gather_rows(dist, sel))
+                acc_x.append(gpu.gather_rows(x, sel))
+            if record:
+                rec_x.append(x[:rec_rows] if (not all_accepted) else x[:rec_rows])
+            n_acc += total_keep
+            n_eval += evaluated
+            base += ws * B
+            rounds += 1
+            tot_cnt = int(counts.sum())
+            self._acc_rate = max(tot_cnt / float(ws * B), 1e-6)
+        self.nr_evaluations_ = int(n_eval)
+        self.last_stats = dict(rounds=rounds, evaluations=int(n_eval),
+                               accepted=int(n_acc))
+        if n_acc < n:
+            ok = False
+        cols = self._assemble(spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
+                              all_accepted)
+        recorded = None
+        if record:
+            recorded = gpu.torch.cat(rec_x, 0) if rec_x else None
+            if ws > 1 and recorded is not None:
+                recorded = dd.allgather_rows(recorded, dev)
+        elif cols is not None:
+            recorded = cols.sum_stats
+        return ColumnarSample(cols, recorded, spec.sum_stat_keys,
+                              record, ok and n_acc == n)
+
+    @staticmethod
+    def _local_cutoff_pos(idx, k):
+        return int(idx[int(k) - 1].item())
+
+    def _propose(self, spec, B, seed, gen, lo, d):
+        if spec.transition is None:
+            th, lp, _, att = gpu.propose(None, None, None, spec.prior_kind,
+                                         spec.prior_params, seed, gen, lo, B,
+                                         self.max_attempts, d)
+        else:
+            th, lp, _, att = spec.transition.propose_device(
+                B, spec.prior_kind, spec.prior_params, seed=seed,
+                generation=gen, idx0=lo, max_attempts=self.max_attempts)
+        return th, lp
+
+    def _assemble(self, spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
+                  all_accepted):
+        rank, ws = dd.world()
+        torch = gpu.torch
+        if acc_theta:
+            theta = torch.cat(acc_theta, 0)
+            lp = torch.cat(acc_lp, 0)
+            dist = torch.cat(acc_d, 0)
+            x = torch.cat(acc_x, 0)
+        else:
+            S = len(spec.sum_stat_keys)
+            theta = torch.empty((0, d), dtype=gpu.F64, device=dev)
+            lp = torch.empty(0, dtype=gpu.F64, device=dev)
+            dist = torch.empty(0, dtype=gpu.F64, device=dev)
+            x = torch.empty((0, S), dtype=gpu.F64, device=dev)
+        # importance weights for this rank's accepted rows (smc.py:768-811)
+        if spec.transition is None or all_accepted:
+            w = torch.ones(theta.shape[0], dtype=gpu.F64, device=dev)
+        else:
+            lt = spec.transition.logpdf_device(theta)
+            w = gpu.importance_weights(lp, lt, spec.weight_scale)
+        if ws > 1:
+            theta = dd.allgather_rows(theta, dev)
+            w = dd.allgather_rows(w, dev)
+            dist = dd.allgather_rows(dist, dev)
+            x = dd.allgather_rows(x, dev)
+        if theta.shape[0] == 0:
+            return None
+        return ColumnarParticles(theta.contiguous(), w.contiguous(),
+                                 dist.contiguous(), x.contiguous(),
+                                 spec.param_names, spec.sum_stat_keys, m=0)

@@ -1,0 +1,544 @@
+"""ABCSMC orchestration (pyabc/smc.py:45-1079), same public API.
+
+The generation loop, calibration, stopping rules and between-generation
+updates follow the reference line for line in behaviour (citations inline).
+What changes is the per-candidate closure: ``_create_simulate_function``
+returns a ``GenerationSpec`` that is still callable per candidate (so the
+reference's sampler contract holds for ``SingleCoreSampler``) but also
+exposes the device pieces -- prior spec, transition, vectorised model,
+distance, epsilon -- that ``BatchedGPUSampler`` runs as batched HIP kernels.
+Populations produced by the batched sampler stay on the GPU; the next fit,
+the adaptive distance update and the epsilon quantile read them in place.
+"""
+import copy
+import datetime
+import logging
+from typing import Callable, List, Union
+
+import numpy as np
+import pandas as pd
+
+from . import gpu
+from .acceptor import Acceptor, SimpleFunctionAcceptor, UniformAcceptor
+from .distance import Distance, PNormDistance, to_distance
+from .epsilon import Epsilon, MedianEpsilon
+from .model import Model, SimpleModel, VectorizedModel
+from .parameters import Parameter
+from .population import Particle, Population
+from .populationstrategy import ConstantPopulationSize, PopulationStrategy
+from .random_variables import RV, Distribution, ModelPerturbationKernel
+from .sampler import BatchedGPUSampler, Sampler, SingleCoreSampler
+from .storage import History
+from .transition import MultivariateNormalTransition, Transition
+from .weighted_statistics import effective_sample_size
+
+logger = logging.getLogger("ABC")
+
+
+def identity(x):
+    return x
+
+
+class GenerationSpec:
+    """Everything one generation needs, per candidate or batched.
+
+    ``__call__`` is the reference closure ``simulate_one`` (smc.py:588-606);
+    the attributes describe the same computation to BatchedGPUSampler.
+    """
+
+    def __init__(self, abc, t, all_accepted=False):
+        self.t = t
+        self.all_accepted = all_accepted
+        self._abc = abc
+        self.param_names = abc.parameter_priors[0].get_parameter_names()
+        self.model = abc.models[0]
+        self.nr_samples_per_parameter = \
+            abc.population_size.nr_samples_per_parameter
+        self.weight_scale = 1.0 / self.nr_samples_per_parameter
+        self.transition = None if (t <= 0 or all_accepted) else abc.transitions[0]
+        self.distance = None if all_accepted else abc.distance_function
+        self.eps = None if all_accepted else abc.eps(t)
+        self.sum_stat_keys = list(abc.x_0.keys())
+        self._closure = None
+        self._init_device(abc)
+
+    def _init_device(self, abc):
+        why = []
+        if len(abc.models) != 1:
+            why.append("more than one model")
+        if not isinstance(self.model, VectorizedModel):
+            why.append("model is not a VectorizedModel")
+        elif list(self.model.sum_stat_keys) != self.sum_stat_keys:
+            why.append("model sum_stat_keys differ from x_0 key order")
+        if abc.summary_statistics is not identity:
+            why.append("custom summary_statistics function")
+        if self.nr_samples_per_parameter != 1:
+            why.append("nr_samples_per_parameter != 1")
+        if not isinstance(abc.acceptor, UniformAcceptor) or \
+                abc.acceptor.use_complete_history:
+            why.append("acceptor is not UniformAcceptor(current time)")
+        if self.distance is not None and not hasattr(self.distance, "device_call"):
+            why.append("distance has no device kernel")
+        if self.transition is not None and not hasattr(self.transition,
+                                                       "propose_device"):
+            why.append("transition has no device kernel")
+        spec = abc.parameter_priors[0].device_spec()
+        if spec is None:
+            why.append("prior component without a device kernel")
+        self.why_not = "; ".join(why)
+        self.batched_capable = not why
+        if self.batched_capable:
+            dev = gpu.require_device()
+            self.prior_kind = gpu.as_dev(spec[0], dtype=gpu.torch.int32, device=dev)
+            self.prior_params = gpu.as_dev(spec[1], device=dev)
+            self.x0vec = gpu.as_dev(np.array([abc.x_0[k] for k in self.sum_stat_keys],
+                                             dtype=np.float64), device=dev)
+
+    def __call__(self):
+        if self._closure is None:
+            if self.all_accepted:
+                self._closure = self._abc._create_simulate_from_prior_function(self.t)
+            else:
+                self._closure = self._abc._create_simulate_function_closure(self.t)
+        return self._closure()
+
+
+class ABCSMC:
+    """Approximate Bayesian Computation - Sequential Monte Carlo
+    (pyabc/smc.py:45-236 for the parameters).  Default sampler here is
+    BatchedGPUSampler when the model is vectorised, else SingleCoreSampler."""
+
+    def __init__(self, models, parameter_priors, distance_function=None,
+                 population_size=100, summary_statistics=identity,
+                 model_prior: RV = None, model_perturbation_kernel=None,
+                 transitions=None, eps: Epsilon = None, sampler: Sampler = None,
+                 acceptor: Acceptor = None,
+                 stop_if_only_single_model_alive: bool = False,
+                 max_nr_recorded_particles: int = np.inf,
+                 show_progress: bool = False):
+        if not isinstance(models, list):
+            models = [models]
+        self.models = list(map(SimpleModel.assert_model, models))
+        if not isinstance(parameter_priors, list):
+            parameter_priors = [parameter_priors]
+        self.parameter_priors = parameter_priors
+        if len(self.models) != len(self.parameter_priors):
+            raise AssertionError(
+                "Number models and number parameter priors have to agree.")
+        if distance_function is None:
+            distance_function = PNormDistance()
+        self.distance_function = to_distance(distance_function)
+        self.summary_statistics = summary_statistics
+        if model_prior is None:
+            model_prior = RV("randint", 0, len(self.models))
+        self.model_prior = model_prior
+        if model_perturbation_kernel is None:
+            model_perturbation_kernel = ModelPerturbationKernel(
+                len(self.models), probability_to_stay=.7)
+        self.model_perturbation_kernel = model_perturbation_kernel
+        if transitions is None:
+            transitions = [MultivariateNormalTransition() for _ in self.models]
+        if not isinstance(transitions, list):
+            transitions = [transitions]
+        self.transitions = transitions
+        if eps is None:
+            eps = MedianEpsilon(median_multiplier=1)
+        self.eps = eps
+        if isinstance(population_size, int):
+            population_size = ConstantPopulationSize(population_size)
+        self.population_size = population_size
+        if sampler is None:
+            sampler = (BatchedGPUSampler()
+                       if all(isinstance(m, VectorizedModel) for m in self.models)
+                       else SingleCoreSampler())
+        self.sampler = sampler
+        if acceptor is None:
+            acceptor = UniformAcceptor()
+        self.acceptor = SimpleFunctionAcceptor.assert_acceptor(acceptor)
+        self.stop_if_only_single_model_alive = stop_if_only_single_model_alive
+        self.max_nr_recorded_particles = max_nr_recorded_particles
+        self.show_progress = show_progress
+        self.x_0 = None
+        self.history = None
+        self._initial_population = None
+        self.minimum_epsilon = None
+        self.max_nr_populations = None
+        self.min_acceptance_rate = None
+        self.generation_log = []
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        del state['sampler']
+        return state
+
+    # -- history ------------------------------------------------------------
+    def new(self, db: str, observed_sum_stat: dict = None, *, gt_model=None,
+            gt_par=None, meta_info=None) -> History:
+        """smc.py:255-353."""
+        if observed_sum_stat is None:
+            observed_sum_stat = {}
+        self.x_0 = observed_sum_stat
+        self.history = History(db)
+        if gt_par is None:
+            gt_par = {}
+        model_names = [model.name for model in self.models]
+        self.history.store_initial_data(
+            gt_model, meta_info, observed_sum_stat, gt_par, model_names,
+            self.distance_function.to_json(), self.eps.to_json(),
+            self.population_size.to_json())
+        return self.history
+
+    def load(self, db: str, abc_id: int = 1, observed_sum_stat: dict = None):
+        """smc.py:355-389 for an in-process History object or db string."""
+        if isinstance(db, History):
+            self.history = db
+        else:
+            raise NotImplementedError(
+                "resuming from a database file is not supported; pass the "
+                "History object of the earlier run")
+        self.history.id = abc_id
+        if observed_sum_stat is None:
+            observed_sum_stat = self.history.observed_sum_stat()
+        self.x_0 = observed_sum_stat
+        return self.history
+
+    # -- calibration (smc.py:391-542) -------------------------------------
+    def _initialize_dist_eps_acc(self, t: int):
+        def get_initial_sum_stats():
+            return self._get_initial_population(t).get_accepted_sum_stats()
+
+        def _get_initial_population_with_distances():
+            population = self._get_initial_population(t)
+            self._update_population_distances(population, t)
+            return population
+
+        def get_initial_weighted_distances():
+            return _get_initial_population_with_distances().get_weighted_distances()
+
+        self.distance_function.initialize(t, get_initial_sum_stats, self.x_0)
+        self.acceptor.initialize(t, get_initial_weighted_distances,
+                                 self.distance_function, self.x_0)
+
+        def get_initial_records():
+            population = _get_initial_population_with_distances()
+            records = []
+            for particle in population.get_list():
+                for d in particle.accepted_distances:
+                    records.append({'distance': d, 'transition_pd_prev': 1.0,
+                                    'transition_pd': 1.0, 'accepted': True})
+            return records
+
+        self.eps.initialize(t, get_initial_weighted_distances,
+                            get_initial_records, self.max_nr_populations,
+                            self.acceptor.get_epsilon_config(t))
+
+    def _update_population_distances(self, population, t):
+        """population.update_distances (population.py:147-162), batched on
+        the device for columnar populations."""
+        if population.columns is not None and hasattr(self.distance_function,
+                                                      "device_call"):
+            x0vec = gpu.as_dev(np.array([self.x_0[k] for k in population.columns.sum_stat_keys],
+                                        dtype=np.float64))
+            population.update_distances_device(self.distance_function, x0vec, t)
+        else:
+            def distance_to_ground_truth(x, par):
+                return self.distance_function(x, self.x_0, t, par)
+            population.update_distances(distance_to_ground_truth)
+
+    def _get_initial_population(self, t: int):
+        if self._initial_population is None:
+            if self.history.n_populations > 0:
+                population = self.history.get_population()
+            else:
+                population = self._sample_from_prior(t)
+                self.history.update_nr_samples(History.PRE_TIME,
+                                               self.sampler.nr_evaluations_)
+            self._initial_population = population
+        return self._initial_population
+
+    def _create_simulate_from_prior_function(self, t: int):
+        model_prior = self.model_prior
+        parameter_priors = self.parameter_priors
+        models = self.models
+        summary_statistics = self.summary_statistics
+
+        def simulate_one():
+            m = int(model_prior.rvs())
+            theta = parameter_priors[m].rvs()
+            model_result = models[m].summary_statistics(t, theta,
+                                                        summary_statistics)
+            return Particle(m=m, parameter=theta, weight=1.0,
+                            accepted_sum_stats=[model_result.sum_stats],
+                            accepted_distances=[np.inf],
+                            rejected_sum_stats=[], rejected_distances=[],
+                            accepted=True)
+        return simulate_one
+
+    def _sample_from_prior(self, t: int):
+        logger.info(f"Calibration sample before t={t}.")
+        spec = GenerationSpec(self, -1, all_accepted=True)
+        sample = self.sampler.sample_until_n_accepted(
+            self.population_size(-1), spec, max_eval=np.inf,
+            all_accepted=True, show_progress=self.show_progress)
+        return sample.get_accepted_population()
+
+    # -- per-candidate closure (smc.py:544-811) ---------------------------
+    def _create_simulate_function(self, t: int):
+        return GenerationSpec(self, t)
+
+    def _create_simulate_function_closure(self, t: int):
+        model_probabilities = self.history.get_model_probabilities(t - 1)
+        m = np.array(model_probabilities.index)
+        p = np.array(model_probabilities.p)
+        model_prior = self.model_prior
+        parameter_priors = self.parameter_priors
+        model_perturbation_kernel = self.model_perturbation_kernel
+        transitions = self.transitions
+        nr_samples_per_parameter = self.population_size.nr_samples_per_parameter
+        models = self.models
+        summary_statistics = self.summary_statistics
+        distance_function = self.distance_function
+        eps = self.eps
+        acceptor = self.acceptor
+        x_0 = self.x_0
+        weight_function = self._create_weight_function(t)
+
+        def simulate_one():
+            parameter = ABCSMC._generate_valid_proposal(
+                t, m, p, model_prior, parameter_priors,
+                model_perturbation_kernel, transitions)
+            return ABCSMC._evaluate_proposal(
+                *parameter, t, nr_samples_per_parameter, models,
+                summary_statistics, distance_function, eps, acceptor, x_0,
+                weight_function)
+        return simulate_one
+
+    @staticmethod
+    def _generate_valid_proposal(t, m, p, model_prior, parameter_priors,
+                                 model_perturbation_kernel, transitions):
+        if t == 0:
+            m_ss = int(model_prior.rvs())
+            theta_ss = parameter_priors[m_ss].rvs()
+            return m_ss, theta_ss
+        n_sample, n_sample_soft_limit = 0, 1000
+        while True:
+            if len(m) > 1:
+                index = int(np.random.choice(len(p), p=p))
+                m_s = m[index]
+                m_ss = model_perturbation_kernel.rvs(m_s)
+                if m_ss not in m:
+                    continue
+            else:
+                m_ss = m[0]
+            theta_ss = Parameter(**transitions[m_ss].rvs().to_dict())
+            if (model_prior.pmf(m_ss)
+                    * parameter_priors[m_ss].pdf(theta_ss) > 0):
+                return m_ss, theta_ss
+            n_sample += 1
+            if n_sample == n_sample_soft_limit:
+                logger.warning(
+                    "Unusually many (model, parameter) samples have prior "
+                    "density zero. The transition might be inappropriate.")
+
+    @staticmethod
+    def _evaluate_proposal(m_ss, theta_ss, t, nr_samples_per_parameter, models,
+                           summary_statistics, distance_function, eps,
+                           acceptor, x_0, weight_function):
+        accepted_sum_stats, accepted_distances = [], []
+        rejected_sum_stats, rejected_distances = [], []
+        accepted_weights = []
+        for _ in range(nr_samples_per_parameter):
+            model_result = models[m_ss].accept(t, theta_ss, summary_statistics,
+                                               distance_function, eps,
+                                               acceptor, x_0)
+            if model_result.accepted:
+                accepted_sum_stats.append(model_result.sum_stats)
+                accepted_distances.append(model_result.distance)
+                accepted_weights.append(model_result.weight)
+            else:
+                rejected_sum_stats.append(model_result.sum_stats)
+                rejected_distances.append(model_result.distance)
+        accepted = len(accepted_sum_stats) > 0
+        weight = (weight_function(accepted_distances, m_ss, theta_ss,
+                                  accepted_weights) if accepted else 0)
+        return Particle(m=m_ss, parameter=theta_ss, weight=weight,
+                        accepted_sum_stats=accepted_sum_stats,
+                        accepted_distances=accepted_distances,
+                        rejected_sum_stats=rejected_sum_stats,
+                        rejected_distances=rejected_distances,
+                        accepted=accepted)
+
+    def _create_transition_pdf(self, t: int, transitions=None):
+        if t == 0:
+            return self._create_prior_pdf()
+        model_probabilities = self.history.get_model_probabilities(t - 1)
+        model_perturbation_kernel = self.model_perturbation_kernel
+        if transitions is None:
+            transitions = self.transitions
+
+        def transition_pdf(m_ss, theta_ss):
+            model_factor = sum(
+                row.p * model_perturbation_kernel.pmf(m_ss, m)
+                for m, row in model_probabilities.iterrows())
+            particle_factor = transitions[m_ss].pdf(pd.Series(dict(theta_ss)))
+            transition_pd = model_factor * particle_factor
+            if transition_pd == 0:
+                logger.debug("Transition density is zero!")
+            return transition_pd
+        return transition_pdf
+
+    def _create_prior_pdf(self):
+        model_prior = self.model_prior
+        parameter_priors = self.parameter_priors
+
+        def prior_pdf(m_ss, theta_ss):
+            return model_prior.pmf(m_ss) * parameter_priors[m_ss].pdf(theta_ss)
+        return prior_pdf
+
+    def _create_weight_function(self, t: int):
+        nr_samples_per_parameter = self.population_size.nr_samples_per_parameter
+        if t == 0:
+            def prior_weight_function(distance_list, m_ss, theta_ss,
+                                      acceptance_weights):
+                weight = len(distance_list) / nr_samples_per_parameter
+                weight *= np.prod(acceptance_weights)
+                return weight
+            return prior_weight_function
+        transition_pdf = self._create_transition_pdf(t)
+        prior_pdf = self._create_prior_pdf()
+
+        def weight_function(distance_list, m_ss, theta_ss, acceptance_weights):
+            prior_pd = prior_pdf(m_ss, theta_ss)
+            transition_pd = transition_pdf(m_ss, theta_ss)
+            acceptance_weight = np.prod(acceptance_weights)
+            fraction = len(distance_list) / nr_samples_per_parameter
+            return prior_pd * acceptance_weight * fraction / transition_pd
+        return weight_function
+
+    # -- run (smc.py:813-958) ----------------------------------------------
+    def run(self, minimum_epsilon: float = None,
+            max_nr_populations: int = np.inf,
+            min_acceptance_rate: float = 0.) -> History:
+        if minimum_epsilon is None:
+            minimum_epsilon = 0.0
+        self.minimum_epsilon = minimum_epsilon
+        self.max_nr_populations = max_nr_populations
+        self.min_acceptance_rate = min_acceptance_rate
+        t0 = self.history.max_t + 1
+        self.history.start_time = datetime.datetime.now()
+        self._fit_transitions(t0)
+        self._adapt_population_size(t0)
+        self._initialize_dist_eps_acc(t0)
+        self.distance_function.configure_sampler(self.sampler)
+        self.eps.configure_sampler(self.sampler)
+        t_max = t0 + max_nr_populations - 1
+        t = t0
+        while t <= t_max:
+            current_eps = self.eps(t)
+            logger.info(f"t: {t}, eps: {current_eps}.")
+            t_start = datetime.datetime.now()
+            simulate_one = self._create_simulate_function(t)
+            pop_size = self.population_size(t)
+            max_eval = (np.inf if min_acceptance_rate == 0.
+                        else pop_size / min_acceptance_rate)
+            sample = self.sampler.sample_until_n_accepted(
+                pop_size, simulate_one, max_eval,
+                show_progress=self.show_progress)
+            if not sample.ok:
+                logger.info("Stopping: sample not ok.")
+                break
+            population = sample.get_accepted_population()
+            n_sim = self.sampler.nr_evaluations_
+            model_names = [model.name for model in self.models]
+            self.history.append_population(t, current_eps, population, n_sim,
+                                           model_names)
+            pop_size = len(population)
+            acceptance_rate = pop_size / n_sim
+            ess = self._ess(population)
+            logger.info(f"Acceptance rate: {pop_size} / {n_sim} = "
+                        f"{acceptance_rate:.4e}, ESS={ess:.4e}.")
+            self._prepare_next_iteration(t + 1, sample, population,
+                                         acceptance_rate)
+            self.generation_log.append(dict(
+                t=t, eps=float(current_eps), n_sim=int(n_sim), ess=float(ess),
+                seconds=(datetime.datetime.now() - t_start).total_seconds()))
+            if current_eps <= minimum_epsilon:
+                logger.info("Stopping: minimum epsilon.")
+                break
+            elif self.stop_if_only_single_model_alive \
+                    and self.history.nr_of_models_alive() <= 1:
+                logger.info("Stopping: single model alive.")
+                break
+            elif acceptance_rate < min_acceptance_rate:
+                logger.info("Stopping: minimum acceptance rate.")
+                break
+            t += 1
+        self.history.done()
+        return self.history
+
+    @staticmethod
+    def _ess(population):
+        """effective_sample_size of the normalised weights (smc.py:930)."""
+        if population.columns is not None:
+            return float(population._stats[1].item())
+        return effective_sample_size(population.get_weighted_distances()['w'])
+
+    def _prepare_next_iteration(self, t, sample, population, acceptance_rate):
+        """smc.py:960-1040."""
+        prev_transitions = copy.deepcopy(self.transitions)
+        self._fit_transitions(t)
+        self._adapt_population_size(t)
+
+        def get_recorded_sum_stats():
+            return sample.first_m_sum_stats(self.max_nr_recorded_particles)
+
+        df_updated = self.distance_function.update(t, get_recorded_sum_stats)
+
+        def get_weighted_distances():
+            if df_updated:
+                self._update_population_distances(population, t)
+            return population.get_weighted_distances()
+
+        self.acceptor.update(t, get_weighted_distances, self.eps(t - 1),
+                             acceptance_rate)
+
+        def get_all_records():
+            recorded_particles = sample.first_m_particles(
+                self.max_nr_recorded_particles)
+            records = []
+            transition_pdf_prev = self._create_transition_pdf(t - 1,
+                                                              prev_transitions)
+            transition_pdf = self._create_transition_pdf(t)
+            for particle in recorded_particles:
+                all_distances = (particle.accepted_distances
+                                 + particle.rejected_distances)
+                tp_prev = transition_pdf_prev(particle.m, particle.parameter)
+                tp = transition_pdf(particle.m, particle.parameter)
+                for d in all_distances:
+                    records.append({'distance': d, 'transition_pd_prev': tp_prev,
+                                    'transition_pd': tp,
+                                    'accepted': particle.accepted})
+            return records
+
+        self.eps.update(t, get_weighted_distances, get_all_records,
+                        acceptance_rate, self.acceptor.get_epsilon_config(t))
+
+    def _adapt_population_size(self, t):
+        if t == 0:
+            return
+        w = self.history.get_model_probabilities(self.history.max_t)["p"].values
+        self.population_size.update(self.transitions, w, t)
+
+    def _fit_transitions(self, t):
+        """smc.py:1065-1079; device-resident populations are fitted in
+        place (no DataFrame round trip)."""
+        if t == 0:
+            return
+        for m in self.history.alive_models(t - 1):
+            cols = self.history.get_population_device(t - 1)
+            tr = self.transitions[m]
+            if cols is not None and hasattr(tr, "fit_device"):
+                tr.fit_device(cols.theta, cols.weights, cols.param_names)
+            else:
+                particles, w = self.history.get_distribution(m, t - 1)
+                tr.fit(particles, w)

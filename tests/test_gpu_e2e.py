@@ -1,0 +1,159 @@
+"""End-to-end ABCSMC(...).run() on the GPU engine.
+
+Statistical parity targets: the conjugate-Gaussian thresholds of the
+reference's test_nondeterministic/test_abc_smc_algorithm.py:309-394
+(posterior CDF sup-difference, |mean - mu|, |sd - sigma|), and the moments
+of reference runs of config 1 (tests/golden/e2e_reference.json, produced by
+importing pyABC 0.10.5).  RNG streams differ from numpy's, so these checks
+are statistical, not bit-exact.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+from scipy import stats
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def c1_abc(pop=1000, sampler=None, seed=0, transition=None, eps=None):
+    import pyabc_amd as pa
+    np.random.seed(seed)
+    model = pa.LinearGaussianModel(["x"], ["y"], src=[0], sigma=[0.5])
+    prior = pa.Distribution(x=pa.RV("norm", 0, 1))
+    abc = pa.ABCSMC(model, prior, pa.PNormDistance(), population_size=pop,
+                    sampler=sampler or pa.BatchedGPUSampler(seed=1000 + seed),
+                    transitions=transition, eps=eps)
+    abc.new("sqlite://", {"y": 2.0})
+    return abc
+
+
+def posterior_check(h, mu, sigma, cdf_tol=0.12, mean_tol=0.07, sd_tol=0.1):
+    df, w = h.get_distribution(0, h.max_t)
+    x = df["x"].values
+    mean = float((x * w).sum())
+    sd = float(np.sqrt((w * (x - mean) ** 2).sum()))
+    # the reference's metric (test_abc_smc_algorithm.py:336-344): weighted
+    # ECDF interpolated on linspace(-8, 8), sup distance to the exact CDF
+    from scipy.interpolate import interp1d
+    order = np.argsort(x)
+    f_emp = interp1d(np.hstack((-200, x[order], 200)),
+                     np.hstack((0, np.cumsum(w[order]), 1)))
+    grid = np.linspace(-8, 8)
+    sup = np.max(np.abs(f_emp(grid) - stats.norm(mu, sigma).cdf(grid)))
+    assert abs(mean - mu) < mean_tol, (mean, mu)
+    assert abs(sd - sigma) < sd_tol, (sd, sigma)
+    assert sup < cdf_tol, sup
+    return mean, sd
+
+
+def test_gaussian_multiple_populations_restated():
+    """test_abc_smc_algorithm.py:354-394 on the batched engine: N = 600,
+    4 generations, MedianEpsilon(.2); thresholds 0.052 / 0.07 / 0.12."""
+    import pyabc_amd as pa
+    for seed in range(3):
+        abc = c1_abc(pop=600, seed=seed, eps=pa.MedianEpsilon(.2))
+        h = abc.run(minimum_epsilon=-1, max_nr_populations=4)
+        assert h.max_t == 3
+        posterior_check(h, 1.6, np.sqrt(0.2), cdf_tol=0.052, sd_tol=0.12)
+
+
+def test_c1_batched_matches_analytic_and_reference():
+    abc = c1_abc()
+    h = abc.run(max_nr_populations=8)
+    assert h.max_t == 7
+    mean, sd = posterior_check(h, 1.6, np.sqrt(0.2))
+    pops = h.get_all_populations()
+    eps = pops["epsilon"].values[1:]
+    assert np.all(np.diff(eps) < 0)
+    path = os.path.join(GOLDEN, "e2e_reference.json")
+    if os.path.exists(path):
+        ref = json.load(open(path))
+        means = [v["mean"] for v in ref.values()]
+        sds = [v["sd"] for v in ref.values()]
+        assert abs(mean - np.mean(means)) < 0.07
+        assert abs(sd - np.mean(sds)) < 0.1
+        # acceptance work per generation within a factor of the reference
+        ref_samples = np.mean([v["samples"][-1] for v in ref.values()])
+        assert 0.3 < pops["samples"].values[-1] / ref_samples < 3
+
+
+def test_c1_single_core_per_particle_path():
+    import pyabc_amd as pa
+    abc = c1_abc(pop=200, sampler=pa.SingleCoreSampler())
+    h = abc.run(max_nr_populations=4)
+    assert h.max_t == 3
+    posterior_check(h, 1.6, np.sqrt(0.2), cdf_tol=0.2, mean_tol=0.2,
+                    sd_tol=0.2)
+
+
+def test_deterministic_given_seed():
+    h1 = c1_abc(pop=2000, seed=3).run(max_nr_populations=3)
+    h2 = c1_abc(pop=2000, seed=3).run(max_nr_populations=3)
+    d1, w1 = h1.get_distribution(0, 2)
+    d2, w2 = h2.get_distribution(0, 2)
+    np.testing.assert_array_equal(d1.values, d2.values)
+    np.testing.assert_array_equal(w1, w2)
+    assert list(h1.get_all_populations()["samples"]) == \
+        list(h2.get_all_populations()["samples"])
+
+
+def test_c2_shape_10d():
+    """10-D conjugate model (config 2 shape, smaller N): posterior N(0.8, 0.2)."""
+    import pyabc_amd as pa
+    np.random.seed(0)
+    d = 10
+    names = [f"p{k}" for k in range(d)]
+    keys = [f"y{k}" for k in range(d)]
+    model = pa.LinearGaussianModel(names, keys, src=list(range(d)),
+                                   sigma=[0.5] * d)
+    prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.PNormDistance(), population_size=20000,
+                    eps=pa.QuantileEpsilon(alpha=0.5),
+                    sampler=pa.BatchedGPUSampler(seed=5))
+    abc.new("sqlite://", {k: 1.0 for k in keys})
+    h = abc.run(max_nr_populations=6)
+    df, w = h.get_distribution(0, h.max_t)
+    mean = (df.values * w[:, None]).sum(0)
+    # posterior mean 0.8 per coordinate; ABC with finite eps inflates spread
+    assert np.all(np.abs(mean - 0.8) < 0.1), mean
+
+
+def test_adaptive_distance_run():
+    import pyabc_amd as pa
+    np.random.seed(1)
+    rng = np.random.default_rng(1234)
+    S = 32
+    names = [f"t{k}" for k in range(4)]
+    keys = [f"s{k:03d}" for k in range(S)]
+    a = rng.uniform(0.5, 2, S)
+    sig = 10 ** rng.uniform(-1, 1, S)
+    model = pa.LinearGaussianModel(names, keys, src=np.arange(S) % 4, a=a,
+                                   sigma=sig)
+    prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
+    x0 = dict(zip(keys, a * 0.5))
+    for sf in (pa.distance.standard_deviation,
+               pa.distance.median_absolute_deviation):
+        dist = pa.AdaptivePNormDistance(scale_function=sf)
+        abc = pa.ABCSMC(model, prior, dist, population_size=5000,
+                        sampler=pa.BatchedGPUSampler(seed=2))
+        abc.new("sqlite://", x0)
+        h = abc.run(max_nr_populations=4)
+        assert h.max_t == 3
+        w_last = dist.weights[max(dist.weights)]
+        assert len(w_last) == S and np.isclose(np.mean(list(w_last.values())), 1)
+        # weights track 1/scale: noisier statistics get smaller weights
+        wv = np.array([w_last[k] for k in keys])
+        assert np.corrcoef(np.log(wv), -np.log(np.sqrt(a ** 2 * 0.1 + sig ** 2)))[0, 1] > 0.8
+
+
+def test_local_transition_run():
+    import pyabc_amd as pa
+    abc = c1_abc(pop=2000, transition=pa.LocalTransition(k=50, k_fraction=None))
+    h = abc.run(max_nr_populations=5)
+    posterior_check(h, 1.6, np.sqrt(0.2), cdf_tol=0.15, mean_tol=0.1,
+                    sd_tol=0.15)
