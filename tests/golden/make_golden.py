@@ -237,7 +237,51 @@ def gen_e2e(seeds=(0, 1, 2, 3)):
         json.dump(out, f, indent=1)
 
 
+def gen_e2e10(seeds=(0, 1, 2, 3), pop=1000, gens=5):
+    """10-D conjugate model (config 2 shape at N=1000): the reference's ABC
+    posterior moments per generation (statistical parity targets)."""
+    d = 10
+    nm = [f"p{k}" for k in range(d)]
+    keys = [f"y{k}" for k in range(d)]
+    out = {}
+    for s in seeds:
+        np.random.seed(s)
+        t0 = time.time()
+
+        def model(p):
+            return {keys[k]: p[nm[k]] + 0.5 * np.random.randn()
+                    for k in range(d)}
+        prior = pyabc.Distribution(**{n: pyabc.RV("norm", 0, 1) for n in nm})
+        abc = pyabc.ABCSMC(model, prior, pyabc.PNormDistance(),
+                           population_size=pop,
+                           eps=QuantileEpsilon(alpha=0.5),
+                           sampler=pyabc.SingleCoreSampler())
+        abc.new("sqlite://", {k: 1.0 for k in keys})
+        h = abc.run(max_nr_populations=gens)
+        pops = h.get_all_populations()
+        means, sds = [], []
+        for t in range(h.max_t + 1):
+            df, w = h.get_distribution(0, t)
+            v = df[nm].values
+            m = (v * w[:, None]).sum(0)
+            means.append([float(a) for a in m])
+            sds.append([float(a) for a in
+                        np.sqrt((w[:, None] * (v - m) ** 2).sum(0))])
+        out[f"d10_seed{s}"] = dict(
+            mean=means, sd=sds,
+            eps=[float(e) for e in pops["epsilon"].values],
+            samples=[int(n) for n in pops["samples"].values],
+            seconds=time.time() - t0)
+        print("e2e d10 seed", s, out[f"d10_seed{s}"]["eps"],
+              np.mean(means[-1]), flush=True)
+    with open(os.path.join(HERE, "e2e_reference_d10.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
+    if "--e2e10" in sys.argv:
+        gen_e2e10()
+        sys.exit(0)
     gen_mvn()
     gen_local()
     gen_distance()
