@@ -2,7 +2,8 @@
 
 Workload (BASELINE.json configs[1], "c2"): 10-D Gaussian model with the
 vectorised simulator y_k = theta_k + 0.5 eps_k, prior N(0, 1)^10, x_0 = 1,
-MultivariateNormalTransition (f64-MFMA transition density), PNormDistance
+MultivariateNormalTransition (x3 limb-split f16-MFMA transition density),
+PNormDistance
 p = 2, QuantileEpsilon(alpha = 0.5), population 1e5 per GPU.  A "step" is one
 full generation: batched candidate generation until N_pop are accepted,
 importance weights (the N_acc x N_pop transition density), fit of the next
@@ -16,8 +17,8 @@ replicated by all-gather each generation ("scaling": "weak": per-GPU accepted
 particles fixed; the transition density per GPU grows with the population).
 
 The JSON line also carries the roofline of the dominant kernel (the fused
-cross-term GEMM + log-sum-exp, mvn_lse_kernel) timed with HIP events on the
-launch stream, and a CPU baseline: the numpy oracle (oracle/) timed on a
+cross-term GEMM + exp2 + sum, mvn_x3_kernel) timed with HIP events recorded
+by libabcgpu on the launch stream around each launch, and a CPU baseline: the numpy oracle (oracle/) timed on a
 bounded sample of the same generation on this host.
 """
 import argparse
@@ -34,6 +35,7 @@ sys.path.insert(0, ROOT)
 
 F64_MFMA_PEAK_TFLOPS = 78.6    # MI355X FP64 matrix (spec)
 F32_MFMA_PEAK_TFLOPS = 157.3   # MI355X FP32 matrix (spec; MI355X_MICROARCH.md)
+F16_MFMA_PEAK_TFLOPS = 2516.6  # MI355X FP16 dense matrix (spec, no sparsity)
 
 
 def parse():
@@ -43,7 +45,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pop", type=int, default=100_000, help="per GPU")
     ap.add_argument("--dim", type=int, default=10)
-    ap.add_argument("--precision", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--precision", default="x3", choices=["x3", "f64", "f32"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -62,36 +64,39 @@ def setup_dist():
 
 
 class KernelTimer:
-    """HIP-event timing of every transition-density launch on its stream."""
+    """Dominant-kernel timing: libabcgpu records HIP events on the launch
+    stream directly around every transition-density GEMM launch
+    (abc_profile_begin/end); the wrapper below only logs the (M, N, d) shape
+    of each call for the algorithmic FLOP count."""
 
     def __init__(self, transition):
-        import torch
-        self.torch = torch
-        self.events = []
         self.shapes = []
         self.active = False
         orig = transition.logpdf_device
 
-        def timed(xd, out=None):
-            if not self.active:
-                return orig(xd, out=out)
-            s = torch.cuda.Event(enable_timing=True)
-            e = torch.cuda.Event(enable_timing=True)
-            s.record()
-            r = orig(xd, out=out)
-            e.record()
-            self.events.append((s, e))
-            self.shapes.append((xd.shape[0], transition._dev_X.shape[0],
-                                xd.shape[1]))
-            return r
-        transition.logpdf_device = timed
+        def logged(xd, out=None):
+            if self.active and getattr(transition, "_mfma", False):
+                self.shapes.append((xd.shape[0], transition._dev_X.shape[0],
+                                    xd.shape[1]))
+            return orig(xd, out=out)
+        transition.logpdf_device = logged
 
-    def summary(self):
-        self.torch.cuda.synchronize()
-        ms = [s.elapsed_time(e) for s, e in self.events]
-        flops = [2.0 * d * M * N for (M, N, d) in self.shapes]
-        pairs = [M * N for (M, N, d) in self.shapes]
-        return ms, flops, pairs
+    def begin(self):
+        from pyabc_amd import _native as nat
+        self.shapes = []
+        self.active = True
+        nat.call("abc_profile_begin")
+
+    def end(self):
+        import ctypes
+        from pyabc_amd import _native as nat
+        self.active = False
+        ms = ctypes.c_double(0.0)
+        n = ctypes.c_int64(0)
+        nat.call("abc_profile_end", ctypes.addressof(ms), ctypes.addressof(n))
+        flops = sum(2.0 * d * M * N for (M, N, d) in self.shapes)
+        pairs = sum(M * N for (M, N, d) in self.shapes)
+        return ms.value, int(n.value), flops, pairs
 
 
 def build_abc(args, rank, ws):
@@ -161,12 +166,12 @@ def main():
     abc.run(max_nr_populations=max(args.warmup, 1))
     barrier()
     n_before = len(abc.generation_log)
-    timer.active = True
+    timer.begin()
     t0 = time.perf_counter()
     abc.run(max_nr_populations=args.steps)
     barrier()
     elapsed = time.perf_counter() - t0
-    timer.active = False
+    k_ms, k_n, k_flops, k_pairs = timer.end()
     gens = abc.generation_log[n_before:]
     steps = len(gens)
     t_local = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -176,12 +181,21 @@ def main():
     n_pop = args.pop * ws
     value = steps * n_pop / elapsed
     pair_evals = steps * n_pop * n_pop / elapsed
-    ms, flops, pairs = timer.summary()
-    # dominant kernel: the transition density launches of the timed region
-    avg_ms = float(np.mean(ms)) if ms else float("nan")
-    avg_flop = float(np.mean(flops)) if flops else float("nan")
-    achieved = avg_flop / (avg_ms * 1e-3) / 1e12
+    # dominant kernel: the transition-density GEMM launches of the timed region
+    avg_ms = k_ms / k_n if k_n else float("nan")
+    achieved = k_flops / (k_ms * 1e-3) / 1e12 if k_n else float("nan")
     peak = F64_MFMA_PEAK_TFLOPS if args.precision == "f64" else F32_MFMA_PEAK_TFLOPS
+    kpad = {"x3": 32 * (math.ceil((args.dim + 4) / 32)
+                        + math.ceil((5 * args.dim + 4) / 32)),
+            "f64": 4 * math.ceil((args.dim + 1) / 4),
+            "f32": 4 * math.ceil((args.dim + 1) / 4)}[args.precision]
+    executed = 2.0 * kpad * k_pairs / (k_ms * 1e-3) / 1e12 if k_n else float("nan")
+    exec_peak = {"x3": F16_MFMA_PEAK_TFLOPS, "f64": F64_MFMA_PEAK_TFLOPS,
+                 "f32": F32_MFMA_PEAK_TFLOPS}[args.precision]
+    kname = {"x3": "mvn_x3_kernel (f16 MFMA, 3-limb split operands, exact-grid "
+                   "f32 accumulation + exp2 + sum)",
+             "f64": "mvn_lse_kernel<double> (f64 MFMA cross term + exp2 + LSE)",
+             "f32": "mvn_lse_kernel<float> (f32 MFMA cross term + exp2 + LSE)"}
     out = None
     if rank == 0:
         cpu = None
@@ -210,7 +224,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": args.precision,
+            "dtype": {"x3": "f32 (f16x3-limb MFMA, f32-grade)", "f64": "f64",
+                      "f32": "f32"}[args.precision],
             "data": "synthetic (device-generated, counter-based RNG)",
             "config": {"workload": "c2: 10-D Gaussian, vectorised simulator, "
                                    "MVN transition, PNorm p=2, QuantileEpsilon(0.5)",
@@ -219,13 +234,18 @@ def main():
             "pair_evals_per_s": pair_evals,
             "acceptance_rate_last": n_pop / gens[-1]["n_sim"] if gens else None,
             "generation_ms": [round(1e3 * g["seconds"], 3) for g in gens],
-            "roofline": {"bound": "mfma", "kernel": "mvn_lse_kernel "
-                         f"({args.precision} MFMA cross term + exp2 + LSE)",
+            "roofline": {"bound": "mfma", "kernel": kname[args.precision],
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak,
-                         "frac_of_f32_mfma_peak": achieved / F32_MFMA_PEAK_TFLOPS,
                          "flop_per_pair": 2 * args.dim,
-                         "launches": len(ms), "avg_launch_ms": avg_ms,
+                         "note": ("achieved = algorithmic 2*d FLOP per (candidate, "
+                                  "population) pair / HIP-event time of the GEMM "
+                                  "launch; peak = fp32 MFMA (x3/f32) or fp64 MFMA"),
+                         "pairs_per_s": k_pairs / (k_ms * 1e-3) if k_n else None,
+                         "executed_mfma_tflops": executed,
+                         "executed_mfma_peak": exec_peak,
+                         "executed_frac": executed / exec_peak,
+                         "launches": k_n, "avg_launch_ms": avg_ms,
                          "traffic": None},
             "cpu_baseline": cpu,
         }

@@ -39,6 +39,8 @@ extern "C" {
 /* Precision of the transition-density kernel. */
 #define ABC_PREC_F64 0 /* f64 MFMA cross term: parity mode (default)   */
 #define ABC_PREC_F32 1 /* f32 MFMA cross term: fast mode (~3e-5 rel.)  */
+#define ABC_PREC_X3 2  /* f16 MFMA on 3-limb split operands: f32-grade
+                          (~1e-7 rel.), fastest; r <= 25 */
 
 /* Prior distribution kinds (scipy.stats names, loc/scale convention). */
 #define ABC_PRIOR_FLAT (-1)  /* no prior: density 1 everywhere (plain rvs) */
@@ -52,6 +54,13 @@ extern "C" {
 
 const char* abc_last_error(void);
 int abc_version(void);
+
+/* Timing of the dominant kernel (the transition-density GEMM launch inside
+ * abc_mvn_logpdf): between begin and end, HIP events are recorded on the
+ * launch stream directly around each such launch; end synchronises on them
+ * and returns the summed elapsed time and the number of launches. */
+int abc_profile_begin(void);
+int abc_profile_end(double* total_ms, int64_t* launches);
 
 /* ---- reductions used by the fits ------------------------------------------
  * Replaces the numpy work in MultivariateNormalTransition.fit
@@ -82,19 +91,28 @@ int abc_normalize_weights(double* w, int64_t N, double* stats, void* ws,
  * density(x_i) = sum_j w_j N(x_i - X_j; 0, Sigma).  Host supplies the fp64
  * eigen-whitening of Sigma (scipy _PSD semantics): U [d x r], mean mu [d].
  * pack: builds the MFMA A-operand image of the population once per fit:
- *   y_j = (X_j - mu) U,  c_j = log(w_j) + log_w_shift - |y_j|^2 / 2.
+ *   y_j = (X_j - mu) U,  c_j = log(w_j) + log_w_shift - |y_j|^2 / 2
+ * (log_w_shift = -log max w keeps every exponent <= 0).  `range` (device,
+ * 2 doubles, nullable; X3 only) receives max_j |y_j| in the log2-scaled
+ * units of the X3 kernel (sqrt(log2 e) y) and the limb grid exponent E the
+ * image was built with; the X3 image is accurate to ~1e-7 for E <= 8 (use
+ * F64 otherwise).
  * logpdf: out[i] = log(sum_j w_j exp(-|(x_i - X_j) U|^2 / 2)) + log_const,
- *   with log_const = -(r log 2pi + log pdet)/2 - log_w_shift supplied by the
- *   host.  prec selects the f64- or f32-MFMA kernel (ABC_PREC_*).  r <= 60. */
+ *   log_const = -(r log 2pi + log pdet)/2 - log_w_shift.  prec selects the
+ *   f64-MFMA, f32-MFMA or limb-split f16-MFMA (X3) kernel.  X3 also needs the
+ *   fp64 population X, w: candidates outside its range (or whose density
+ *   underflows 2^-60 relative to max w) are recomputed by the fp64 direct
+ *   kernel on the device.  r <= 59 (X3: r <= 25). */
 size_t abc_mvn_packed_bytes(int64_t N, int r, int prec);
 int abc_mvn_pack_population(const double* X, const double* w, int64_t N, int d,
                             const double* mu, const double* U, int r,
                             double log_w_shift, int prec, void* packed,
-                            void* stream);
+                            double* range, void* stream);
 size_t abc_mvn_logpdf_workspace(int64_t M, int64_t N, int r, int prec);
 int abc_mvn_logpdf(const double* x, int64_t M, int d, const void* packed,
-                   int64_t N, const double* mu, const double* U, int r,
-                   int prec, double log_const, double* out, void* ws,
+                   const double* X, const double* w, int64_t N,
+                   const double* mu, const double* U, int r, int prec,
+                   double log_const, double log_w_shift, double* out, void* ws,
                    size_t ws_bytes, void* stream);
 /* Direct-difference fp64 VALU path: any r, and scipy's singular-covariance
  * support mask (pairs with |(x_i - X_j) V| >= support_tol get density 0;

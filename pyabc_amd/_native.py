@@ -23,6 +23,8 @@ SZ = C.c_size_t
 SIGNATURES = {
     "abc_last_error": (C.c_char_p, []),
     "abc_version": (I32, []),
+    "abc_profile_begin": (I32, []),
+    "abc_profile_end": (I32, [P, P]),
     "abc_weighted_moments_workspace": (SZ, [I64, I32]),
     "abc_weighted_moments": (I32, [P, P, I64, I32, P, P, SZ, P]),
     "abc_scan_workspace": (SZ, [I64]),
@@ -30,10 +32,11 @@ SIGNATURES = {
     "abc_normalize_weights_workspace": (SZ, [I64]),
     "abc_normalize_weights": (I32, [P, I64, P, P, SZ, P]),
     "abc_mvn_packed_bytes": (SZ, [I64, I32, I32]),
-    "abc_mvn_pack_population": (I32, [P, P, I64, I32, P, P, I32, D, I32, P, P]),
+    "abc_mvn_pack_population": (I32, [P, P, I64, I32, P, P, I32, D, I32, P, P,
+                                      P]),
     "abc_mvn_logpdf_workspace": (SZ, [I64, I64, I32, I32]),
-    "abc_mvn_logpdf": (I32, [P, I64, I32, P, I64, P, P, I32, I32, D, P, P,
-                             SZ, P]),
+    "abc_mvn_logpdf": (I32, [P, I64, I32, P, P, P, I64, P, P, I32, I32, D, D,
+                             P, P, SZ, P]),
     "abc_mvn_logpdf_direct": (I32, [P, I64, P, P, I64, I32, P, I32, P, I32,
                                     D, D, P, P]),
     "abc_propose": (I32, [P, P, I64, I32, P, P, P, U64, U32, I64, I64, I32,
@@ -70,6 +73,7 @@ ABC_ERR_NOT_ENOUGH_PARTICLES = -4
 ABC_ERR_UNSUPPORTED = -5
 ABC_PREC_F64 = 0
 ABC_PREC_F32 = 1
+ABC_PREC_X3 = 2
 
 PRIOR_KINDS = {"norm": 0, "uniform": 1, "expon": 2, "laplace": 3,
                "lognorm": 4, "gamma": 5, "beta": 6}

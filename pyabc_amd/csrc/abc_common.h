@@ -10,6 +10,9 @@ namespace abc {
 
 // ---- error reporting (abc_errors.cpp) --------------------------------------
 int set_error(int code, const char* fmt, ...);
+// HIP-event timing around the dominant kernel's launch (abc_profile.cpp)
+void profile_start(hipStream_t s);
+void profile_stop(hipStream_t s);
 
 #define ABC_CHECK_ARG(cond, ...)                                           \
   do { if (!(cond)) return ::abc::set_error(ABC_ERR_INVALID, __VA_ARGS__); } while (0)

@@ -379,9 +379,24 @@ int dispatch_lse(const Plan& p, const T* A, const T* B, const double* m0,
 }  // namespace
 }  // namespace abc
 
+namespace abc {
+size_t x3_packed_bytes(int64_t N, int r);
+int x3_max_rank();
+int x3_pack_population(const double* X, const double* w, int64_t N, int d,
+                       const double* mu, const double* U, int r,
+                       double log_w_shift, void* packed, double* range,
+                       hipStream_t s);
+size_t x3_logpdf_workspace(int64_t M, int64_t N, int r);
+int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
+              const double* X, const double* w, int64_t N, const double* mu,
+              const double* U, int r, double log_const, double log_norm,
+              double* out, void* ws, size_t ws_bytes, hipStream_t s);
+}  // namespace abc
+
 using namespace abc;
 
 extern "C" size_t abc_mvn_packed_bytes(int64_t N, int r, int prec) {
+  if (prec == ABC_PREC_X3) return x3_packed_bytes(N, r);
   const int KB = (int)ceil_div(r + 1, 4);
   const int64_t NT = ceil_div(N > 0 ? N : 1, 16);
   return (size_t)NT * 64 * KB * (prec == ABC_PREC_F32 ? 4 : 8);
@@ -391,11 +406,17 @@ extern "C" int abc_mvn_pack_population(const double* X, const double* w,
                                        int64_t N, int d, const double* mu,
                                        const double* U, int r,
                                        double log_w_shift, int prec,
-                                       void* packed, void* stream) {
+                                       void* packed, double* range,
+                                       void* stream) {
   ABC_CHECK_ARG(N >= 0 && d >= 1 && d <= 64, "pack: bad N=%lld d=%d", (long long)N, d);
   ABC_CHECK_ARG(r >= 1 && r <= 59, "pack: rank r=%d outside [1, 59]", r);
-  ABC_CHECK_ARG(prec == ABC_PREC_F32 || prec == ABC_PREC_F64, "pack: bad prec");
+  ABC_CHECK_ARG(prec == ABC_PREC_F32 || prec == ABC_PREC_F64 || prec == ABC_PREC_X3,
+                "pack: bad prec");
   ABC_CHECK_ARG(packed && mu && U && (N == 0 || (X && w)), "pack: null pointer");
+  if (prec == ABC_PREC_X3)
+    return x3_pack_population(X, w, N, d, mu, U, r, log_w_shift, packed, range,
+                              as_stream(stream));
+  if (range) ABC_HIP(hipMemsetAsync(range, 0, 2 * sizeof(double), as_stream(stream)));
   const int KB = (int)ceil_div(r + 1, 4);
   const int64_t NT = ceil_div(N > 0 ? N : 1, 16);
   const int64_t rows = NT * 16;
@@ -411,19 +432,26 @@ extern "C" int abc_mvn_pack_population(const double* X, const double* w,
 }
 
 extern "C" size_t abc_mvn_logpdf_workspace(int64_t M, int64_t N, int r, int prec) {
+  if (prec == ABC_PREC_X3) return x3_logpdf_workspace(M, N, r);
   return plan_ws(make_plan(M, N, r, prec));
 }
 
 extern "C" int abc_mvn_logpdf(const double* x, int64_t M, int d,
-                              const void* packed, int64_t N, const double* mu,
+                              const void* packed, const double* X,
+                              const double* w, int64_t N, const double* mu,
                               const double* U, int r, int prec,
-                              double log_const, double* out, void* ws,
-                              size_t ws_bytes, void* stream) {
+                              double log_const, double log_w_shift,
+                              double* out, void* ws, size_t ws_bytes,
+                              void* stream) {
   ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= 64, "logpdf: bad M/N/d");
   ABC_CHECK_ARG(r >= 1 && r <= 59, "logpdf: rank r=%d outside [1, 59]", r);
-  ABC_CHECK_ARG(prec == ABC_PREC_F32 || prec == ABC_PREC_F64, "logpdf: bad prec");
+  ABC_CHECK_ARG(prec == ABC_PREC_F32 || prec == ABC_PREC_F64 || prec == ABC_PREC_X3,
+                "logpdf: bad prec");
   if (M == 0) return ABC_OK;
   ABC_CHECK_ARG(x && packed && mu && U && out, "logpdf: null pointer");
+  if (prec == ABC_PREC_X3)
+    return x3_logpdf(x, M, d, packed, X, w, N, mu, U, r, log_const,
+                     log_const + log_w_shift, out, ws, ws_bytes, as_stream(stream));
   Plan p = make_plan(M, N, r, prec);
   if (ws_bytes < plan_ws(p))
     return set_error(ABC_ERR_WORKSPACE, "logpdf: workspace %zu < %zu", ws_bytes, plan_ws(p));
@@ -441,12 +469,16 @@ extern "C" int abc_mvn_logpdf(const double* x, int64_t M, int d,
     hipLaunchKernelGGL(pack_candidates_kernel<float>, gB, bB, 0, s, x, M, d, mu, U, r,
                        p.KB, (float*)Bp, m0, p.MTpad);
     ABC_LAUNCHED();
+    profile_start(s);
     rc = dispatch_lse<float>(p, (const float*)packed, (const float*)Bp, m0, pm, pl, s);
+    profile_stop(s);
   } else {
     hipLaunchKernelGGL(pack_candidates_kernel<double>, gB, bB, 0, s, x, M, d, mu, U, r,
                        p.KB, (double*)Bp, m0, p.MTpad);
     ABC_LAUNCHED();
+    profile_start(s);
     rc = dispatch_lse<double>(p, (const double*)packed, (const double*)Bp, m0, pm, pl, s);
+    profile_stop(s);
   }
   if (rc) return rc;
   ABC_LAUNCHED();

@@ -1,0 +1,574 @@
+// MultivariateNormalTransition.pdf, "x3" precision: the whitened cross-term
+// GEMM on f16 MFMA (v_mfma_f32_16x16x32_f16) with every operand split into
+// three 11-bit limbs, exact-grid accumulation in f32, fused with exp2 and the
+// weighted sum over the population.  Result accuracy is that of an f32
+// direct-difference evaluation (~1e-7 relative; tested at 2e-6 against the
+// fp64 oracle), at f16-MFMA issue rates.
+//
+// Reference: pyabc/transition/multivariatenormal.py:99-113,
+//   dens(x_i) = sum_j w_j N(x_i - X_j; 0, Sigma),
+// restated with the host's fp64 eigen-whitening U (U U^T = Sigma^-1) and the
+// log2 scaling folded into the coordinates (q = sqrt(log2 e)):
+//   y_j = q (X_j - mu) U,  z_i = q (x_i - mu) U
+//   s_ij = c_j - m_i + z_i . y_j              (log2 units, s_ij <= 0)
+//   c_j = log2e (log w_j - log w_max) - |y_j|^2 / 2,   m_i = |z_i|^2 / 2
+//   dens(x_i) = exp(log_const) * sum_j 2^s_ij,  log_const = log_norm + log w_max
+//
+// Limbs.  With the grid unit G = 2^(E-11), E chosen per fit on the device
+// from the population's largest whitened norm (E = max(3, ceil(log2(1.25
+// max|y| + 2 sqrt(r) + 4))), E <= 8), a coordinate v (|v| <= 2^E) is
+//   v = a1 G + a2 G 2^-11 + a3 G 2^-22      (a1, a2, a3 integers, |a| <= 2048)
+// and every slot value is such an integer times a power of two, so it is an
+// exact f16 (subnormal f16 operands and products are exact on gfx950: probe
+// tools/probes/mfma_f16_numerics.hip) and every product an exact f32.  Kept
+// products (limb indices p, q in 1..3) are the classes p + q <= 4:
+//   class 0: v1 w1                      multiples of G^2
+//   class 1: v1 w2 + v2 w1              multiples of G^2 2^-11
+//   class 2: v1 w3 + v2 w2 + v3 w1      multiples of G^2 2^-22
+// c and m are split into five limbs on the grids 2^22 G^2, 2^11 G^2, G^2
+// (hi) and G^2 2^-11, G^2 2^-22 (lo).  The K dimension holds, in this order,
+//   MFMA block 0       : class 0 (r), C0 C1 C2, M0 M1 M2, O     -> r + 7
+//   MFMA blocks 1 ..   : class 1 (2r), class 2 (3r), C3 C4, M3 M4 -> 5r + 4
+// The f16 MFMA sums each group of 8 products wide and adds the groups to the
+// accumulator in K order with f32 rounding (same probe).  Every block-0 term
+// is a multiple of G^2 and every partial sum is bounded by |c| + |m| + |o| +
+// |z||y| < 2^(2E+2) = 2^24 G^2 (norm checks below), so block 0 is EXACT.  O is
+// a per-candidate integer offset (B = -o, A = 1): a first pass over the
+// chunk runs block 0 alone (1 MFMA of KB per tile, exact s_hi) to find each
+// column's max, then o = ceil(max s_hi) is written into the B fragment and
+// the main pass leaves s - o <= 1 with the dominant pairs near 0, so the lo
+// blocks round at 2^-24 |s - o|.  Dropped
+// terms (class 3, limb residual) are < 2^(2E-35) per coordinate; numpy
+// emulation of this exact scheme: <= 1e-7 relative on the golden vectors.
+//
+// Layout (HBM): image = 256-byte header (max |y|^2/2, E, ok) + fragments
+// [NT][KB][64 lanes][8 halves] in the order of v_mfma_f32_16x16x32_f16 (lane
+// l holds row l & 15, k = 32 kb + 8 (l >> 4) + j); the population image is
+// built once per fit, the candidate image per call.  Each lane owns ONE
+// candidate column (l & 15) and four population rows of every 16x16 tile, so
+// the sum over the population stays in registers until a final 4-lane
+// combine.  Candidates outside the norm bound, and candidates whose density
+// underflows 2^-60 relative to max w (all pairs beyond ~11 kernel widths),
+// are recomputed by the fp64 direct kernel (rescue list; empty in practice).
+#include "abc_common.h"
+
+namespace abc {
+namespace {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr double LOG2E = 1.4426950408889634074;
+constexpr double SQRT_LOG2E = 1.2011224087864498;  // sqrt(log2 e)
+constexpr double LN2 = 0.69314718055994530942;
+constexpr int MAX_R = 25;       // K0 = r + 7 <= 32
+constexpr int E_MIN = 3, E_MAX = 8;
+constexpr float O_MIN = -64.f;  // offsets below this: density < 2^-60 -> rescue
+constexpr size_t HDR = 256;     // image header bytes
+
+struct Header { double maxsq; int E; int ok; };
+
+__host__ __device__ constexpr int x3_k0(int r) { return r + 7; }
+__host__ __device__ constexpr int x3_k12(int r) { return 5 * r + 4; }
+__host__ __device__ inline int x3_kb0(int r) { return (x3_k0(r) + 31) / 32; }
+__host__ __device__ inline int x3_kb12(int r) { return (x3_k12(r) + 31) / 32; }
+
+struct Limbs3 { double a1, a2, a3; };  // integers
+struct Limbs5 { double c[5]; };        // integers
+
+__device__ __forceinline__ Limbs3 split_coord(double v, int E) {
+  Limbs3 L;
+  const double G = ldexp(1.0, E - 11);
+  L.a1 = rint(v / G);
+  double r = v - L.a1 * G;
+  L.a2 = rint(ldexp(r / G, 11));
+  r -= ldexp(L.a2 * G, -11);
+  L.a3 = rint(ldexp(r / G, 22));
+  return L;
+}
+
+// grid exponent (log2) of scalar limb l: 2E-22 + {22, 11, 0, -11, -22}
+__device__ __forceinline__ int scalar_exp(int l, int E) { return 2 * E - 22 + 22 - 11 * l; }
+
+__device__ __forceinline__ Limbs5 split_scalar(double c, int E) {
+  Limbs5 L;
+  double r = c;
+  for (int l = 0; l < 5; ++l) {
+    const int e = scalar_exp(l, E);
+    L.c[l] = rint(ldexp(r, -e));
+    r -= ldexp(L.c[l], e);
+  }
+  return L;
+}
+
+// limb x 2^e as an (exact) f16 operand value
+__device__ __forceinline__ float opv(double limb, int e) { return (float)ldexp(limb, e); }
+
+// Value of K slot k for the population side (SIDE 0, A operand: carries c)
+// or the candidate side (SIDE 1, B operand: carries -m and the offset).
+template <int SIDE>
+__device__ __forceinline__ float slot_value(int k, int r, int K0pad, int E,
+                                            const Limbs3* L, const Limbs5& S) {
+  if (k < K0pad) {
+    const int e0 = 2 * (E - 11);
+    if (k < r) {  // class 0: a1 b1 G^2
+      const int x = e0 >> 1;  // floor
+      return opv(L[k].a1, SIDE == 0 ? x : e0 - x);
+    }
+    const int q = k - r;
+    if (q < 6) {  // scalar hi limbs: 0..2 = c (A), 3..5 = m (B)
+      const int l = q % 3;
+      const int e = scalar_exp(l, E);
+      const int x = e > 4 ? 4 : e;  // limb side exponent (|limb| <= 2048)
+      const bool limb_side = (q < 3) == (SIDE == 0);
+      return limb_side ? opv(S.c[l], x) : opv(1.0, e - x);
+    }
+    if (q == 6) return SIDE == 0 ? 1.f : 0.f;  // O: B = -o (set in the kernel)
+    return 0.f;
+  }
+  const int q = k - K0pad;
+  if (q < 5 * r) {
+    const int cls = q / r, dim = q % r;
+    // (p, q) limb pairs: (1,2) (2,1) (1,3) (2,2) (3,1)
+    const int pa[5] = {1, 2, 1, 2, 3}, pb[5] = {2, 1, 3, 2, 1};
+    const int p = SIDE == 0 ? pa[cls] : pb[cls];
+    const int etot = 2 * (E - 11) - 11 * (pa[cls] + pb[cls] - 2);
+    const int x = etot >> 1;
+    const double limb = p == 1 ? L[dim].a1 : (p == 2 ? L[dim].a2 : L[dim].a3);
+    return opv(limb, SIDE == 0 ? x : etot - x);
+  }
+  const int e4 = q - 5 * r;
+  if (e4 < 4) {  // scalar lo limbs: 0..1 = c (A), 2..3 = m (B)
+    const int l = 3 + (e4 & 1);
+    const int e = scalar_exp(l, E);
+    const int x = e < -24 ? -24 : e;  // limb side
+    const bool limb_side = (e4 < 2) == (SIDE == 0);
+    return limb_side ? opv(S.c[l], x) : opv(1.0, e - x);
+  }
+  return 0.f;
+}
+
+// Whitened, log2-scaled point of row `row`; returns |v|^2 / 2.
+__device__ __forceinline__ double whiten(const double* __restrict__ P, int64_t row,
+                                         int d, const double* __restrict__ mu,
+                                         const double* __restrict__ U, int r,
+                                         double* v) {
+  double h = 0.0;
+  for (int k = 0; k < r; ++k) {
+    double acc = 0.0;
+    for (int q = 0; q < d; ++q) acc += (P[row * d + q] - mu[q]) * U[q * r + k];
+    acc *= SQRT_LOG2E;
+    v[k] = acc;
+    h += acc * acc;
+  }
+  return 0.5 * h;
+}
+
+// max |y_j|^2 / 2 over the rows with w > 0 (atomicMax on the bit pattern of
+// a non-negative double, which is monotone).
+__global__ __launch_bounds__(256) void pop_range_kernel(
+    const double* __restrict__ X, const double* __restrict__ w, int64_t N,
+    int d, const double* __restrict__ mu, const double* __restrict__ U, int r,
+    Header* __restrict__ hdr) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double h = 0.0;
+  if (row < N && w[row] > 0.0) {
+    double v[MAX_R];
+    h = whiten(X, row, d, mu, U, r, v);
+  }
+  h = wave_max(h);
+  if ((threadIdx.x & 63) == 0 && h > 0.0)
+    atomicMax((unsigned long long*)&hdr->maxsq,
+              (unsigned long long)__double_as_longlong(h));
+}
+
+__global__ void x3_setup_kernel(Header* __restrict__ hdr, int r,
+                                double* __restrict__ range) {
+  const double ymax = sqrt(2.0 * hdr->maxsq);
+  int E = (int)ceil(log2(1.25 * ymax + 2.0 * sqrt((double)r) + 4.0));
+  if (E < E_MIN) E = E_MIN;
+  hdr->E = E;
+  hdr->ok = E <= E_MAX ? 1 : 0;
+  if (range) { range[0] = ymax; range[1] = (double)E; }
+}
+
+// One thread per image row (population row or candidate column): computes the
+// limbs and scatters the K slot values into the fragment image.
+template <int SIDE>
+__global__ __launch_bounds__(128) void pack_x3_kernel(
+    const double* __restrict__ P, const double* __restrict__ w, int64_t n,
+    int d, const double* __restrict__ mu, const double* __restrict__ U, int r,
+    double log_w_shift, int KB0, int KB, const Header* __restrict__ hdr,
+    _Float16* __restrict__ img, int64_t ntiles, int32_t* __restrict__ flags) {
+  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= ntiles * 16) return;
+  const int E = hdr->E;
+  const bool ok = hdr->ok != 0;
+  const double L2 = ldexp(1.0, 2 * E);  // 2^(2E): bound of |y|^2 and |c|
+  double v[MAX_R];
+  Limbs3 L[MAX_R];
+  double scalar = SIDE == 0 ? -L2 : 0.0;  // padding: c = -2^(2E), m = 0
+  bool bad = false;
+  for (int k = 0; k < r; ++k) v[k] = 0.0;
+  if (row < n) {
+    const double h = whiten(P, row, d, mu, U, r, v);
+    if (SIDE == 0) {
+      const double wj = w[row];
+      bad = !(wj > 0.0) || !(2.0 * h <= L2);
+      scalar = bad ? -L2 : fmax((log(wj) + log_w_shift) * LOG2E - h, -L2);
+    } else {
+      bad = !ok || !(2.0 * h <= L2);
+      scalar = bad ? -L2 : -h;
+    }
+    if (bad)
+      for (int k = 0; k < r; ++k) v[k] = 0.0;
+  }
+  if (flags && row < n) flags[row] = bad ? 1 : 0;
+  for (int k = 0; k < r; ++k) L[k] = split_coord(v[k], E);
+  const Limbs5 S = split_scalar(scalar, E);
+  const int64_t t = row >> 4;
+  const int rl = (int)(row & 15);
+  const int K0pad = 32 * KB0;
+  const int Ktot = 32 * KB;
+  for (int k = 0; k < Ktot; ++k) {
+    const float val = slot_value<SIDE>(k, r, K0pad, E, L, S);
+    const int kb = k >> 5, kk = k & 31;
+    const int lane = rl + 16 * (kk >> 3), j = kk & 7;
+    img[(((t * KB + kb) * 64) + lane) * 8 + j] = (_Float16)val;
+  }
+}
+
+// ---- the fused limb-split GEMM + exp2 + weighted sum -----------------------
+// One wave = CT candidate tiles x one population chunk; block = 4 waves; 1-D
+// grid, block b -> XCD b % 8 owns chunks {xcd, xcd + 8, ...} so that the
+// blocks sharing a population chunk share one XCD's L2 (speed only).
+// Pass 1: block 0 only -> per-column max of s_hi -> integer offset o.
+// Pass 2: all blocks -> per lane, sum over its population rows of 2^(s - o).
+template <int KB, int CT>
+__global__ __launch_bounds__(256) void mvn_x3_kernel(
+    const half8* __restrict__ A, const half8* __restrict__ Bi, int64_t MT,
+    int64_t NT, int nchunk, int64_t tiles_per_chunk, int64_t ngroups, int koff,
+    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t bid = blockIdx.x;
+  const int cpx = nchunk >> 3;
+  const int64_t xcd = bid & 7, jb = bid >> 3;
+  const int chunk = (int)(xcd + 8 * (jb % cpx));
+  const int64_t group = jb / cpx;
+  if (group >= ngroups) return;
+  const int64_t ct0 = (group * 4 + wave) * CT;
+  // which lane / element of the block-0 B fragment holds the offset slot
+  const bool off_lane = (lane >> 4) == ((koff & 31) >> 3);
+  const int off_j = koff & 7;
+
+  half8 b[CT][KB];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    const int64_t ct = ct0 + c < MT ? ct0 + c : MT - 1;  // clamp: dup work, never stored
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) b[c][kb] = Bi[(ct * KB + kb) * 64 + lane];
+  }
+  const int64_t t_begin = (int64_t)chunk * tiles_per_chunk;
+  const int64_t t_end = t_begin + tiles_per_chunk < NT ? t_begin + tiles_per_chunk : NT;
+
+  // ---- pass 1: exact s_hi (offset slot still 0) -> column max -> o
+  float o[CT];
+  {
+    float mx[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) mx[c] = -INFINITY;
+    half8 a0 = t_begin < t_end ? A[(t_begin * KB) * 64 + lane] : half8{};
+    for (int64_t t = t_begin; t < t_end; ++t) {
+      const int64_t tn = (t + 1 < t_end) ? t + 1 : t;
+      const half8 a0n = A[(tn * KB) * 64 + lane];
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+            a0, b[c][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        mx[c] = fmaxf(fmaxf(mx[c], fmaxf(acc[0], acc[1])), fmaxf(acc[2], acc[3]));
+      }
+      a0 = a0n;
+    }
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      float cm = fmaxf(mx[c], __shfl_xor(mx[c], 16, 64));
+      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      o[c] = fmaxf(ceilf(cm), O_MIN);
+      if (off_lane) b[c][0][off_j] = (_Float16)(-o[c]);
+    }
+  }
+
+  // ---- pass 2: full limb-split GEMM, exp2, sums
+  double l64[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) l64[c] = 0.0;
+  half8 a[KB], an[KB];
+  if (t_begin < t_end) {
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) a[kb] = A[(t_begin * KB + kb) * 64 + lane];
+  }
+  int64_t t = t_begin;
+  while (t < t_end) {
+    // f32 partial sums over at most 16 tiles (64 terms per lane), then fp64
+    float ls[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) ls[c] = 0.f;
+    const int64_t t_stop = t + 16 < t_end ? t + 16 : t_end;
+    for (; t < t_stop; ++t) {
+      const int64_t tn = (t + 1 < t_end) ? t + 1 : t;
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) an[kb] = A[(tn * KB + kb) * 64 + lane];
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[kb], b[c][kb], acc, 0, 0, 0);
+        ls[c] += (__builtin_amdgcn_exp2f(acc[0]) + __builtin_amdgcn_exp2f(acc[1])) +
+                 (__builtin_amdgcn_exp2f(acc[2]) + __builtin_amdgcn_exp2f(acc[3]));
+      }
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) a[kb] = an[kb];
+    }
+#pragma unroll
+    for (int c = 0; c < CT; ++c) l64[c] += (double)ls[c];
+  }
+  // lanes l, l^16, l^32, l^48 hold the same candidate column (same o)
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    double v = l64[c];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    const int64_t ct = ct0 + c;
+    if (lane < 16 && ct < MT) {
+      part_o[(int64_t)chunk * Mpad + ct * 16 + lane] = (double)o[c];
+      part_l[(int64_t)chunk * Mpad + ct * 16 + lane] = v;
+    }
+  }
+}
+
+__global__ void x3_combine_kernel(const double* __restrict__ part_o,
+                                  const double* __restrict__ part_l, int nchunk,
+                                  int64_t M, int64_t Mpad, double log_const,
+                                  const int32_t* __restrict__ cflags,
+                                  double* __restrict__ out,
+                                  int64_t* __restrict__ rescue,
+                                  unsigned int* __restrict__ nrescue) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M) return;
+  double om = -INFINITY;
+  for (int c = 0; c < nchunk; ++c)
+    if (part_l[(int64_t)c * Mpad + i] > 0.0) om = fmax(om, part_o[(int64_t)c * Mpad + i]);
+  double s = 0.0;
+  for (int c = 0; c < nchunk; ++c) {
+    const double l = part_l[(int64_t)c * Mpad + i];
+    if (l > 0.0) s += l * exp2(part_o[(int64_t)c * Mpad + i] - om);
+  }
+  const double lg = om + log2(s);  // log2 of sum_j 2^s_ij
+  // below 2^-60 (relative to max w) terms flushed at the f32 exp2 floor
+  // could matter: recompute in fp64
+  if (cflags[i] || !(s > 0.0) || !(lg >= -60.0)) {
+    const unsigned int q = atomicAdd(nrescue, 1u);
+    rescue[q] = i;
+    out[i] = -INFINITY;
+    return;
+  }
+  out[i] = log_const + LN2 * lg;
+}
+
+// fp64 direct difference for the rescue list (full-rank U, no support mask):
+// log( sum_j w_j exp(-|(x_i - X_j) U|^2 / 2) ) + log_norm.
+__global__ __launch_bounds__(256) void x3_rescue_kernel(
+    const int64_t* __restrict__ rescue, const unsigned int* __restrict__ nrescue,
+    const double* __restrict__ x, const double* __restrict__ X,
+    const double* __restrict__ w, int64_t N, int d,
+    const double* __restrict__ U, int r, double log_norm,
+    double* __restrict__ out) {
+  __shared__ double sm[4], sl[4];
+  const unsigned int n = *nrescue;
+  for (unsigned int q = blockIdx.x; q < n; q += gridDim.x) {
+    const int64_t i = rescue[q];
+    double xi[64];
+    for (int k = 0; k < d; ++k) xi[k] = x[i * d + k];
+    double m = -INFINITY, l = 0.0;
+    for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
+      const double wj = w[j];
+      if (!(wj > 0.0)) continue;
+      double maha = 0.0;
+      for (int k = 0; k < r; ++k) {
+        double p = 0.0;
+        for (int c = 0; c < d; ++c) p += (xi[c] - X[j * d + c]) * U[c * r + k];
+        maha += p * p;
+      }
+      const double s = log(wj) - 0.5 * maha;
+      if (s > m) { l = l * exp(m - s) + 1.0; m = s; }
+      else l += exp(s - m);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const double mo = __shfl_xor(m, o, 64), lo = __shfl_xor(l, o, 64);
+      const double mx = fmax(m, mo);
+      double s = 0.0;
+      if (l > 0.0) s += l * exp(m - mx);
+      if (lo > 0.0) s += lo * exp(mo - mx);
+      m = (l > 0.0 || lo > 0.0) ? mx : m;
+      l = s;
+    }
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { sm[wv] = m; sl[wv] = l; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double mx = -INFINITY;
+      for (int k = 0; k < 4; ++k) if (sl[k] > 0.0) mx = fmax(mx, sm[k]);
+      double s = 0.0;
+      for (int k = 0; k < 4; ++k) if (sl[k] > 0.0) s += sl[k] * exp(sm[k] - mx);
+      out[i] = (s > 0.0) ? mx + log(s) + log_norm : -INFINITY;
+    }
+    __syncthreads();
+  }
+}
+
+struct PlanX3 {
+  int KB0, KB, CT, nchunk;
+  int64_t MT, NT, MTpad, groups, tiles_per_chunk, Mpad;
+};
+
+PlanX3 make_plan_x3(int64_t M, int64_t N, int r) {
+  PlanX3 p;
+  p.KB0 = x3_kb0(r);
+  p.KB = p.KB0 + x3_kb12(r);
+  p.CT = p.KB <= 3 ? 8 : 4;
+  p.MT = ceil_div(M > 0 ? M : 1, 16);
+  p.NT = ceil_div(N > 0 ? N : 1, 16);
+  const int64_t waves = ceil_div(p.MT, p.CT);
+  p.groups = ceil_div(waves, 4);
+  p.MTpad = p.groups * 4 * p.CT;
+  p.Mpad = p.MTpad * 16;
+  // enough waves to fill 256 CUs (2 waves/SIMD) several times over, chunks
+  // of >= 32 population tiles
+  const int64_t want = ceil_div(8192, p.groups * 4);
+  const int64_t maxc = ceil_div(p.NT, 32);
+  int64_t nc = want < maxc ? want : maxc;
+  nc = ceil_div(nc < 1 ? 1 : nc, 8) * 8;
+  if (nc > 1024) nc = 1024;
+  p.nchunk = (int)nc;
+  p.tiles_per_chunk = ceil_div(p.NT, p.nchunk);
+  return p;
+}
+
+size_t plan_x3_ws(const PlanX3& p) {
+  size_t off = 0;
+  size_only<_Float16>(off, (size_t)p.MTpad * p.KB * 64 * 8);  // candidate image
+  size_only<int32_t>(off, (size_t)p.Mpad);                     // candidate flags
+  size_only<double>(off, (size_t)p.nchunk * p.Mpad);           // partial offsets
+  size_only<double>(off, (size_t)p.nchunk * p.Mpad);           // partial sums
+  size_only<int64_t>(off, (size_t)p.Mpad);                     // rescue list
+  size_only<unsigned int>(off, 64);                            // rescue count
+  return off + 256;
+}
+
+template <int KB, int CT>
+void launch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
+               double* po, double* pl, hipStream_t s) {
+  const int64_t blocks = p.groups * p.nchunk;
+  hipLaunchKernelGGL((mvn_x3_kernel<KB, CT>), dim3((unsigned)blocks), dim3(256),
+                     0, s, A, B, p.MT, p.NT, p.nchunk, p.tiles_per_chunk,
+                     p.groups, koff, po, pl, p.Mpad);
+}
+
+int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
+                double* po, double* pl, hipStream_t s) {
+  switch (p.KB) {
+    case 2: launch_x3<2, 8>(p, A, B, koff, po, pl, s); break;
+    case 3: launch_x3<3, 8>(p, A, B, koff, po, pl, s); break;
+    case 4: launch_x3<4, 4>(p, A, B, koff, po, pl, s); break;
+    case 5: launch_x3<5, 4>(p, A, B, koff, po, pl, s); break;
+    case 6: launch_x3<6, 4>(p, A, B, koff, po, pl, s); break;
+    default:
+      return set_error(ABC_ERR_UNSUPPORTED, "mvn x3: KB=%d unsupported", p.KB);
+  }
+  return ABC_OK;
+}
+
+}  // namespace
+
+// ---- internal entry points used by abc_mvn.hip ------------------------------
+size_t x3_packed_bytes(int64_t N, int r) {
+  const int KB = x3_kb0(r) + x3_kb12(r);
+  const int64_t NT = ceil_div(N > 0 ? N : 1, 16);
+  return HDR + (size_t)NT * KB * 64 * 8 * sizeof(_Float16);
+}
+
+int x3_max_rank() { return MAX_R; }
+
+int x3_pack_population(const double* X, const double* w, int64_t N, int d,
+                       const double* mu, const double* U, int r,
+                       double log_w_shift, void* packed, double* range,
+                       hipStream_t s) {
+  if (r > MAX_R)
+    return set_error(ABC_ERR_UNSUPPORTED, "mvn x3: rank %d > %d", r, MAX_R);
+  const int64_t NT = ceil_div(N > 0 ? N : 1, 16);
+  Header* hdr = (Header*)packed;
+  ABC_HIP(hipMemsetAsync(hdr, 0, HDR, s));
+  if (N > 0) {
+    hipLaunchKernelGGL(pop_range_kernel, dim3((unsigned)ceil_div(N, 256)), dim3(256),
+                       0, s, X, w, N, d, mu, U, r, hdr);
+    ABC_LAUNCHED();
+  }
+  hipLaunchKernelGGL(x3_setup_kernel, dim3(1), dim3(1), 0, s, hdr, r, range);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(pack_x3_kernel<0>, dim3((unsigned)ceil_div(NT * 16, 128)),
+                     dim3(128), 0, s, X, w, N, d, mu, U, r, log_w_shift,
+                     x3_kb0(r), x3_kb0(r) + x3_kb12(r), (const Header*)hdr,
+                     (_Float16*)((char*)packed + HDR), NT, (int32_t*)nullptr);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
+size_t x3_logpdf_workspace(int64_t M, int64_t N, int r) {
+  return plan_x3_ws(make_plan_x3(M, N, r));
+}
+
+int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
+              const double* X, const double* w, int64_t N, const double* mu,
+              const double* U, int r, double log_const, double log_norm,
+              double* out, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (r > MAX_R)
+    return set_error(ABC_ERR_UNSUPPORTED, "mvn x3: rank %d > %d", r, MAX_R);
+  if (!X || !w)
+    return set_error(ABC_ERR_INVALID, "mvn x3: X and w are needed (rescue path)");
+  PlanX3 p = make_plan_x3(M, N, r);
+  if (ws_bytes < plan_x3_ws(p))
+    return set_error(ABC_ERR_WORKSPACE, "mvn x3: workspace %zu < %zu", ws_bytes,
+                     plan_x3_ws(p));
+  Carver cv(ws, ws_bytes);
+  _Float16* Bimg = cv.take<_Float16>((size_t)p.MTpad * p.KB * 64 * 8);
+  int32_t* cflags = cv.take<int32_t>((size_t)p.Mpad);
+  double* po = cv.take<double>((size_t)p.nchunk * p.Mpad);
+  double* pl = cv.take<double>((size_t)p.nchunk * p.Mpad);
+  int64_t* rescue = cv.take<int64_t>((size_t)p.Mpad);
+  unsigned int* nres = cv.take<unsigned int>(64);
+  if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "mvn x3: workspace carve");
+  const Header* hdr = (const Header*)packed;
+  const half8* Aimg = (const half8*)((const char*)packed + HDR);
+  ABC_HIP(hipMemsetAsync(nres, 0, sizeof(unsigned int), s));
+  hipLaunchKernelGGL(pack_x3_kernel<1>, dim3((unsigned)ceil_div(p.MTpad * 16, 128)),
+                     dim3(128), 0, s, x, (const double*)nullptr, M, d, mu, U, r,
+                     0.0, p.KB0, p.KB, hdr, Bimg, p.MTpad, cflags);
+  ABC_LAUNCHED();
+  profile_start(s);
+  int rc = dispatch_x3(p, Aimg, (const half8*)Bimg, r + 6, po, pl, s);
+  profile_stop(s);
+  if (rc) return rc;
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(x3_combine_kernel, dim3((unsigned)ceil_div(M, 256)), dim3(256),
+                     0, s, po, pl, p.nchunk, M, p.Mpad, log_const, cflags, out,
+                     rescue, nres);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(x3_rescue_kernel, dim3(512), dim3(256), 0, s, rescue, nres,
+                     x, X, w, N, d, U, r, log_norm, out);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
+}  // namespace abc

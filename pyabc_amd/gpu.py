@@ -107,17 +107,21 @@ def normalize_weights(w):
 
 # ---- MultivariateNormalTransition -----------------------------------------
 
-def mvn_pack(X, w, mu, U, shift, prec):
+def mvn_pack(X, w, mu, U, shift, prec, with_range=False):
+    """Population operand image; with_range also returns the device range
+    [max |y_jk|, max |y_j|^2 / 2] (log2-scaled whitened units)."""
     N, d = X.shape
     r = U.shape[1]
     nb = nat.query("abc_mvn_packed_bytes", N, r, prec)
     packed = torch.empty(nb, dtype=torch.uint8, device=X.device)
+    rng = torch.zeros(2, dtype=F64, device=X.device) if with_range else None
     nat.call("abc_mvn_pack_population", p(X), p(w), N, d, p(mu), p(U), r,
-             float(shift), prec, p(packed), stream_ptr())
-    return packed
+             float(shift), prec, p(packed), p(rng), stream_ptr())
+    return (packed, rng) if with_range else packed
 
 
-def mvn_logpdf(x, packed, N, mu, U, prec, log_const, out=None):
+def mvn_logpdf(x, packed, N, mu, U, prec, log_const, out=None, X=None, w=None,
+               shift=0.0):
     M, d = x.shape
     r = U.shape[1]
     out = torch.empty(M, dtype=F64, device=x.device) if out is None else out
@@ -125,8 +129,9 @@ def mvn_logpdf(x, packed, N, mu, U, prec, log_const, out=None):
         return out
     nb = nat.query("abc_mvn_logpdf_workspace", M, N, r, prec)
     ws = workspace(nb, "mvn")
-    nat.call("abc_mvn_logpdf", p(x), M, d, p(packed), N, p(mu), p(U), r, prec,
-             float(log_const), p(out), p(ws), ws.numel(), stream_ptr())
+    nat.call("abc_mvn_logpdf", p(x), M, d, p(packed), p(X), p(w), N, p(mu),
+             p(U), r, prec, float(log_const), float(shift), p(out), p(ws),
+             ws.numel(), stream_ptr())
     return out
 
 

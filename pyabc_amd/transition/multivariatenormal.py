@@ -57,14 +57,21 @@ class MultivariateNormalTransition(Transition):
     """Transition via a multivariate Gaussian KDE (GPU).
 
     Parameters as in the reference (``scaling``, ``bandwidth_selector``), plus
-    ``precision``: "f64" (default; f64-MFMA cross term, parity mode) or "f32"
-    (f32-MFMA cross term, ~3e-5 relative density error at N=1e5, d=10).
+    ``precision`` of the transition-density kernel:
+
+    * "x3" (default): f16 MFMA on three-limb split operands with exact-grid
+      f32 accumulation -- f32-grade accuracy (~1e-7 relative) at the highest
+      throughput.  Populations outside its range (whitened norm beyond
+      ~200 kernel widths, rank > 25) use "f64" automatically.
+    * "f64": f64-MFMA cross term (2e-6 relative; the exp2 is f32).
+    * "f32": plain f32-MFMA cross term (~3e-5 relative at N=1e5, d=10).
     """
     MFMA_MAX_RANK = 59
+    X3_MAX_RANK = 25
 
     def __init__(self, scaling: float = 1,
                  bandwidth_selector: BandwidthSelector = silverman_rule_of_thumb,
-                 precision: str = "f64"):
+                 precision: str = "x3"):
         self.scaling = scaling
         self.bandwidth_selector = bandwidth_selector
         self.precision = precision
@@ -123,14 +130,28 @@ class MultivariateNormalTransition(Transition):
         self._rank = psd["rank"]
         self._support_tol = psd["tol"]
         self._log_norm = -0.5 * (psd["rank"] * gpu.LOG_2PI + psd["log_pdet"])
-        self._prec = nat.ABC_PREC_F32 if self.precision == "f32" else nat.ABC_PREC_F64
+        self._prec = {"f32": nat.ABC_PREC_F32, "f64": nat.ABC_PREC_F64,
+                      "x3": nat.ABC_PREC_X3}[self.precision]
         self._mfma = 1 <= psd["rank"] == d and psd["rank"] <= self.MFMA_MAX_RANK
-        self._shift = math.log(N)
-        if self._mfma:
+        if self._prec == nat.ABC_PREC_X3 and psd["rank"] > self.X3_MAX_RANK:
+            self._prec = nat.ABC_PREC_F64
+        self._dev_packed = None
+        if self._mfma and self._prec == nat.ABC_PREC_X3:
+            # exponents <= 0: shift by -log max w (one host read per fit)
+            self._shift = -math.log(float(wd.max().item()))
+            packed, rng = gpu.mvn_pack(Xd, wd, self._dev_mu, self._dev_U,
+                                       self._shift, self._prec, with_range=True)
+            # range = [max whitened norm, grid exponent E]; E <= 8 keeps the
+            # dropped limb products below 2^-19 (see abc_mvn_x3.hip)
+            ymax, E = rng.cpu().numpy()
+            if E <= 8:
+                self._dev_packed = packed
+            else:  # population too spread for the limb grid: fp64 MFMA
+                self._prec = nat.ABC_PREC_F64
+        if self._mfma and self._dev_packed is None:
+            self._shift = math.log(N)
             self._dev_packed = gpu.mvn_pack(Xd, wd, self._dev_mu, self._dev_U,
                                             self._shift, self._prec)
-        else:
-            self._dev_packed = None
         self._dev_flat_kind = gpu.as_dev(np.full(d, -1), dtype=gpu.torch.int32,
                                          device=dev)
         self._dev_flat_params = gpu.torch.zeros(4 * d, dtype=gpu.F64, device=dev)
@@ -143,7 +164,9 @@ class MultivariateNormalTransition(Transition):
         if self._mfma:
             return gpu.mvn_logpdf(xd, self._dev_packed, self._dev_X.shape[0],
                                   self._dev_mu, self._dev_U, self._prec,
-                                  self._log_norm - self._shift, out=out)
+                                  self._log_norm - self._shift, out=out,
+                                  X=self._dev_X, w=self._dev_w,
+                                  shift=self._shift)
         return gpu.mvn_logpdf_direct(xd, self._dev_X, self._dev_w, self._dev_U,
                                      self._dev_V, self._support_tol,
                                      self._log_norm, out=out)

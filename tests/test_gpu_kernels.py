@@ -37,7 +37,8 @@ MVN = ["d1_n1000", "d2_n500", "d10_n4096", "d3_unnorm_scaled"]
 
 
 @pytest.mark.parametrize("tag", MVN)
-@pytest.mark.parametrize("precision,rtol", [("f64", 2e-6), ("f32", 1e-4)])
+@pytest.mark.parametrize("precision,rtol", [("x3", 1e-6), ("f64", 2e-6),
+                                            ("f32", 1e-4)])
 def test_mvn_pdf_golden(dev, tag, precision, rtol):
     import pandas as pd
     from pyabc_amd.transition import MultivariateNormalTransition
@@ -86,14 +87,51 @@ def test_mvn_pdf_large_vs_oracle(dev):
     cols = [f"p{k}" for k in range(d)]
     t = MultivariateNormalTransition()
     t.fit(pd.DataFrame(X, columns=cols), w.copy())
+    assert t.precision == "x3" and t._prec == 2
     cand = t.rvs(4096).values
     ref = oracle.mvn_logpdf(cand[:200], X, w, t.cov)
     lp = t.logpdf_device(T(cand)).cpu().numpy()
-    np.testing.assert_allclose(np.exp(lp[:200] - ref), 1.0, rtol=2e-6)
+    np.testing.assert_allclose(np.exp(lp[:200] - ref), 1.0, rtol=1e-6)
+    t64 = MultivariateNormalTransition(precision="f64")
+    t64.fit(pd.DataFrame(X, columns=cols), w.copy())
+    lp64 = t64.logpdf_device(T(cand)).cpu().numpy()
+    np.testing.assert_allclose(np.exp(lp64[:200] - ref), 1.0, rtol=2e-6)
+    # all 4096: x3 against the f64-MFMA kernel
+    np.testing.assert_allclose(np.exp(lp - lp64), 1.0, rtol=3e-6)
     t32 = MultivariateNormalTransition(precision="f32")
     t32.fit(pd.DataFrame(X, columns=cols), w.copy())
     lp32 = t32.logpdf_device(T(cand)).cpu().numpy()
     np.testing.assert_allclose(np.exp(lp32 - lp), 1.0, rtol=1e-4)
+
+
+def test_mvn_x3_rescue_and_edges(dev):
+    """x3 kernel: candidates outside the limb range and candidates whose
+    density underflows are recomputed in fp64; zero weights; ragged sizes."""
+    import pandas as pd
+    from pyabc_amd.transition import MultivariateNormalTransition
+    rng = np.random.default_rng(11)
+    for N, d in [(1, 3), (17, 2), (1000, 5), (4099, 10)]:
+        X = rng.normal(0, 1, (N, d))
+        w = np.exp(rng.standard_normal(N))
+        if N > 10:
+            w[::7] = 0.0
+        w /= w.sum()
+        cols = [f"p{k}" for k in range(d)]
+        t = MultivariateNormalTransition()
+        t.fit(pd.DataFrame(X, columns=cols), w.copy())
+        near = X[rng.integers(0, N, 300)] + 0.5 * rng.standard_normal((300, d))
+        far = np.vstack([np.full(d, 40.0), np.full(d, -1e3),
+                         X[0] + 8.0 * np.sqrt(np.diag(t.cov)) * 12])
+        x = np.vstack([near, far])
+        lp = t.logpdf_device(T(x)).cpu().numpy()
+        ref = oracle.mvn_logpdf(x, X, w, t.cov)
+        ok = np.isfinite(ref)
+        assert (np.isfinite(lp) == ok).all()
+        if t._prec == 2:
+            np.testing.assert_allclose(np.exp(lp[:300] - ref[:300]), 1.0,
+                                       rtol=1e-6)
+        np.testing.assert_allclose(lp[300:][ok[300:]], ref[300:][ok[300:]],
+                                   rtol=1e-9)
 
 
 @pytest.mark.parametrize("tag,kw", [("k50", dict(k=50, k_fraction=None)),
