@@ -33,13 +33,18 @@ def _headers():
     return hs
 
 
+# per-file extra flags: the x3 kernel keeps its MFMA accumulators in VGPRs
+# (gfx950's unified register file) instead of AGPRs + v_accvgpr_read copies
+EXTRA = {"abc_mvn_x3.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def _compile(src):
     obj = os.path.join(OBJ, os.path.basename(src) + ".o")
     newest_dep = max([os.path.getmtime(src)] +
                      [os.path.getmtime(h) for h in _headers()])
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj, False
-    cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+    cmd = [HIPCC] + FLAGS + EXTRA.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

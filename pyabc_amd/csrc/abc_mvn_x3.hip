@@ -50,6 +50,7 @@
 // combine.  Candidates outside the norm bound, and candidates whose density
 // underflows 2^-60 relative to max w (all pairs beyond ~11 kernel widths),
 // are recomputed by the fp64 direct kernel (rescue list; empty in practice).
+#include <stdlib.h>
 #include "abc_common.h"
 
 namespace abc {
@@ -244,11 +245,18 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
 // blocks sharing a population chunk share one XCD's L2 (speed only).
 // Pass 1: block 0 only -> per-column max of s_hi -> integer offset o.
 // Pass 2: all blocks -> per lane, sum over its population rows of 2^(s - o).
+__device__ __forceinline__ float max3(float a, float b, float c) {
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+
 template <int KB, int CT>
 __global__ __launch_bounds__(256) void mvn_x3_kernel(
     const half8* __restrict__ A, const half8* __restrict__ Bi, int64_t MT,
     int64_t NT, int nchunk, int64_t tiles_per_chunk, int64_t ngroups, int koff,
-    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad) {
+    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad,
+    int mode) {
+  // mode (timing experiments only; results are wrong unless 0):
+  // 1 = pass 1 only, 2 = pass 2 only
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t bid = blockIdx.x;
@@ -271,24 +279,33 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
   }
   const int64_t t_begin = (int64_t)chunk * tiles_per_chunk;
   const int64_t t_end = t_begin + tiles_per_chunk < NT ? t_begin + tiles_per_chunk : NT;
+  const int64_t t_last = t_end - 1;
+  const half8* __restrict__ Al = A + lane;
+  auto tile = [&](int64_t t) { return (t < t_end ? t : t_last) * KB; };
 
-  // ---- pass 1: exact s_hi (offset slot still 0) -> column max -> o
+  // ---- pass 1: exact s_hi (offset slot still 0) -> column max -> o.
+  // Block-0 fragments through a ring of 4 registers (prefetch distance 4).
   float o[CT];
-  {
+  if (t_begin < t_end && mode != 2) {
     float mx[CT];
 #pragma unroll
     for (int c = 0; c < CT; ++c) mx[c] = -INFINITY;
-    half8 a0 = t_begin < t_end ? A[(t_begin * KB) * 64 + lane] : half8{};
-    for (int64_t t = t_begin; t < t_end; ++t) {
-      const int64_t tn = (t + 1 < t_end) ? t + 1 : t;
-      const half8 a0n = A[(tn * KB) * 64 + lane];
+    half8 ring[4];
 #pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-            a0, b[c][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        mx[c] = fmaxf(fmaxf(mx[c], fmaxf(acc[0], acc[1])), fmaxf(acc[2], acc[3]));
+    for (int u = 0; u < 4; ++u) ring[u] = Al[tile(t_begin + u) * 64];
+    for (int64_t t = t_begin; t < t_end; t += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (t + u < t_end) {
+#pragma unroll
+          for (int c = 0; c < CT; ++c) {
+            const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                ring[u], b[c][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            mx[c] = max3(max3(mx[c], acc[0], acc[1]), acc[2], acc[3]);
+          }
+        }
+        ring[u] = Al[tile(t + u + 4) * 64];
       }
-      a0 = a0n;
     }
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
@@ -297,43 +314,76 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
       o[c] = fmaxf(ceilf(cm), O_MIN);
       if (off_lane) b[c][0][off_j] = (_Float16)(-o[c]);
     }
+  } else {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) o[c] = O_MIN;
   }
 
-  // ---- pass 2: full limb-split GEMM, exp2, sums
+  if (mode == 1) {
+    if (lane < 16) part_l[(int64_t)chunk * Mpad + ct0 * 16 + lane] = o[0];
+    return;
+  }
+  // ---- pass 2: full limb-split GEMM, exp2, sums.  Two register buffers of
+  // population fragments (prefetch distance 2).  Work runs as a stream of
+  // (tile, c) units: the MFMA chain of unit u is issued next to the
+  // exp2/sum of unit u-1, so one wave keeps the MFMA and VALU pipes busy.
   double l64[CT];
+  float ls[CT];
 #pragma unroll
-  for (int c = 0; c < CT; ++c) l64[c] = 0.0;
-  half8 a[KB], an[KB];
-  if (t_begin < t_end) {
+  for (int c = 0; c < CT; ++c) { l64[c] = 0.0; ls[c] = 0.f; }
+  half8 a0[KB], a1[KB];
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb) a[kb] = A[(t_begin * KB + kb) * 64 + lane];
+  for (int kb = 0; kb < KB; ++kb) {
+    a0[kb] = Al[(tile(t_begin) + kb) * 64];
+    a1[kb] = Al[(tile(t_begin + 1) + kb) * 64];
   }
-  int64_t t = t_begin;
-  while (t < t_end) {
-    // f32 partial sums over at most 16 tiles (64 terms per lane), then fp64
-    float ls[CT];
+  auto chain = [&](const half8 (&a)[KB], int c) {
+    f32x4 r = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < CT; ++c) ls[c] = 0.f;
-    const int64_t t_stop = t + 16 < t_end ? t + 16 : t_end;
-    for (; t < t_stop; ++t) {
-      const int64_t tn = (t + 1 < t_end) ? t + 1 : t;
+    for (int kb = 0; kb < KB; ++kb)
+      r = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[kb], b[c][kb], r, 0, 0, 0);
+    return r;
+  };
+  auto expsum = [&](const f32x4& v) {
+    return (__builtin_amdgcn_exp2f(v[0]) + __builtin_amdgcn_exp2f(v[1])) +
+           (__builtin_amdgcn_exp2f(v[2]) + __builtin_amdgcn_exp2f(v[3]));
+  };
+  // one tile: units (t, 0..CT-1); `carry` is the last unit of the previous
+  // tile (c = CT-1), summed under the MFMAs of unit (t, 0)
+  auto do_tile = [&](const half8 (&a)[KB], f32x4& carry, bool has_carry) {
+    f32x4 prev = chain(a, 0);
+    if (has_carry) ls[CT - 1] += expsum(carry);
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) an[kb] = A[(tn * KB + kb) * 64 + lane];
-#pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[kb], b[c][kb], acc, 0, 0, 0);
-        ls[c] += (__builtin_amdgcn_exp2f(acc[0]) + __builtin_amdgcn_exp2f(acc[1])) +
-                 (__builtin_amdgcn_exp2f(acc[2]) + __builtin_amdgcn_exp2f(acc[3]));
-      }
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) a[kb] = an[kb];
+    for (int c = 1; c < CT; ++c) {
+      const f32x4 cur = chain(a, c);
+      ls[c - 1] += expsum(prev);
+      prev = cur;
     }
+    carry = prev;
+  };
+  f32x4 carry = {0.f, 0.f, 0.f, 0.f};
+  bool has_carry = false;
+  int nflush = 0;
+  for (int64_t t = t_begin; t < t_end; t += 2) {
+    do_tile(a0, carry, has_carry);
+    has_carry = true;
 #pragma unroll
-    for (int c = 0; c < CT; ++c) l64[c] += (double)ls[c];
+    for (int kb = 0; kb < KB; ++kb) a0[kb] = Al[(tile(t + 2) + kb) * 64];
+    if (t + 1 < t_end) {
+      do_tile(a1, carry, true);
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) a1[kb] = Al[(tile(t + 3) + kb) * 64];
+    }
+    // f32 partial sums over at most 16 tiles (64 terms per lane), then fp64
+    if (++nflush == 8) {
+      nflush = 0;
+#pragma unroll
+      for (int c = 0; c < CT; ++c) { l64[c] += (double)ls[c]; ls[c] = 0.f; }
+    }
   }
+  if (has_carry) ls[CT - 1] += expsum(carry);
+#pragma unroll
+  for (int c = 0; c < CT; ++c) l64[c] += (double)ls[c];
   // lanes l, l^16, l^32, l^48 hold the same candidate column (same o)
 #pragma unroll
   for (int c = 0; c < CT; ++c) {
@@ -467,13 +517,22 @@ size_t plan_x3_ws(const PlanX3& p) {
   return off + 256;
 }
 
+int debug_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("ABC_X3_DEBUG_MODE");
+    m = e ? atoi(e) : 0;
+  }
+  return m;
+}
+
 template <int KB, int CT>
 void launch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
                double* po, double* pl, hipStream_t s) {
   const int64_t blocks = p.groups * p.nchunk;
   hipLaunchKernelGGL((mvn_x3_kernel<KB, CT>), dim3((unsigned)blocks), dim3(256),
                      0, s, A, B, p.MT, p.NT, p.nchunk, p.tiles_per_chunk,
-                     p.groups, koff, po, pl, p.Mpad);
+                     p.groups, koff, po, pl, p.Mpad, debug_mode());
 }
 
 int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
