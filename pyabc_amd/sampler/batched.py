@@ -135,6 +135,8 @@ class BatchedGPUSampler(Sampler):
 
         acc_theta, acc_lp, acc_d, acc_x = [], [], [], []
         rec_x = []
+        keeps = []          # per round: accepted rows kept by each rank
+        rec_keeps = []      # per round: recorded rows of each rank
         n_acc = 0
         base = 0
         n_eval = 0
@@ -161,21 +163,19 @@ class BatchedGPUSampler(Sampler):
             keep = dd.cutoff(counts, n - n_acc)
             total_keep = int(keep.sum())
             k_mine = int(keep[rank])
-            # evaluations up to the cutoff (global order)
+            # evaluations up to the cutoff (global order); rec_all = recorded
+            # rows of every rank this round (identical on all ranks)
+            rec_all = np.full(ws, B, dtype=np.int64)
             if n_acc + total_keep >= n:
                 c_rank = int(np.nonzero(keep)[0][-1])
                 pos = self._local_cutoff_pos(idx, keep[c_rank]) if rank == c_rank else -1
                 pos = dd.allgather_counts(pos, dev)[c_rank]
                 evaluated = c_rank * B + pos + 1
-                if rank < c_rank:
-                    rec_rows = B
-                elif rank == c_rank:
-                    rec_rows = pos + 1
-                else:
-                    rec_rows = 0
+                rec_all[c_rank] = pos + 1
+                rec_all[c_rank + 1:] = 0
             else:
                 evaluated = ws * B
-                rec_rows = B
+            rec_rows = int(rec_all[rank])
             if k_mine:
                 sel = idx[:k_mine]
                 acc_theta.append(gpu.gather_rows(theta, sel))
@@ -183,7 +183,9 @@ class BatchedGPUSampler(Sampler):
                 acc_d.append(gpu.gather_rows(dist, sel))
                 acc_x.append(gpu.gather_rows(x, sel))
             if record:
-                rec_x.append(x[:rec_rows] if (not all_accepted) else x[:rec_rows])
+                rec_x.append(x[:rec_rows])
+                rec_keeps.append(rec_all)
+            keeps.append(keep)
             n_acc += total_keep
             n_eval += evaluated
             base += ws * B
@@ -196,12 +198,16 @@ class BatchedGPUSampler(Sampler):
         if n_acc < n:
             ok = False
         cols = self._assemble(spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
-                              all_accepted)
+                              all_accepted, keeps)
         recorded = None
         if record:
             recorded = gpu.torch.cat(rec_x, 0) if rec_x else None
             if ws > 1 and recorded is not None:
                 recorded = dd.allgather_rows(recorded, dev)
+                perm = self.global_order(rec_keeps)
+                if perm.size and np.any(perm != np.arange(perm.size)):
+                    recorded = gpu.gather_rows(
+                        recorded, gpu.torch.as_tensor(perm, device=dev))
         elif cols is not None:
             recorded = cols.sum_stats
         return ColumnarSample(cols, recorded, spec.sum_stat_keys,
@@ -222,8 +228,25 @@ class BatchedGPUSampler(Sampler):
                 generation=gen, idx0=lo, max_attempts=self.max_attempts)
         return th, lp
 
+    @staticmethod
+    def global_order(keeps):
+        """Permutation from the rank-major all-gather (rank 0's rows of every
+        round, then rank 1's, ...) to global candidate-index order (round
+        major, then rank), from the per-round keep counts [rounds x ranks]."""
+        k = np.asarray(keeps, dtype=np.int64).reshape(len(keeps), -1)
+        if k.size == 0:
+            return np.zeros(0, dtype=np.int64)
+        rank_start = np.concatenate([[0], np.cumsum(k.sum(0))[:-1]])
+        round_off = np.cumsum(k, axis=0) - k          # [rounds x ranks]
+        starts = (rank_start[None, :] + round_off).ravel()   # round-major
+        lens = k.ravel()
+        tot = int(lens.sum())
+        base = np.repeat(starts - np.concatenate([[0], np.cumsum(lens)[:-1]]),
+                         lens)
+        return base + np.arange(tot, dtype=np.int64)
+
     def _assemble(self, spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
-                  all_accepted):
+                  all_accepted, keeps):
         rank, ws = dd.world()
         torch = gpu.torch
         if acc_theta:
@@ -248,6 +271,16 @@ class BatchedGPUSampler(Sampler):
             w = dd.allgather_rows(w, dev)
             dist = dd.allgather_rows(dist, dev)
             x = dd.allgather_rows(x, dev)
+            # rows arrive rank-major; restore global candidate-index order so
+            # the population (and every later draw keyed on it) is the same
+            # for any number of ranks
+            perm = self.global_order(keeps)
+            if perm.size and np.any(perm != np.arange(perm.size)):
+                pd_ = torch.as_tensor(perm, device=dev)
+                theta = gpu.gather_rows(theta, pd_)
+                w = gpu.gather_rows(w, pd_)
+                dist = gpu.gather_rows(dist, pd_)
+                x = gpu.gather_rows(x, pd_)
         if theta.shape[0] == 0:
             return None
         return ColumnarParticles(theta.contiguous(), w.contiguous(),

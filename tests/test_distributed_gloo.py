@@ -1,0 +1,200 @@
+"""World-size-2 gloo tests of the candidate-sharded sampler (CPU, no GPU).
+
+The real ``BatchedGPUSampler.sample_until_n_accepted`` loop and the
+``sampler/distributed.py`` collectives run on two gloo ranks.  The per-stage
+device calls (propose, simulate, distance, compaction, gather, weights) are
+replaced -- in this test only -- by the oracle's replay of the same
+counter-based streams (``oracle/sampler.py``), so the sharded run must give
+exactly the population of the single-rank run: the first n accepted in global
+candidate-index order, with the same ``nr_evaluations_`` and the
+same recorded sum stats.  The product path never routes through these doubles
+(``gpu.require_device`` raises without a GPU).
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+import oracle.sampler as osamp
+
+D = 3
+SEED = 4242
+GEN = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class _Population:
+    def __init__(self):
+        rng = np.random.default_rng(3)
+        self.X = rng.normal(0.2, 1.0, (500, D))
+        w = np.exp(0.3 * rng.standard_normal(500))
+        self.w = w / w.sum()
+        self.L = np.linalg.cholesky(0.3 * np.eye(D) + 0.05)
+
+
+class _Transition:
+    """propose_device / logpdf_device doubles: oracle replay on CPU."""
+
+    def __init__(self, pop):
+        self.pop = pop
+        self.cov = pop.L @ pop.L.T
+
+    def propose_device(self, B, kind, params, seed, generation, idx0,
+                       max_attempts):
+        th, lp, _, _ = osamp.propose_mvn(self.pop.X, self.pop.w, self.pop.L,
+                                         seed, generation, idx0, B,
+                                         ["norm"] * D, np.tile([0, 1, 0, 0], (D, 1)))
+        return torch.from_numpy(th), torch.from_numpy(lp), None, None
+
+    def logpdf_device(self, theta):
+        return torch.from_numpy(oracle.mvn_logpdf(theta.numpy(), self.pop.X,
+                                                  self.pop.w, self.cov))
+
+
+class _Model:
+    def simulate_batch(self, theta, seed, gen, lo):
+        return torch.from_numpy(osamp.simulate_linear_gaussian(
+            theta.numpy(), np.arange(D), np.ones(D), np.full(D, 0.5), seed,
+            gen, lo))
+
+
+class _Distance:
+    def device_call(self, x, x0, t, keys):
+        return torch.from_numpy(oracle.pnorm(x.numpy(), x0.numpy()))
+
+
+class _Spec:
+    batched_capable = True
+
+    def __init__(self, eps):
+        pop = _Population()
+        self.t = GEN
+        self.param_names = [f"p{k}" for k in range(D)]
+        self.sum_stat_keys = [f"y{k}" for k in range(D)]
+        self.transition = _Transition(pop)
+        self.model = _Model()
+        self.distance = _Distance()
+        self.x0vec = torch.ones(D, dtype=torch.float64)
+        self.eps = eps
+        self.weight_scale = 1.0
+        self.prior_kind = None
+        self.prior_params = None
+
+
+def _install_cpu_doubles(monkeypatch_like):
+    from pyabc_amd.sampler import batched
+    g = batched.gpu
+
+    def accept_compact(d, eps):
+        idx = torch.nonzero(d <= eps).flatten().to(torch.int64)
+        return idx, torch.tensor(idx.numel())
+
+    def gather_rows(x, idx, n=None):
+        return x.index_select(0, idx)
+
+    def importance_weights(lp, lt, scale=1.0):
+        return torch.exp(lp - lt) * scale
+
+    monkeypatch_like(g, "require_device", lambda: torch.device("cpu"))
+    monkeypatch_like(g, "accept_compact", accept_compact)
+    monkeypatch_like(g, "gather_rows", gather_rows)
+    monkeypatch_like(g, "importance_weights", importance_weights)
+
+
+def _run(n, eps, batch, record):
+    from pyabc_amd.sampler import BatchedGPUSampler
+    s = BatchedGPUSampler(batch_size=batch, seed=SEED)
+    s.sample_factory.record_rejected = record
+    sample = s.sample_until_n_accepted(n, _Spec(eps))
+    c = sample._cols
+    rec = sample._recorded
+    return dict(theta=c.theta.numpy(), w=c.weights.numpy(),
+                d=c.distances.numpy(), x=c.sum_stats.numpy(),
+                n_eval=np.array(s.nr_evaluations_),
+                rec=(rec.numpy() if rec is not None else np.zeros(0)))
+
+
+def _worker(rank, ws, port, out_dir, n, eps, batch, record):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        _install_cpu_doubles(setattr)
+        res = _run(n, eps, batch, record)
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,batch,record", [(300, 256, True), (37, 64, False),
+                                            (1, 128, True)])
+def test_sharded_sampler_matches_single_rank(monkeypatch, n, batch, record):
+    eps = 1.6
+    _install_cpu_doubles(monkeypatch.setattr)
+    ref = _run(n, eps, batch * 2, record)   # 1 rank, same global round size
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_worker, args=(2, _free_port(), tmp, n, eps, batch,
+                                          record),
+                           nprocs=2, join=True, start_method="spawn")
+        for rank in range(2):
+            got = dict(np.load(os.path.join(tmp, f"r{rank}.npz")))
+            assert int(got["n_eval"]) == int(ref["n_eval"])
+            for k in ("theta", "w", "d", "x"):
+                assert got[k].shape[0] == n
+                np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+            if record:
+                np.testing.assert_array_equal(got["rec"], ref["rec"])
+    # the cutoff keeps exactly the first n accepted in global index order
+    assert np.all(ref["d"] <= eps)
+
+
+def _collective_worker(rank, ws, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        from pyabc_amd.sampler import distributed as dd
+        dev = torch.device("cpu")
+        assert dd.world() == (rank, ws)
+        counts = dd.allgather_counts(10 * rank + 3, dev)
+        rows = torch.full((rank + 1, 2), float(rank), dtype=torch.float64)
+        gathered = dd.allgather_rows(rows, dev)
+        empty = dd.allgather_rows(torch.zeros((0, 2), dtype=torch.float64), dev)
+        b = dd.broadcast_int(99 if rank == 0 else -1, dev)
+        np.savez(os.path.join(out_dir, f"c{rank}.npz"), counts=counts,
+                 gathered=gathered.numpy(), empty=np.array(empty.shape),
+                 b=np.array(b))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collectives_two_ranks():
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_collective_worker, args=(2, _free_port(), tmp),
+                           nprocs=2, join=True, start_method="spawn")
+        for rank in range(2):
+            r = np.load(os.path.join(tmp, f"c{rank}.npz"))
+            np.testing.assert_array_equal(r["counts"], [3, 13])
+            np.testing.assert_array_equal(r["gathered"],
+                                          [[0, 0], [1, 1], [1, 1]])
+            np.testing.assert_array_equal(r["empty"], [0, 2])
+            assert int(r["b"]) == 99
+
+
+def test_cutoff_prefix():
+    from pyabc_amd.sampler.distributed import cutoff, rank_range
+    np.testing.assert_array_equal(cutoff([5, 7, 2], 9), [5, 4, 0])
+    np.testing.assert_array_equal(cutoff([0, 0], 3), [0, 0])
+    np.testing.assert_array_equal(cutoff([4, 4], 8), [4, 4])
+    assert rank_range(100, 10, 3) == (130, 140)
