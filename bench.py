@@ -162,17 +162,33 @@ def main():
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
-    # warmup: calibration + W generations
-    abc.run(max_nr_populations=max(args.warmup, 1))
-    barrier()
-    n_before = len(abc.generation_log)
-    timer.begin()
-    t0 = time.perf_counter()
-    abc.run(max_nr_populations=args.steps)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    k_ms, k_n, k_flops, k_pairs = timer.end()
-    gens = abc.generation_log[n_before:]
+    # one run of W + K generations: calibration + W untimed warm-up
+    # generations, then EXACTLY K timed ones (each: sample until N accepted,
+    # importance weights, fit of the next transition, epsilon update),
+    # bracketed by barrier + synchronize, started/stopped from the
+    # per-generation hook so every timed generation is a genuine continuation
+    warm = max(args.warmup, 1)
+    clock = {}
+
+    def on_generation(t):
+        done = len(abc.generation_log)
+        if done == warm:
+            barrier()
+            timer.begin()
+            clock["n0"] = done
+            clock["t0"] = time.perf_counter()
+        elif done == warm + args.steps:
+            barrier()
+            clock["t1"] = time.perf_counter()
+            clock["kernel"] = timer.end()
+    abc.generation_callback = on_generation
+    abc.run(max_nr_populations=warm + args.steps)
+    if "t1" not in clock:
+        raise RuntimeError("run stopped before the timed generations finished")
+    elapsed = clock["t1"] - clock["t0"]
+    k_ms, k_n, k_flops, k_pairs = clock["kernel"]
+    n_before = clock["n0"]
+    gens = abc.generation_log[n_before:n_before + args.steps]
     steps = len(gens)
     t_local = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if ws > 1:

@@ -165,6 +165,9 @@ class ABCSMC:
         self.max_nr_populations = None
         self.min_acceptance_rate = None
         self.generation_log = []
+        # optional callable(t) run after each completed generation (timing
+        # hooks; not part of the reference API)
+        self.generation_callback = None
 
     def __getstate__(self):
         state = self.__dict__.copy()
@@ -462,6 +465,8 @@ class ABCSMC:
             self.generation_log.append(dict(
                 t=t, eps=float(current_eps), n_sim=int(n_sim), ess=float(ess),
                 seconds=(datetime.datetime.now() - t_start).total_seconds()))
+            if self.generation_callback is not None:
+                self.generation_callback(t)
             if current_eps <= minimum_epsilon:
                 logger.info("Stopping: minimum epsilon.")
                 break

@@ -3,8 +3,10 @@
 Reference: pyabc/storage/history.py:104-1229 (SQLAlchemy ORM, one row per
 particle / parameter / sum stat; SURVEY.md §8f row 1 ranks a faster writer as
 the next component after the hot path).  This store keeps every generation
-columnar: the latest population stays on the GPU (device tensors, no host
-round trip between generations) and older ones are moved to host numpy.
+columnar and HBM-resident: populations stay on the GPU as device tensors (no
+host round trip inside the generation loop) until the resident history
+exceeds ``History.DEVICE_BUDGET``; older ones then move to host numpy.  Host
+copies are made on first query only.
 The query methods ABCSMC and users need (get_distribution,
 get_model_probabilities, get_population, get_all_populations, max_t,
 total_nr_simulations, ...) return the reference's pandas shapes.  The
@@ -64,6 +66,21 @@ class _Gen:
                 model_probabilities=mp)
         return self.host
 
+    def model_probabilities(self):
+        pop = self.population
+        if self.host is None and pop is not None and pop.columns is not None:
+            return {pop.columns.m: 1.0}      # single-model columnar population
+        return self.to_host().get("model_probabilities") or {0: 1.0}
+
+    def device_bytes(self):
+        pop = self.population
+        if pop is None or pop.columns is None:
+            return 0
+        c = pop.columns
+        return sum(t.numel() * t.element_size()
+                   for t in (c.theta, c.weights, c.distances, c.sum_stats)
+                   if t is not None)
+
     def offload(self):
         """Drop the device copy once the generation is no longer needed."""
         self.to_host()
@@ -72,6 +89,10 @@ class _Gen:
 
 class History:
     PRE_TIME = -1
+
+    # generations stay in HBM (288 GB per MI355X) until the device-resident
+    # history exceeds this many bytes; then the oldest are moved to the host
+    DEVICE_BUDGET = 16 << 30
 
     def __init__(self, db: str = "sqlite://", stores_sum_stats: bool = True):
         self.db = db
@@ -104,10 +125,16 @@ class History:
                           model_names):
         self._gens[t] = _Gen(t, current_epsilon, nr_simulations, population,
                              model_names)
-        # keep only the newest generation on the device
-        for tt, g in self._gens.items():
-            if tt < t - 1 and g.population is not None:
-                g.offload()
+        # keep generations device-resident (no host round trip inside the
+        # generation loop); offload the oldest beyond the HBM budget
+        resident = sorted(tt for tt, g in self._gens.items()
+                          if g.population is not None)
+        used = sum(self._gens[tt].device_bytes() for tt in resident)
+        for tt in resident[:-2]:
+            if used <= self.DEVICE_BUDGET:
+                break
+            used -= self._gens[tt].device_bytes()
+            self._gens[tt].offload()
 
     def done(self):
         self.end_time = datetime.datetime.now()
@@ -178,8 +205,7 @@ class History:
         t = self.max_t if t is None else t
         if t not in self._gens:
             return pd.DataFrame({"p": []})
-        h = self._gens[t].to_host()
-        mp = h.get("model_probabilities") or {0: 1.0}
+        mp = self._gens[t].model_probabilities()
         return pd.DataFrame({"p": list(mp.values())}, index=list(mp.keys()))
 
     def alive_models(self, t=None):

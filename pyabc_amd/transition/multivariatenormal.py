@@ -231,7 +231,16 @@ class _LazyFrame:
     def __len__(self):
         return int(self._Xd.shape[0])
 
+    def __deepcopy__(self, memo):
+        # the device population is immutable after fit: share it, and do not
+        # materialise the host frame just to copy it
+        new = _LazyFrame(self._Xd, list(self.columns))
+        new._df = self._df
+        return new
+
     def __getattr__(self, item):
+        if item.startswith("__"):
+            raise AttributeError(item)
         return getattr(self._frame(), item)
 
     def __getitem__(self, item):
@@ -251,6 +260,11 @@ class _LazyArray:
     def __len__(self):
         return int(self._wd.shape[0])
 
+    def __deepcopy__(self, memo):
+        new = _LazyArray(self._wd)
+        new._a = self._a
+        return new
+
     @property
     def size(self):
         return int(self._wd.numel())
@@ -264,6 +278,8 @@ class _LazyArray:
         return a if dtype is None else a.astype(dtype)
 
     def __getattr__(self, item):
+        if item.startswith("__"):
+            raise AttributeError(item)
         return getattr(self._arr(), item)
 
     def __getitem__(self, item):
