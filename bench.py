@@ -74,11 +74,11 @@ class KernelTimer:
         self.active = False
         orig = transition.logpdf_device
 
-        def logged(xd, out=None):
+        def logged(xd, out=None, hint=None):
             if self.active and getattr(transition, "_mfma", False):
                 self.shapes.append((xd.shape[0], transition._dev_X.shape[0],
                                     xd.shape[1]))
-            return orig(xd, out=out)
+            return orig(xd, out=out, hint=hint)
         transition.logpdf_device = logged
 
     def begin(self):

@@ -99,10 +99,17 @@ int abc_normalize_weights(double* w, int64_t N, double* stats, void* ws,
  * F64 otherwise).
  * logpdf: out[i] = log(sum_j w_j exp(-|(x_i - X_j) U|^2 / 2)) + log_const,
  *   log_const = -(r log 2pi + log pdet)/2 - log_w_shift.  prec selects the
- *   f64-MFMA, f32-MFMA or limb-split f16-MFMA (X3) kernel.  X3 also needs the
- *   fp64 population X, w: candidates outside its range (or whose density
- *   underflows 2^-60 relative to max w) are recomputed by the fp64 direct
- *   kernel on the device.  r <= 59 (X3: r <= 25). */
+ *   f64-MFMA, f32-MFMA or limb-split f16-MFMA (X3) kernel.  The X3 image
+ *   also stores the fp64 whitened population and log2 weights: candidates
+ *   outside its range (or whose density underflows 2^-60 relative to max w)
+ *   are recomputed from them in fp64 on the device (X, w may be NULL for
+ *   X3).  r <= 59 (X3: r <= 25).
+ *   hint_rows (device int64 [M], nullable; X3 only): for each candidate a
+ *   population row near it -- the proposal's ancestor in the sampler.  Its
+ *   exact fp64 log-kernel value becomes the candidate's exponent offset, which
+ *   replaces the X3 kernel's max pre-pass over the population (a quarter of
+ *   its MFMA work).  Invalid rows (outside [0, N) or w <= 0) send the
+ *   candidate to the fp64 rescue path. */
 size_t abc_mvn_packed_bytes(int64_t N, int r, int prec);
 int abc_mvn_pack_population(const double* X, const double* w, int64_t N, int d,
                             const double* mu, const double* U, int r,
@@ -112,8 +119,9 @@ size_t abc_mvn_logpdf_workspace(int64_t M, int64_t N, int r, int prec);
 int abc_mvn_logpdf(const double* x, int64_t M, int d, const void* packed,
                    const double* X, const double* w, int64_t N,
                    const double* mu, const double* U, int r, int prec,
-                   double log_const, double log_w_shift, double* out, void* ws,
-                   size_t ws_bytes, void* stream);
+                   double log_const, double log_w_shift, double* out,
+                   const int64_t* hint_rows, void* ws, size_t ws_bytes,
+                   void* stream);
 /* Direct-difference fp64 VALU path: any r, and scipy's singular-covariance
  * support mask (pairs with |(x_i - X_j) V| >= support_tol get density 0;
  * V [d x nv] null-space basis, nv = d - r). */

@@ -36,7 +36,7 @@ SIGNATURES = {
                                       P]),
     "abc_mvn_logpdf_workspace": (SZ, [I64, I64, I32, I32]),
     "abc_mvn_logpdf": (I32, [P, I64, I32, P, P, P, I64, P, P, I32, I32, D, D,
-                             P, P, SZ, P]),
+                             P, P, P, SZ, P]),
     "abc_mvn_logpdf_direct": (I32, [P, I64, P, P, I64, I32, P, I32, P, I32,
                                     D, D, P, P]),
     "abc_propose": (I32, [P, P, I64, I32, P, P, P, U64, U32, I64, I64, I32,

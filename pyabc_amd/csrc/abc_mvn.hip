@@ -390,7 +390,8 @@ size_t x3_logpdf_workspace(int64_t M, int64_t N, int r);
 int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
               const double* X, const double* w, int64_t N, const double* mu,
               const double* U, int r, double log_const, double log_norm,
-              double* out, void* ws, size_t ws_bytes, hipStream_t s);
+              double* out, const int64_t* hint, void* ws, size_t ws_bytes,
+              hipStream_t s);
 }  // namespace abc
 
 using namespace abc;
@@ -441,8 +442,8 @@ extern "C" int abc_mvn_logpdf(const double* x, int64_t M, int d,
                               const double* w, int64_t N, const double* mu,
                               const double* U, int r, int prec,
                               double log_const, double log_w_shift,
-                              double* out, void* ws, size_t ws_bytes,
-                              void* stream) {
+                              double* out, const int64_t* hint_rows, void* ws,
+                              size_t ws_bytes, void* stream) {
   ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= 64, "logpdf: bad M/N/d");
   ABC_CHECK_ARG(r >= 1 && r <= 59, "logpdf: rank r=%d outside [1, 59]", r);
   ABC_CHECK_ARG(prec == ABC_PREC_F32 || prec == ABC_PREC_F64 || prec == ABC_PREC_X3,
@@ -451,7 +452,8 @@ extern "C" int abc_mvn_logpdf(const double* x, int64_t M, int d,
   ABC_CHECK_ARG(x && packed && mu && U && out, "logpdf: null pointer");
   if (prec == ABC_PREC_X3)
     return x3_logpdf(x, M, d, packed, X, w, N, mu, U, r, log_const,
-                     log_const + log_w_shift, out, ws, ws_bytes, as_stream(stream));
+                     log_const + log_w_shift, out, hint_rows, ws, ws_bytes,
+                     as_stream(stream));
   Plan p = make_plan(M, N, r, prec);
   if (ws_bytes < plan_ws(p))
     return set_error(ABC_ERR_WORKSPACE, "logpdf: workspace %zu < %zu", ws_bytes, plan_ws(p));

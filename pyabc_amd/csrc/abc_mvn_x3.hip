@@ -49,7 +49,8 @@
 // the sum over the population stays in registers until a final 4-lane
 // combine.  Candidates outside the norm bound, and candidates whose density
 // underflows 2^-60 relative to max w (all pairs beyond ~11 kernel widths),
-// are recomputed by the fp64 direct kernel (rescue list; empty in practice).
+// are recomputed in fp64 from the whitened population Y and log2 weights lw
+// stored after the fragments (rescue list; empty in practice).
 #include <stdlib.h>
 #include "abc_common.h"
 
@@ -200,7 +201,11 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
     const double* __restrict__ P, const double* __restrict__ w, int64_t n,
     int d, const double* __restrict__ mu, const double* __restrict__ U, int r,
     double log_w_shift, int KB0, int KB, const Header* __restrict__ hdr,
-    _Float16* __restrict__ img, int64_t ntiles, int32_t* __restrict__ flags) {
+    _Float16* __restrict__ img, int64_t ntiles, int32_t* __restrict__ flags,
+    double* __restrict__ Y, double* __restrict__ lw, int64_t Np,
+    const int64_t* __restrict__ hint, float* __restrict__ cand_o, int koff) {
+  // SIDE 0 writes the fp64 whitened population Y [n x r] and its log2
+  // weights lw [n] (rescue + hints); SIDE 1 reads them for the hint rows
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= ntiles * 16) return;
   const int E = hdr->E;
@@ -210,21 +215,40 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
   Limbs3 L[MAX_R];
   double scalar = SIDE == 0 ? -L2 : 0.0;  // padding: c = -2^(2E), m = 0
   bool bad = false;
+  float hint_o = O_MIN;
   for (int k = 0; k < r; ++k) v[k] = 0.0;
   if (row < n) {
     const double h = whiten(P, row, d, mu, U, r, v);
     if (SIDE == 0) {
       const double wj = w[row];
       bad = !(wj > 0.0) || !(2.0 * h <= L2);
-      scalar = bad ? -L2 : fmax((log(wj) + log_w_shift) * LOG2E - h, -L2);
+      const double lwj = wj > 0.0 ? (log(wj) + log_w_shift) * LOG2E : -INFINITY;
+      scalar = bad ? -L2 : fmax(lwj - h, -L2);
+      for (int k = 0; k < r; ++k) Y[row * r + k] = v[k];
+      lw[row] = lwj;
     } else {
       bad = !ok || !(2.0 * h <= L2);
       scalar = bad ? -L2 : -h;
+      if (hint && !bad) {
+        // offset from the hint row j (the proposal's ancestor): the exact
+        // fp64 exponent s_ij = log2e (log w_j + shift) - |z_i - y_j|^2 / 2,
+        // rounded up to an integer, replaces the max pre-pass
+        const int64_t j = hint[row];
+        if (j < 0 || j >= Np || !(lw[j] > -INFINITY)) {
+          bad = true;
+        } else {
+          double q = 0.0;
+          for (int k = 0; k < r; ++k) { const double t = v[k] - Y[j * r + k]; q += t * t; }
+          hint_o = (float)fmax(ceil(lw[j] - 0.5 * q), (double)O_MIN);
+        }
+        scalar = bad ? -L2 : -h;
+      }
     }
     if (bad)
       for (int k = 0; k < r; ++k) v[k] = 0.0;
   }
   if (flags && row < n) flags[row] = bad ? 1 : 0;
+  if (cand_o) cand_o[row] = hint_o;
   for (int k = 0; k < r; ++k) L[k] = split_coord(v[k], E);
   const Limbs5 S = split_scalar(scalar, E);
   const int64_t t = row >> 4;
@@ -236,6 +260,11 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
     const int kb = k >> 5, kk = k & 31;
     const int lane = rl + 16 * (kk >> 3), j = kk & 7;
     img[(((t * KB + kb) * 64) + lane) * 8 + j] = (_Float16)val;
+  }
+  if (SIDE == 1 && hint) {  // B = -o in the offset slot (A = 1)
+    const int kb = koff >> 5, kk = koff & 31;
+    const int lane = rl + 16 * (kk >> 3), j = kk & 7;
+    img[(((t * KB + kb) * 64) + lane) * 8 + j] = (_Float16)(-hint_o);
   }
 }
 
@@ -249,7 +278,7 @@ __device__ __forceinline__ float max3(float a, float b, float c) {
   return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
 
-template <int KB, int CT>
+template <int KB, int CT, bool PASS1>
 __global__ __launch_bounds__(256) void mvn_x3_kernel(
     const half8* __restrict__ A, const half8* __restrict__ Bi, int64_t MT,
     int64_t NT, int nchunk, int64_t tiles_per_chunk, int64_t ngroups, int koff,
@@ -286,7 +315,7 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
   // ---- pass 1: exact s_hi (offset slot still 0) -> column max -> o.
   // Block-0 fragments through a ring of 4 registers (prefetch distance 4).
   float o[CT];
-  if (t_begin < t_end && mode != 2) {
+  if (PASS1 && t_begin < t_end && mode != 2) {
     float mx[CT];
 #pragma unroll
     for (int c = 0; c < CT; ++c) mx[c] = -INFINITY;
@@ -392,7 +421,7 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
     v += __shfl_xor(v, 32, 64);
     const int64_t ct = ct0 + c;
     if (lane < 16 && ct < MT) {
-      part_o[(int64_t)chunk * Mpad + ct * 16 + lane] = (double)o[c];
+      if (PASS1) part_o[(int64_t)chunk * Mpad + ct * 16 + lane] = (double)o[c];
       part_l[(int64_t)chunk * Mpad + ct * 16 + lane] = v;
     }
   }
@@ -402,23 +431,32 @@ __global__ void x3_combine_kernel(const double* __restrict__ part_o,
                                   const double* __restrict__ part_l, int nchunk,
                                   int64_t M, int64_t Mpad, double log_const,
                                   const int32_t* __restrict__ cflags,
+                                  const float* __restrict__ cand_o,
                                   double* __restrict__ out,
                                   int64_t* __restrict__ rescue,
                                   unsigned int* __restrict__ nrescue) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M) return;
   double om = -INFINITY;
-  for (int c = 0; c < nchunk; ++c)
-    if (part_l[(int64_t)c * Mpad + i] > 0.0) om = fmax(om, part_o[(int64_t)c * Mpad + i]);
   double s = 0.0;
-  for (int c = 0; c < nchunk; ++c) {
-    const double l = part_l[(int64_t)c * Mpad + i];
-    if (l > 0.0) s += l * exp2(part_o[(int64_t)c * Mpad + i] - om);
+  if (cand_o) {  // one offset per candidate (hinted launch): plain sum
+    om = (double)cand_o[i];
+    for (int c = 0; c < nchunk; ++c) s += part_l[(int64_t)c * Mpad + i];
+  } else {
+    for (int c = 0; c < nchunk; ++c)
+      if (part_l[(int64_t)c * Mpad + i] > 0.0) om = fmax(om, part_o[(int64_t)c * Mpad + i]);
+    for (int c = 0; c < nchunk; ++c) {
+      const double l = part_l[(int64_t)c * Mpad + i];
+      if (l > 0.0) s += l * exp2(part_o[(int64_t)c * Mpad + i] - om);
+    }
   }
   const double lg = om + log2(s);  // log2 of sum_j 2^s_ij
   // below 2^-60 (relative to max w) terms flushed at the f32 exp2 floor
   // could matter: recompute in fp64
-  if (cflags[i] || !(s > 0.0) || !(lg >= -60.0)) {
+  // hinted offsets: the dominant terms round at 2^-24 |s - o| <= 2^-24
+  // (lg - om); beyond lg - om > 20 (offset far below the true maximum, or
+  // > 2^20 comparable terms) recompute in fp64 too
+  if (cflags[i] || !(s > 0.0) || !(lg >= -60.0) || (cand_o && lg - om > 20.0)) {
     const unsigned int q = atomicAdd(nrescue, 1u);
     rescue[q] = i;
     out[i] = -INFINITY;
@@ -427,42 +465,50 @@ __global__ void x3_combine_kernel(const double* __restrict__ part_o,
   out[i] = log_const + LN2 * lg;
 }
 
-// fp64 direct difference for the rescue list (full-rank U, no support mask):
-// log( sum_j w_j exp(-|(x_i - X_j) U|^2 / 2) ) + log_norm.
+// fp64 rescue of the listed candidates over the stored whitened population:
+// s_ij = lw_j - |z_i - y_j|^2 / 2 (log2 units, the same s as the MFMA path).
+// Grid (slice, candidate slot): block (sx, cy) takes candidates cy, cy + gy,
+// ... and population rows of slice sx; (max, sum) partials go to pm / pl
+// [slice][q] (the main kernel's partial arrays, free again after combine).
 __global__ __launch_bounds__(256) void x3_rescue_kernel(
     const int64_t* __restrict__ rescue, const unsigned int* __restrict__ nrescue,
-    const double* __restrict__ x, const double* __restrict__ X,
-    const double* __restrict__ w, int64_t N, int d,
-    const double* __restrict__ U, int r, double log_norm,
-    double* __restrict__ out) {
+    const double* __restrict__ x, int d, const double* __restrict__ mu,
+    const double* __restrict__ U, int r, const double* __restrict__ Y,
+    const double* __restrict__ lw, int64_t N, double* __restrict__ pm,
+    double* __restrict__ pl, int64_t Mpad) {
+  __shared__ double z[MAX_R];
   __shared__ double sm[4], sl[4];
   const unsigned int n = *nrescue;
-  for (unsigned int q = blockIdx.x; q < n; q += gridDim.x) {
+  const int64_t per = (N + gridDim.x - 1) / gridDim.x;
+  const int64_t j0 = (int64_t)blockIdx.x * per;
+  const int64_t j1 = j0 + per < N ? j0 + per : N;
+  for (unsigned int q = blockIdx.y; q < n; q += gridDim.y) {
     const int64_t i = rescue[q];
-    double xi[64];
-    for (int k = 0; k < d; ++k) xi[k] = x[i * d + k];
+    if (threadIdx.x < r) {
+      const int k = threadIdx.x;
+      double acc = 0.0;
+      for (int c = 0; c < d; ++c) acc += (x[i * d + c] - mu[c]) * U[c * r + k];
+      z[k] = acc * SQRT_LOG2E;
+    }
+    __syncthreads();
     double m = -INFINITY, l = 0.0;
-    for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
-      const double wj = w[j];
-      if (!(wj > 0.0)) continue;
-      double maha = 0.0;
-      for (int k = 0; k < r; ++k) {
-        double p = 0.0;
-        for (int c = 0; c < d; ++c) p += (xi[c] - X[j * d + c]) * U[c * r + k];
-        maha += p * p;
-      }
-      const double s = log(wj) - 0.5 * maha;
-      if (s > m) { l = l * exp(m - s) + 1.0; m = s; }
-      else l += exp(s - m);
+    for (int64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
+      const double lwj = lw[j];
+      if (!(lwj > -INFINITY)) continue;
+      double q2 = 0.0;
+      for (int k = 0; k < r; ++k) { const double t = z[k] - Y[j * r + k]; q2 += t * t; }
+      const double sj = lwj - 0.5 * q2;
+      if (sj > m) { l = l * exp2(m - sj) + 1.0; m = sj; }
+      else l += exp2(sj - m);
     }
     for (int o = 32; o > 0; o >>= 1) {
       const double mo = __shfl_xor(m, o, 64), lo = __shfl_xor(l, o, 64);
       const double mx = fmax(m, mo);
-      double s = 0.0;
-      if (l > 0.0) s += l * exp(m - mx);
-      if (lo > 0.0) s += lo * exp(mo - mx);
+      double t = 0.0;
+      if (l > 0.0) t += l * exp2(m - mx);
+      if (lo > 0.0) t += lo * exp2(mo - mx);
       m = (l > 0.0 || lo > 0.0) ? mx : m;
-      l = s;
+      l = t;
     }
     const int wv = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) { sm[wv] = m; sl[wv] = l; }
@@ -470,12 +516,31 @@ __global__ __launch_bounds__(256) void x3_rescue_kernel(
     if (threadIdx.x == 0) {
       double mx = -INFINITY;
       for (int k = 0; k < 4; ++k) if (sl[k] > 0.0) mx = fmax(mx, sm[k]);
-      double s = 0.0;
-      for (int k = 0; k < 4; ++k) if (sl[k] > 0.0) s += sl[k] * exp(sm[k] - mx);
-      out[i] = (s > 0.0) ? mx + log(s) + log_norm : -INFINITY;
+      double t = 0.0;
+      for (int k = 0; k < 4; ++k) if (sl[k] > 0.0) t += sl[k] * exp2(sm[k] - mx);
+      pm[(int64_t)blockIdx.x * Mpad + q] = mx;
+      pl[(int64_t)blockIdx.x * Mpad + q] = t;
     }
     __syncthreads();
   }
+}
+
+__global__ void x3_rescue_final(const int64_t* __restrict__ rescue,
+                                const unsigned int* __restrict__ nrescue,
+                                int nslice, const double* __restrict__ pm,
+                                const double* __restrict__ pl, int64_t Mpad,
+                                double log_const, double* __restrict__ out) {
+  const unsigned int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= *nrescue) return;
+  double mx = -INFINITY;
+  for (int c = 0; c < nslice; ++c)
+    if (pl[(int64_t)c * Mpad + q] > 0.0) mx = fmax(mx, pm[(int64_t)c * Mpad + q]);
+  double t = 0.0;
+  for (int c = 0; c < nslice; ++c) {
+    const double l = pl[(int64_t)c * Mpad + q];
+    if (l > 0.0) t += l * exp2(pm[(int64_t)c * Mpad + q] - mx);
+  }
+  out[rescue[q]] = t > 0.0 ? log_const + LN2 * (mx + log2(t)) : -INFINITY;
 }
 
 struct PlanX3 {
@@ -510,6 +575,7 @@ size_t plan_x3_ws(const PlanX3& p) {
   size_t off = 0;
   size_only<_Float16>(off, (size_t)p.MTpad * p.KB * 64 * 8);  // candidate image
   size_only<int32_t>(off, (size_t)p.Mpad);                     // candidate flags
+  size_only<float>(off, (size_t)p.Mpad);                       // hinted offsets
   size_only<double>(off, (size_t)p.nchunk * p.Mpad);           // partial offsets
   size_only<double>(off, (size_t)p.nchunk * p.Mpad);           // partial sums
   size_only<int64_t>(off, (size_t)p.Mpad);                     // rescue list
@@ -528,21 +594,28 @@ int debug_mode() {
 
 template <int KB, int CT>
 void launch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
-               double* po, double* pl, hipStream_t s) {
+               double* po, double* pl, bool pass1, hipStream_t s) {
   const int64_t blocks = p.groups * p.nchunk;
-  hipLaunchKernelGGL((mvn_x3_kernel<KB, CT>), dim3((unsigned)blocks), dim3(256),
-                     0, s, A, B, p.MT, p.NT, p.nchunk, p.tiles_per_chunk,
-                     p.groups, koff, po, pl, p.Mpad, debug_mode());
+  if (pass1)
+    hipLaunchKernelGGL((mvn_x3_kernel<KB, CT, true>), dim3((unsigned)blocks),
+                       dim3(256), 0, s, A, B, p.MT, p.NT, p.nchunk,
+                       p.tiles_per_chunk, p.groups, koff, po, pl, p.Mpad,
+                       debug_mode());
+  else
+    hipLaunchKernelGGL((mvn_x3_kernel<KB, CT, false>), dim3((unsigned)blocks),
+                       dim3(256), 0, s, A, B, p.MT, p.NT, p.nchunk,
+                       p.tiles_per_chunk, p.groups, koff, po, pl, p.Mpad,
+                       debug_mode());
 }
 
 int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
-                double* po, double* pl, hipStream_t s) {
+                double* po, double* pl, bool pass1, hipStream_t s) {
   switch (p.KB) {
-    case 2: launch_x3<2, 8>(p, A, B, koff, po, pl, s); break;
-    case 3: launch_x3<3, 8>(p, A, B, koff, po, pl, s); break;
-    case 4: launch_x3<4, 4>(p, A, B, koff, po, pl, s); break;
-    case 5: launch_x3<5, 4>(p, A, B, koff, po, pl, s); break;
-    case 6: launch_x3<6, 4>(p, A, B, koff, po, pl, s); break;
+    case 2: launch_x3<2, 8>(p, A, B, koff, po, pl, pass1, s); break;
+    case 3: launch_x3<3, 8>(p, A, B, koff, po, pl, pass1, s); break;
+    case 4: launch_x3<4, 4>(p, A, B, koff, po, pl, pass1, s); break;
+    case 5: launch_x3<5, 4>(p, A, B, koff, po, pl, pass1, s); break;
+    case 6: launch_x3<6, 4>(p, A, B, koff, po, pl, pass1, s); break;
     default:
       return set_error(ABC_ERR_UNSUPPORTED, "mvn x3: KB=%d unsupported", p.KB);
   }
@@ -552,10 +625,21 @@ int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
 }  // namespace
 
 // ---- internal entry points used by abc_mvn.hip ------------------------------
-size_t x3_packed_bytes(int64_t N, int r) {
+// image = header | fragments [NT][KB][64][8] f16 | Y [N x r] f64 | lw [N] f64
+size_t x3_frag_bytes(int64_t N, int r) {
   const int KB = x3_kb0(r) + x3_kb12(r);
   const int64_t NT = ceil_div(N > 0 ? N : 1, 16);
-  return HDR + (size_t)NT * KB * 64 * 8 * sizeof(_Float16);
+  return align_up((size_t)NT * KB * 64 * 8 * sizeof(_Float16), 256);
+}
+double* x3_Y(const void* packed, int64_t N, int r) {
+  return (double*)((char*)packed + HDR + x3_frag_bytes(N, r));
+}
+double* x3_lw(const void* packed, int64_t N, int r) {
+  return x3_Y(packed, N, r) + align_up((size_t)(N > 0 ? N : 1) * r, 32);
+}
+size_t x3_packed_bytes(int64_t N, int r) {
+  return HDR + x3_frag_bytes(N, r) +
+         sizeof(double) * (align_up((size_t)(N > 0 ? N : 1) * r, 32) + (N > 0 ? N : 1));
 }
 
 int x3_max_rank() { return MAX_R; }
@@ -579,7 +663,9 @@ int x3_pack_population(const double* X, const double* w, int64_t N, int d,
   hipLaunchKernelGGL(pack_x3_kernel<0>, dim3((unsigned)ceil_div(NT * 16, 128)),
                      dim3(128), 0, s, X, w, N, d, mu, U, r, log_w_shift,
                      x3_kb0(r), x3_kb0(r) + x3_kb12(r), (const Header*)hdr,
-                     (_Float16*)((char*)packed + HDR), NT, (int32_t*)nullptr);
+                     (_Float16*)((char*)packed + HDR), NT, (int32_t*)nullptr,
+                     x3_Y(packed, N, r), x3_lw(packed, N, r), N,
+                     (const int64_t*)nullptr, (float*)nullptr, 0);
   ABC_LAUNCHED();
   return ABC_OK;
 }
@@ -591,11 +677,10 @@ size_t x3_logpdf_workspace(int64_t M, int64_t N, int r) {
 int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
               const double* X, const double* w, int64_t N, const double* mu,
               const double* U, int r, double log_const, double log_norm,
-              double* out, void* ws, size_t ws_bytes, hipStream_t s) {
+              double* out, const int64_t* hint, void* ws, size_t ws_bytes,
+              hipStream_t s) {
   if (r > MAX_R)
     return set_error(ABC_ERR_UNSUPPORTED, "mvn x3: rank %d > %d", r, MAX_R);
-  if (!X || !w)
-    return set_error(ABC_ERR_INVALID, "mvn x3: X and w are needed (rescue path)");
   PlanX3 p = make_plan_x3(M, N, r);
   if (ws_bytes < plan_x3_ws(p))
     return set_error(ABC_ERR_WORKSPACE, "mvn x3: workspace %zu < %zu", ws_bytes,
@@ -603,6 +688,7 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
   Carver cv(ws, ws_bytes);
   _Float16* Bimg = cv.take<_Float16>((size_t)p.MTpad * p.KB * 64 * 8);
   int32_t* cflags = cv.take<int32_t>((size_t)p.Mpad);
+  float* cand_o = cv.take<float>((size_t)p.Mpad);
   double* po = cv.take<double>((size_t)p.nchunk * p.Mpad);
   double* pl = cv.take<double>((size_t)p.nchunk * p.Mpad);
   int64_t* rescue = cv.take<int64_t>((size_t)p.Mpad);
@@ -613,19 +699,28 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
   ABC_HIP(hipMemsetAsync(nres, 0, sizeof(unsigned int), s));
   hipLaunchKernelGGL(pack_x3_kernel<1>, dim3((unsigned)ceil_div(p.MTpad * 16, 128)),
                      dim3(128), 0, s, x, (const double*)nullptr, M, d, mu, U, r,
-                     0.0, p.KB0, p.KB, hdr, Bimg, p.MTpad, cflags);
+                     log_norm - log_const, p.KB0, p.KB, hdr, Bimg, p.MTpad, cflags,
+                     x3_Y(packed, N, r), x3_lw(packed, N, r), N, hint,
+                     hint ? cand_o : (float*)nullptr, r + 6);
   ABC_LAUNCHED();
   profile_start(s);
-  int rc = dispatch_x3(p, Aimg, (const half8*)Bimg, r + 6, po, pl, s);
+  int rc = dispatch_x3(p, Aimg, (const half8*)Bimg, r + 6, po, pl, hint == nullptr, s);
   profile_stop(s);
   if (rc) return rc;
   ABC_LAUNCHED();
   hipLaunchKernelGGL(x3_combine_kernel, dim3((unsigned)ceil_div(M, 256)), dim3(256),
-                     0, s, po, pl, p.nchunk, M, p.Mpad, log_const, cflags, out,
+                     0, s, po, pl, p.nchunk, M, p.Mpad, log_const, cflags,
+                     hint ? (const float*)cand_o : (const float*)nullptr, out,
                      rescue, nres);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(x3_rescue_kernel, dim3(512), dim3(256), 0, s, rescue, nres,
-                     x, X, w, N, d, U, r, log_norm, out);
+  const int gy = (int)(2048 / p.nchunk > 1 ? 2048 / p.nchunk : 1);
+  hipLaunchKernelGGL(x3_rescue_kernel, dim3((unsigned)p.nchunk, (unsigned)gy),
+                     dim3(256), 0, s, rescue, nres, x, d, mu, U, r,
+                     (const double*)x3_Y(packed, N, r),
+                     (const double*)x3_lw(packed, N, r), N, po, pl, p.Mpad);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(x3_rescue_final, dim3((unsigned)ceil_div(M, 256)), dim3(256),
+                     0, s, rescue, nres, p.nchunk, po, pl, p.Mpad, log_const, out);
   ABC_LAUNCHED();
   return ABC_OK;
 }

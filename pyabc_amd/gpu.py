@@ -121,17 +121,23 @@ def mvn_pack(X, w, mu, U, shift, prec, with_range=False):
 
 
 def mvn_logpdf(x, packed, N, mu, U, prec, log_const, out=None, X=None, w=None,
-               shift=0.0):
+               shift=0.0, hint=None):
+    """hint: optional device int64 [M] population rows near the candidates
+    (the proposal's ancestors; X3 skips its max pre-pass)."""
     M, d = x.shape
     r = U.shape[1]
     out = torch.empty(M, dtype=F64, device=x.device) if out is None else out
     if M == 0:
         return out
+    if hint is not None:
+        if hint.dtype != I64 or hint.numel() != M:
+            raise ValueError("mvn_logpdf: hint must be int64 [M]")
+        hint = hint.contiguous()
     nb = nat.query("abc_mvn_logpdf_workspace", M, N, r, prec)
     ws = workspace(nb, "mvn")
     nat.call("abc_mvn_logpdf", p(x), M, d, p(packed), p(X), p(w), N, p(mu),
-             p(U), r, prec, float(log_const), float(shift), p(out), p(ws),
-             ws.numel(), stream_ptr())
+             p(U), r, prec, float(log_const), float(shift), p(out), p(hint),
+             p(ws), ws.numel(), stream_ptr())
     return out
 
 

@@ -133,7 +133,7 @@ class BatchedGPUSampler(Sampler):
         record = self.sample_factory.record_rejected
         d = len(spec.param_names)
 
-        acc_theta, acc_lp, acc_d, acc_x = [], [], [], []
+        acc_theta, acc_lp, acc_d, acc_x, acc_anc = [], [], [], [], []
         rec_x = []
         keeps = []          # per round: accepted rows kept by each rank
         rec_keeps = []      # per round: recorded rows of each rank
@@ -148,7 +148,7 @@ class BatchedGPUSampler(Sampler):
                 break
             B = self._round_size(n - n_acc, ws)
             lo, _ = dd.rank_range(base, B, rank)
-            theta, lp = self._propose(spec, B, seed, gen, lo, d)
+            theta, lp, anc = self._propose(spec, B, seed, gen, lo, d)
             x = spec.model.simulate_batch(theta, seed, gen, lo)
             if all_accepted or spec.distance is None:
                 dist = gpu.torch.full((B,), np.inf, dtype=gpu.F64, device=dev)
@@ -182,6 +182,9 @@ class BatchedGPUSampler(Sampler):
                 acc_lp.append(gpu.gather_rows(lp, sel))
                 acc_d.append(gpu.gather_rows(dist, sel))
                 acc_x.append(gpu.gather_rows(x, sel))
+                if anc is not None:   # int64 rows moved as 8-byte words
+                    acc_anc.append(gpu.gather_rows(
+                        anc.view(gpu.F64), sel).view(gpu.I64))
             if record:
                 rec_x.append(x[:rec_rows])
                 rec_keeps.append(rec_all)
@@ -198,7 +201,7 @@ class BatchedGPUSampler(Sampler):
         if n_acc < n:
             ok = False
         cols = self._assemble(spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
-                              all_accepted, keeps)
+                              all_accepted, keeps, acc_anc)
         recorded = None
         if record:
             recorded = gpu.torch.cat(rec_x, 0) if rec_x else None
@@ -222,11 +225,12 @@ class BatchedGPUSampler(Sampler):
             th, lp, _, att = gpu.propose(None, None, None, spec.prior_kind,
                                          spec.prior_params, seed, gen, lo, B,
                                          self.max_attempts, d)
+            anc = None
         else:
-            th, lp, _, att = spec.transition.propose_device(
+            th, lp, anc, att = spec.transition.propose_device(
                 B, spec.prior_kind, spec.prior_params, seed=seed,
                 generation=gen, idx0=lo, max_attempts=self.max_attempts)
-        return th, lp
+        return th, lp, anc
 
     @staticmethod
     def global_order(keeps):
@@ -246,7 +250,7 @@ class BatchedGPUSampler(Sampler):
         return base + np.arange(tot, dtype=np.int64)
 
     def _assemble(self, spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
-                  all_accepted, keeps):
+                  all_accepted, keeps, acc_anc=()):
         rank, ws = dd.world()
         torch = gpu.torch
         if acc_theta:
@@ -264,7 +268,11 @@ class BatchedGPUSampler(Sampler):
         if spec.transition is None or all_accepted:
             w = torch.ones(theta.shape[0], dtype=gpu.F64, device=dev)
         else:
-            lt = spec.transition.logpdf_device(theta)
+            # ancestors of the accepted rows: population rows near them,
+            # used by the x3 density kernel as exponent offsets
+            anc = (torch.cat(acc_anc, 0) if acc_anc and
+                   len(acc_anc) == len(acc_theta) else None)
+            lt = spec.transition.logpdf_device(theta, hint=anc)
             w = gpu.importance_weights(lp, lt, spec.weight_scale)
         if ws > 1:
             theta = dd.allgather_rows(theta, dev)

@@ -110,7 +110,7 @@ class LocalTransition(Transition):
     def normalization(self):
         return self._host_arrays()["normalization"]
 
-    def logpdf_device(self, xd, out=None):
+    def logpdf_device(self, xd, out=None, hint=None):
         return gpu.local_logpdf(xd, self._dev_X, self._dev_w, self._dev_inv,
                                 self._dev_lnorm, out=out)
 

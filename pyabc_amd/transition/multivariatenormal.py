@@ -159,14 +159,17 @@ class MultivariateNormalTransition(Transition):
         self._counter = 0
 
     # -- density -----------------------------------------------------------
-    def logpdf_device(self, xd, out=None):
-        """log density at device points xd [M, d] (columns in fit order)."""
+    def logpdf_device(self, xd, out=None, hint=None):
+        """log density at device points xd [M, d] (columns in fit order).
+        hint: optional device int64 [M] rows of the fitted population near
+        the points (the ancestors propose_device drew them from)."""
         if self._mfma:
             return gpu.mvn_logpdf(xd, self._dev_packed, self._dev_X.shape[0],
                                   self._dev_mu, self._dev_U, self._prec,
                                   self._log_norm - self._shift, out=out,
                                   X=self._dev_X, w=self._dev_w,
-                                  shift=self._shift)
+                                  shift=self._shift,
+                                  hint=hint if self._prec == nat.ABC_PREC_X3 else None)
         return gpu.mvn_logpdf_direct(xd, self._dev_X, self._dev_w, self._dev_U,
                                      self._dev_V, self._support_tol,
                                      self._log_norm, out=out)

@@ -59,7 +59,7 @@ class _Transition:
                                          ["norm"] * D, np.tile([0, 1, 0, 0], (D, 1)))
         return torch.from_numpy(th), torch.from_numpy(lp), None, None
 
-    def logpdf_device(self, theta):
+    def logpdf_device(self, theta, hint=None):
         return torch.from_numpy(oracle.mvn_logpdf(theta.numpy(), self.pop.X,
                                                   self.pop.w, self.cov))
 

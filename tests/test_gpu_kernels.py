@@ -134,6 +134,48 @@ def test_mvn_x3_rescue_and_edges(dev):
                                    rtol=1e-9)
 
 
+def test_mvn_x3_hinted_offsets(dev):
+    """x3 with per-candidate offsets from a hint row (the sampler passes the
+    proposal's ancestor) instead of the max pre-pass: ancestors, random rows,
+    far rows (offset clamped, rescue) and invalid rows (-> fp64 rescue) all
+    match the oracle within 2e-6 relative (the offset adds up to
+    2^-24 * 20 * ln 2 = 8e-7 to the pre-pass path's rounding)."""
+    import pandas as pd
+    from pyabc_amd.transition import MultivariateNormalTransition
+    rng = np.random.default_rng(21)
+    for N, d in [(50, 2), (3000, 10), (20_000, 10)]:
+        X = 0.8 + np.sqrt(0.2) * rng.standard_normal((N, d))
+        w = np.exp(0.5 * rng.standard_normal(N))
+        w[::11] = 0.0
+        w /= w.sum()
+        cols = [f"p{k}" for k in range(d)]
+        t = MultivariateNormalTransition()
+        t.fit(pd.DataFrame(X, columns=cols), w.copy())
+        assert t._prec == 2
+        M = 700
+        th, _, anc, _ = t.propose_device(M)
+        x = th.cpu().numpy()
+        ref = oracle.mvn_logpdf(x, X, w, t.cov)
+        base = t.logpdf_device(th).cpu().numpy()
+        hints = {
+            "ancestor": anc,
+            "random": torch.as_tensor(rng.integers(0, N, M), device=dev),
+            "far": torch.as_tensor(np.argmax(((X - X.mean(0)) ** 2).sum(1))
+                                   * np.ones(M, dtype=np.int64), device=dev),
+            "invalid": torch.as_tensor(np.where(np.arange(M) % 3 == 0, -1,
+                                                np.where(np.arange(M) % 3 == 1,
+                                                         N + 5, 0)),
+                                       device=dev),
+        }
+        for name, h in hints.items():
+            lp = t.logpdf_device(th, hint=h.to(torch.int64)).cpu().numpy()
+            np.testing.assert_allclose(np.exp(lp - ref), 1.0, rtol=2e-6,
+                                       err_msg=f"N={N} hint={name}")
+        np.testing.assert_allclose(np.exp(base - ref), 1.0, rtol=1e-6)
+    with pytest.raises(ValueError):
+        t.logpdf_device(th, hint=torch.zeros(3, dtype=torch.int64, device=dev))
+
+
 @pytest.mark.parametrize("tag,kw", [("k50", dict(k=50, k_fraction=None)),
                                     ("default", dict())])
 def test_local_golden(dev, tag, kw):

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--M", type=int, default=100_000)
     ap.add_argument("--d", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--prec", default="x3,f64")
+    ap.add_argument("--prec", default="x3,x3+hint,f64")
     a = ap.parse_args()
     import pandas as pd
     import torch
@@ -36,16 +36,21 @@ def main():
     res = {}
     cand = None
     for prec in a.prec.split(","):
+        hinted = prec.endswith("+hint")
+        prec = prec.replace("+hint", "")
         t = MultivariateNormalTransition(precision=prec)
         t.fit(pd.DataFrame(X, columns=cols), w.copy())
         if cand is None:
-            cand = t.propose_device(a.M)[0]
-        t.logpdf_device(cand)
+            cand, _, anc, _ = t.propose_device(a.M)
+        hint = anc if hinted else None
+        if hinted:
+            prec += "+hint"
+        t.logpdf_device(cand, hint=hint)
         torch.cuda.synchronize()
         nat.call("abc_profile_begin")
         t0 = time.perf_counter()
         for _ in range(a.reps):
-            out = t.logpdf_device(cand)
+            out = t.logpdf_device(cand, hint=hint)
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / a.reps
         ms = ctypes.c_double(0)
@@ -55,11 +60,12 @@ def main():
         pairs = a.M * a.N
         res[prec] = out.cpu().numpy()
         print(f"{prec}: kernel {kms:.3f} ms  call {1e3 * wall:.3f} ms  "
-              f"{pairs / kms / 1e9:.3e} pairs/s  "
+              f"{pairs / kms / 1e9:.3e} Gpairs/s  "
               f"{2 * a.d * pairs / kms / 1e9:.1f} TFLOP/s(2d/pair)", flush=True)
-    if "x3" in res and "f64" in res:
-        err = np.abs(np.expm1(res["x3"] - res["f64"]))
-        print(f"x3 vs f64: max rel {err.max():.3e}  mean {err.mean():.3e}")
+    for k in ("x3", "x3+hint"):
+        if k in res and "f64" in res:
+            err = np.abs(np.expm1(res[k] - res["f64"]))
+            print(f"{k} vs f64: max rel {err.max():.3e}  mean {err.mean():.3e}")
 
 
 if __name__ == "__main__":
