@@ -66,7 +66,8 @@ int abc_profile_end(double* total_ms, int64_t* launches);
  * Replaces the numpy work in MultivariateNormalTransition.fit
  * (pyabc/transition/multivariatenormal.py:72-83, smart_cov util.py:4-16):
  * out[0] = sum w, out[1] = sum w^2, out[2 .. 2+d) = weighted mean
- * (sum w x / sum w), out[2+d .. 2+d+d*d) = sum w (x-mean)(x-mean)^T / sum w.
+ * (sum w x / sum w), out[2+d .. 2+d+d*d) = sum w (x-mean)(x-mean)^T / sum w,
+ * out[2+d+d*d] = max w (out holds 3 + d + d*d doubles).
  * Deterministic two-pass fp64 (per-block partials, fixed-order combine). */
 size_t abc_weighted_moments_workspace(int64_t N, int d);
 int abc_weighted_moments(const double* X, const double* w, int64_t N, int d,

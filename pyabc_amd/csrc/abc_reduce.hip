@@ -63,6 +63,20 @@ __global__ void moments1_final(const double* __restrict__ part, int nblk,
   }
 }
 
+// max w for the generic path (single block; fixed order)
+__global__ void mom1_max_generic(const double* __restrict__ w, int64_t N,
+                                 double* __restrict__ out) {
+  __shared__ double sh[256];
+  double m = 0.0;
+  for (int64_t r = threadIdx.x; r < N; r += blockDim.x) m = fmax(m, w[r]);
+  sh[threadIdx.x] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int t = 1; t < 256; ++t) m = fmax(m, sh[t]);
+    *out = m;
+  }
+}
+
 // pass 2: sum w (x - mean)(x - mean)^T, one (a, b) entry per thread slot
 __global__ __launch_bounds__(256) void moments2_kernel(
     const double* __restrict__ X, const double* __restrict__ w, int64_t N,
@@ -108,6 +122,144 @@ __global__ void moments2_final(const double* __restrict__ part, int nblk,
     for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * npair + c];
     out[2 + d + c] = s / sw;
   }
+}
+
+// ---- fast path: d fixed at compile time, one row per thread ----------------
+// Rows are strided over the grid; each thread keeps its row sums in
+// registers; blocks reduce by wave butterflies + LDS in fixed order (bitwise
+// reproducible); the final kernels reduce the block partials by a fixed tree.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// sum over the block of NV per-thread values -> out[0..NV) (thread 0 writes)
+template <int NV>
+__device__ __forceinline__ void block_sums(const double (&v)[NV], double* sh,
+                                           double* __restrict__ out) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const double t = wave_sum(v[c]);
+    if (lane == 0) sh[wv * NV + c] = t;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < NV; c += blockDim.x)
+    out[c] = (sh[c] + sh[NV + c]) + (sh[2 * NV + c] + sh[3 * NV + c]);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void mom1_fast(const double* __restrict__ X,
+                                                 const double* __restrict__ w,
+                                                 int64_t N, double* __restrict__ part,
+                                                 double* __restrict__ pmax) {
+  constexpr int NV = D + 2;
+  __shared__ double sh[4 * NV];
+  __shared__ double shm[4];
+  double v[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) v[c] = 0.0;
+  double mx = 0.0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const double wr = w[r];
+    v[0] += wr;
+    v[1] += wr * wr;
+    mx = fmax(mx, wr);
+#pragma unroll
+    for (int q = 0; q < D; ++q) v[2 + q] += wr * X[r * D + q];
+  }
+  block_sums<NV>(v, sh, part + (int64_t)blockIdx.x * NV);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+  if ((threadIdx.x & 63) == 0) shm[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) pmax[blockIdx.x] = fmax(fmax(shm[0], shm[1]), fmax(shm[2], shm[3]));
+}
+
+// out[c] = sum over nblk partials of column c (ncol columns), one wave per
+// column, fixed order; `scale_from` >= 0 divides columns >= scale_from by
+// out[0] (already final) -- used for the mean / covariance normalisation
+__global__ __launch_bounds__(256) void mom_final(const double* __restrict__ part,
+                                                 int nblk, int ncol, int col0,
+                                                 double* __restrict__ out,
+                                                 bool divide) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= ncol) return;
+  double s = 0.0;
+  for (int b = lane; b < nblk; b += 64) s += part[(int64_t)b * ncol + c];
+  s = wave_sum(s);
+  if (lane == 0) out[col0 + c] = divide ? s / out[0] : s;
+}
+
+__global__ void mom_max_final(const double* __restrict__ pmax, int nblk,
+                              double* __restrict__ out) {
+  double m = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += 64) m = fmax(m, pmax[b]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+  if (threadIdx.x == 0) *out = m;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void mom2_fast(const double* __restrict__ X,
+                                                 const double* __restrict__ w,
+                                                 int64_t N,
+                                                 const double* __restrict__ mom,
+                                                 double* __restrict__ part) {
+  constexpr int NV = D * (D + 1) / 2;  // upper triangle, row-major
+  __shared__ double sh[4 * NV];
+  double mean[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) mean[q] = mom[2 + q] / mom[0];  // raw sums here
+  double v[NV];
+#pragma unroll
+  for (int c = 0; c < NV; ++c) v[c] = 0.0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < N;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const double wr = w[r];
+    double xc[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) xc[q] = X[r * D + q] - mean[q];
+    int c = 0;
+#pragma unroll
+    for (int a = 0; a < D; ++a)
+#pragma unroll
+      for (int b = a; b < D; ++b) v[c++] += wr * xc[a] * xc[b];
+  }
+  block_sums<NV>(v, sh, part + (int64_t)blockIdx.x * NV);
+}
+
+// upper-triangle sums -> full symmetric d x d, divided by sum w; means
+// divided by sum w (same fp64 division as the generic path)
+template <int D>
+__global__ void mom2_expand(const double* __restrict__ tri, double* __restrict__ out) {
+  const int t = threadIdx.x;
+  if (t < D) out[2 + t] = out[2 + t] / out[0];
+  if (t >= D * D) return;
+  int a = t / D, b = t % D;
+  if (a > b) { const int x = a; a = b; b = x; }
+  const int c = a * D - a * (a - 1) / 2 + (b - a);
+  out[2 + D + t] = tri[c] / out[0];
+}
+
+template <int D>
+void moments_fast(const double* X, const double* w, int64_t N, double* out,
+                  double* p1, double* p2, double* pmax, double* tri, hipStream_t s) {
+  constexpr int NV1 = D + 2, NV2 = D * (D + 1) / 2;
+  const int nblk = (int)(ceil_div(N, 256) < MOM_BLOCKS ? ceil_div(N, 256) : MOM_BLOCKS);
+  hipLaunchKernelGGL(mom1_fast<D>, dim3(nblk), dim3(256), 0, s, X, w, N, p1, pmax);
+  // raw column sums (sum w, sum w^2, sum w x); means are divided in mom2
+  hipLaunchKernelGGL(mom_final, dim3((unsigned)ceil_div(NV1, 4)), dim3(256), 0, s, p1, nblk,
+                     NV1, 0, out, false);
+  hipLaunchKernelGGL(mom_max_final, dim3(1), dim3(64), 0, s, pmax, nblk,
+                     out + 2 + D + D * D);
+  hipLaunchKernelGGL(mom2_fast<D>, dim3(nblk), dim3(256), 0, s, X, w, N, out, p2);
+  hipLaunchKernelGGL(mom_final, dim3((unsigned)ceil_div(NV2, 4)), dim3(256), 0, s, p2, nblk,
+                     NV2, 0, tri, false);
+  hipLaunchKernelGGL(mom2_expand<D>, dim3(1), dim3(256), 0, s, tri, out);
 }
 
 // ---- scan -------------------------------------------------------------------
@@ -245,6 +397,8 @@ extern "C" size_t abc_weighted_moments_workspace(int64_t N, int d) {
   size_t off = 0;
   size_only<double>(off, (size_t)MOM_BLOCKS * (2 + d));
   size_only<double>(off, (size_t)MOM_BLOCKS * d * d);
+  size_only<double>(off, (size_t)MOM_BLOCKS);
+  size_only<double>(off, (size_t)d * d);
   return off + 256;
 }
 
@@ -258,7 +412,18 @@ extern "C" int abc_weighted_moments(const double* X, const double* w,
   Carver cv(ws, ws_bytes);
   double* p1 = cv.take<double>((size_t)MOM_BLOCKS * (2 + d));
   double* p2 = cv.take<double>((size_t)MOM_BLOCKS * d * d);
+  double* pmax = cv.take<double>((size_t)MOM_BLOCKS);
+  double* tri = cv.take<double>((size_t)d * d);
   hipStream_t s = as_stream(stream);
+  switch (d) {
+#define ABC_MOM_CASE(D) \
+    case D: moments_fast<D>(X, w, N, out, p1, p2, pmax, tri, s); ABC_LAUNCHED(); return ABC_OK;
+    ABC_MOM_CASE(1) ABC_MOM_CASE(2) ABC_MOM_CASE(3) ABC_MOM_CASE(4)
+    ABC_MOM_CASE(5) ABC_MOM_CASE(6) ABC_MOM_CASE(8) ABC_MOM_CASE(10)
+    ABC_MOM_CASE(12) ABC_MOM_CASE(16)
+#undef ABC_MOM_CASE
+    default: break;
+  }
   const int nblk = (int)(ceil_div(N, MOM_ROWS) < MOM_BLOCKS ? ceil_div(N, MOM_ROWS) : MOM_BLOCKS);
   const size_t lds = sizeof(double) * (MOM_ROWS * d + MOM_ROWS);
   hipLaunchKernelGGL(moments1_kernel, dim3(nblk), dim3(256), lds, s, X, w, N, d, p1);
@@ -268,6 +433,8 @@ extern "C" int abc_weighted_moments(const double* X, const double* w,
   hipLaunchKernelGGL(moments2_kernel, dim3(nblk), dim3(256), lds, s, X, w, N, d, out, p2);
   ABC_LAUNCHED();
   hipLaunchKernelGGL(moments2_final, dim3(1), dim3(256), 0, s, p2, nblk, d, out);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(mom1_max_generic, dim3(1), dim3(256), 0, s, w, N, out + 2 + d + d * d);
   ABC_LAUNCHED();
   return ABC_OK;
 }

@@ -147,19 +147,23 @@ __device__ __forceinline__ int64_t upper_bound(const double* cdf, int64_t N,
 }
 
 // One thread per candidate.  L: [d x d] row-major (per-particle when
-// per_particle_L, the LocalTransition Cholesky factors).
-template <bool PER_PARTICLE_L>
+// per_particle_L, the LocalTransition Cholesky factors).  D > 0 fixes d at
+// compile time so the per-candidate vectors live in registers (D = 0: any
+// d <= 64, arrays in scratch).
+template <int D, bool PER_PARTICLE_L>
 __global__ __launch_bounds__(256) void propose_kernel(
     const double* __restrict__ X, const double* __restrict__ cdf, int64_t N,
-    int d, const double* __restrict__ L, const int32_t* __restrict__ kind,
+    int d_rt, const double* __restrict__ L, const int32_t* __restrict__ kind,
     const double* __restrict__ params, uint64_t seed, uint32_t gen,
     int64_t idx0, int64_t B, int max_attempts, double* __restrict__ theta,
     double* __restrict__ lp_out, int64_t* __restrict__ anc_out,
     int32_t* __restrict__ att_out) {
+  constexpr int DM = D > 0 ? D : 64;
+  const int d = D > 0 ? D : d_rt;
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const uint64_t g = (uint64_t)(idx0 + b);
-  double th[64];
+  double th[DM];
   double lp = -INFINITY;
   int64_t j = -1;
   int att = 0;
@@ -167,31 +171,69 @@ __global__ __launch_bounds__(256) void propose_kernel(
   for (; att < max_attempts; ++att) {
     const uint32_t s0 = (uint32_t)att * SLOTS_PER_ATTEMPT;
     if (X == nullptr) {
-      for (int k = 0; k < d; ++k)
-        th[k] = prior_draw1(kind[k], params + 4 * k, g, s0 + SLOT_PRIOR + 512u * k, gen, seed);
+#pragma unroll
+      for (int k = 0; k < DM; ++k)
+        if (k < d)
+          th[k] = prior_draw1(kind[k], params + 4 * k, g, s0 + SLOT_PRIOR + 512u * k, gen, seed);
     } else {
       u32x4 r = philox(g, s0 + SLOT_ANCESTOR, gen, seed);
       j = upper_bound(cdf, N, uniform53(r.x, r.y) * total);
-      double n[64];
-      for (int q = 0; q < d; q += 4) {
-        double n4[4];
-        normals4(g, s0 + SLOT_PERTURB + (uint32_t)(q >> 2), gen, seed, n4);
-        for (int e = 0; e < 4 && q + e < d; ++e) n[q + e] = n4[e];
+      double n[(DM + 3) / 4 * 4];
+#pragma unroll
+      for (int q = 0; q < DM; q += 4) {
+        if (q < d) {
+          double n4[4];
+          normals4(g, s0 + SLOT_PERTURB + (uint32_t)(q >> 2), gen, seed, n4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) n[q + e] = n4[e];
+        }
       }
       const double* Lj = PER_PARTICLE_L ? L + j * d * d : L;
-      for (int k = 0; k < d; ++k) {
-        double acc = X[j * d + k];
-        for (int q = 0; q < d; ++q) acc += Lj[k * d + q] * n[q];
-        th[k] = acc;
+#pragma unroll
+      for (int k = 0; k < DM; ++k) {
+        if (k < d) {
+          double acc = X[j * d + k];
+#pragma unroll
+          for (int q = 0; q < DM; ++q)
+            if (q < d) acc += Lj[k * d + q] * n[q];
+          th[k] = acc;
+        }
       }
     }
-    lp = prior_logpdf(kind, params, d, th);
+    lp = 0.0;
+#pragma unroll
+    for (int k = 0; k < DM; ++k)
+      if (k < d) lp += prior_logpdf1(kind[k], params + 4 * k, th[k]);
     if (lp > -INFINITY) break;  // prior density > 0 (smc.py:654-656)
   }
-  for (int k = 0; k < d; ++k) theta[b * d + k] = th[k];
+#pragma unroll
+  for (int k = 0; k < DM; ++k)
+    if (k < d) theta[b * d + k] = th[k];
   lp_out[b] = lp;
   if (anc_out) anc_out[b] = j;
   if (att_out) att_out[b] = (lp > -INFINITY) ? att + 1 : max_attempts + 1;
+}
+
+template <bool PPL>
+void launch_propose(int d, dim3 grid, hipStream_t s, const double* X,
+                    const double* cdf, int64_t N, const double* L,
+                    const int32_t* kind, const double* params, uint64_t seed,
+                    uint32_t gen, int64_t idx0, int64_t B, int max_attempts,
+                    double* theta, double* lp, int64_t* anc, int32_t* att) {
+#define ABC_PROPOSE_CASE(DD)                                                     \
+  case DD:                                                                       \
+    hipLaunchKernelGGL((propose_kernel<DD, PPL>), grid, dim3(256), 0, s, X, cdf, \
+                       N, d, L, kind, params, seed, gen, idx0, B, max_attempts,  \
+                       theta, lp, anc, att);                                     \
+    break;
+  switch (d) {
+    ABC_PROPOSE_CASE(1) ABC_PROPOSE_CASE(2) ABC_PROPOSE_CASE(3)
+    ABC_PROPOSE_CASE(4) ABC_PROPOSE_CASE(5) ABC_PROPOSE_CASE(6)
+    ABC_PROPOSE_CASE(8) ABC_PROPOSE_CASE(10) ABC_PROPOSE_CASE(12)
+    ABC_PROPOSE_CASE(16)
+    default: ABC_PROPOSE_CASE(0)
+  }
+#undef ABC_PROPOSE_CASE
 }
 
 __global__ void prior_logpdf_kernel(const double* __restrict__ th, int64_t B,
@@ -343,10 +385,9 @@ extern "C" int abc_propose(const double* X, const double* cdf, int64_t N,
   if (B == 0) return ABC_OK;
   ABC_CHECK_ARG(theta && prior_logpdf && prior_kind && prior_params, "propose: null pointer");
   ABC_CHECK_ARG(X == nullptr || (cdf && L && N >= 1), "propose: population needs cdf, L, N");
-  hipLaunchKernelGGL(propose_kernel<false>, dim3((unsigned)ceil_div(B, 256)), dim3(256), 0,
-                     as_stream(stream), X, cdf, N, d, L, prior_kind, prior_params, seed,
-                     generation, idx0, B, max_attempts, theta, prior_logpdf, ancestor,
-                     attempts);
+  launch_propose<false>(d, dim3((unsigned)ceil_div(B, 256)), as_stream(stream), X, cdf,
+                        N, L, prior_kind, prior_params, seed, generation, idx0, B,
+                        max_attempts, theta, prior_logpdf, ancestor, attempts);
   ABC_LAUNCHED();
   return ABC_OK;
 }
@@ -364,10 +405,9 @@ extern "C" int abc_local_propose(const double* X, const double* cdf, int64_t N,
   if (B == 0) return ABC_OK;
   ABC_CHECK_ARG(X && cdf && chol && N >= 1 && theta && prior_logpdf && prior_kind &&
                 prior_params, "local_propose: null pointer");
-  hipLaunchKernelGGL(propose_kernel<true>, dim3((unsigned)ceil_div(B, 256)), dim3(256), 0,
-                     as_stream(stream), X, cdf, N, d, chol, prior_kind, prior_params, seed,
-                     generation, idx0, B, max_attempts, theta, prior_logpdf, ancestor,
-                     attempts);
+  launch_propose<true>(d, dim3((unsigned)ceil_div(B, 256)), as_stream(stream), X, cdf,
+                       N, chol, prior_kind, prior_params, seed, generation, idx0, B,
+                       max_attempts, theta, prior_logpdf, ancestor, attempts);
   ABC_LAUNCHED();
   return ABC_OK;
 }

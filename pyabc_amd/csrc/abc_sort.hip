@@ -206,6 +206,23 @@ __global__ __launch_bounds__(ST) void exscan_apply(const int64_t* __restrict__ i
   for (int k = 0; k < SI; ++k) { if (b + k < n) out[b + k] = run; run += v[k]; }
 }
 
+// single-workgroup exclusive scan for small histograms (n <= SCAN1_MAX):
+// one launch instead of three; fixed order, deterministic
+constexpr int64_t SCAN1_MAX = 1 << 14;
+__global__ __launch_bounds__(ST) void exscan_single(const int64_t* __restrict__ in,
+                                                    int64_t n,
+                                                    int64_t* __restrict__ out) {
+  __shared__ int64_t sh[ST];
+  const int64_t per = (n + ST - 1) / ST;
+  const int64_t b0 = threadIdx.x * per;
+  int64_t s = 0;
+  for (int64_t k = 0; k < per; ++k) if (b0 + k < n) s += in[b0 + k];
+  int64_t tot;
+  int64_t run = block_exscan(s, sh, tot);
+  for (int64_t k = 0; k < per; ++k)
+    if (b0 + k < n) { const int64_t v = in[b0 + k]; out[b0 + k] = run; run += v; }
+}
+
 struct SortBufs {
   uint64_t* k0; uint64_t* k1; double* v0; double* v1;
   int64_t* hist; int64_t* off; int64_t* sums;
@@ -251,13 +268,19 @@ int run_sort(SortBufs& b, int64_t nseg, int64_t seg_len, hipStream_t s) {
     hipLaunchKernelGGL(radix_hist_kernel, dim3((unsigned)ntile), dim3(RT), 0, s, b.k0,
                        seg_len, tps, shift, b.hist);
     ABC_LAUNCHED();
-    hipLaunchKernelGGL(exscan_sums, dim3((unsigned)nsum), dim3(ST), 0, s, b.hist, nh, b.sums);
-    ABC_LAUNCHED();
-    hipLaunchKernelGGL(exscan_top, dim3(1), dim3(ST), 0, s, b.sums, nsum);
-    ABC_LAUNCHED();
-    hipLaunchKernelGGL(exscan_apply, dim3((unsigned)nsum), dim3(ST), 0, s, b.hist, nh, b.sums,
-                       b.off);
-    ABC_LAUNCHED();
+    if (nh <= SCAN1_MAX) {
+      hipLaunchKernelGGL(exscan_single, dim3(1), dim3(ST), 0, s, b.hist, nh, b.off);
+      ABC_LAUNCHED();
+    } else {
+      hipLaunchKernelGGL(exscan_sums, dim3((unsigned)nsum), dim3(ST), 0, s, b.hist, nh,
+                         b.sums);
+      ABC_LAUNCHED();
+      hipLaunchKernelGGL(exscan_top, dim3(1), dim3(ST), 0, s, b.sums, nsum);
+      ABC_LAUNCHED();
+      hipLaunchKernelGGL(exscan_apply, dim3((unsigned)nsum), dim3(ST), 0, s, b.hist, nh,
+                         b.sums, b.off);
+      ABC_LAUNCHED();
+    }
     if (b.v0)
       hipLaunchKernelGGL(radix_scatter_kernel<true>, dim3((unsigned)ntile), dim3(RT), 0, s,
                          b.k0, b.v0, seg_len, tps, shift, b.off, b.k1, b.v1);

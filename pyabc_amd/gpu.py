@@ -72,16 +72,18 @@ def as_dev(a, dtype=None, device=None):
 
 # ---- reductions -----------------------------------------------------------
 
-def weighted_moments(X, w):
-    """(sum w, sum w^2, mean [d], cov_biased [d, d]) as float64 numpy."""
+def weighted_moments(X, w, with_max=False):
+    """(sum w, sum w^2, mean [d], cov_biased [d, d]) as float64 numpy
+    (+ max w with with_max), one device-to-host read."""
     N, d = X.shape
-    out = torch.empty(2 + d + d * d, dtype=F64, device=X.device)
+    out = torch.empty(3 + d + d * d, dtype=F64, device=X.device)
     nb = nat.query("abc_weighted_moments_workspace", N, d)
     ws = workspace(nb)
     nat.call("abc_weighted_moments", p(X), p(w), N, d, p(out), p(ws), ws.numel(),
              stream_ptr())
     o = out.cpu().numpy()
-    return o[0], o[1], o[2:2 + d].copy(), o[2 + d:].reshape(d, d).copy()
+    res = (o[0], o[1], o[2:2 + d].copy(), o[2 + d:2 + d + d * d].reshape(d, d).copy())
+    return res + (o[2 + d + d * d],) if with_max else res
 
 
 def inclusive_scan(x, out=None):

@@ -103,7 +103,8 @@ class MultivariateNormalTransition(Transition):
 
     def _fit_device_arrays(self, Xd, wd):
         N, d = Xd.shape
-        sw, sw2, mean, cov_b = gpu.weighted_moments(Xd, wd)
+        sw, sw2, mean, cov_b, wmax = gpu.weighted_moments(Xd, wd, with_max=True)
+        self._wmax = float(wmax)
         if N == 1:
             sample_cov = np.diag(np.abs(Xd[0].cpu().numpy()))
         else:
@@ -138,7 +139,7 @@ class MultivariateNormalTransition(Transition):
         self._dev_packed = None
         if self._mfma and self._prec == nat.ABC_PREC_X3:
             # exponents <= 0: shift by -log max w (one host read per fit)
-            self._shift = -math.log(float(wd.max().item()))
+            self._shift = -math.log(self._wmax)
             packed, rng = gpu.mvn_pack(Xd, wd, self._dev_mu, self._dev_U,
                                        self._shift, self._prec, with_range=True)
             # range = [max whitened norm, grid exponent E]; E <= 8 keeps the

@@ -255,18 +255,27 @@ def test_column_mad_large(dev):
         np.testing.assert_array_equal(mad, oracle.median_absolute_deviation(X))
 
 
-def test_weighted_moments(dev):
+@pytest.mark.parametrize("N,d", [(10_001, 7), (10_001, 10), (1, 10), (300, 1),
+                                 (100_000, 3), (77, 20)])
+def test_weighted_moments(dev, N, d):
+    """np.cov(X, aweights=w) pieces; d in {1..6, 8, 10, 12, 16} run the
+    register fast path, others the generic LDS path."""
     from pyabc_amd import gpu
     rng = np.random.default_rng(3)
-    X = rng.standard_normal((10_001, 7)) + 5
-    w = rng.uniform(size=10_001)
-    sw, sw2, mean, cov_b = gpu.weighted_moments(T(X), T(w))
+    X = rng.standard_normal((N, d)) + 5
+    w = rng.uniform(size=N)
+    sw, sw2, mean, cov_b, wmax = gpu.weighted_moments(T(X), T(w), with_max=True)
+    assert wmax == w.max()
     assert sw == pytest.approx(w.sum(), rel=1e-13)
     assert sw2 == pytest.approx((w ** 2).sum(), rel=1e-13)
     np.testing.assert_allclose(mean, w @ X / w.sum(), rtol=1e-13)
-    wn = w / w.sum()
-    cov_ref = np.cov(X, aweights=w, rowvar=False)
-    np.testing.assert_allclose(cov_b * sw / (sw - sw2 / sw), cov_ref, rtol=1e-11)
+    if N > 1:
+        cov_ref = np.cov(X, aweights=w, rowvar=False)
+        np.testing.assert_allclose(cov_b * sw / (sw - sw2 / sw), cov_ref,
+                                   rtol=1e-10, atol=1e-13)
+    # bitwise reproducible run to run
+    again = gpu.weighted_moments(T(X), T(w))
+    assert np.array_equal(again[3], cov_b) and again[0] == sw
 
 
 def test_scan(dev):
