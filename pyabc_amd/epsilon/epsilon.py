@@ -81,7 +81,7 @@ class QuantileEpsilon(Epsilon):
         if self._initial_epsilon != 'from_sample':
             return
         self._update(t, get_weighted_distances())
-        logger.info(f"initial epsilon is {self._look_up[t]}")
+        logger.info(f"initial epsilon is {self(t)}")
 
     def __call__(self, t):
         if not self._look_up:
@@ -91,6 +91,8 @@ class QuantileEpsilon(Epsilon):
         except KeyError as e:
             raise KeyError(f"The epsilon value for time {t} does not exist: "
                            f"{repr(e)} ")
+        if isinstance(eps, _PendingEps):  # device quantile still in flight
+            eps = self._look_up[t] = eps.value()
         return eps
 
     def _set_initial_value(self, t):
@@ -99,7 +101,6 @@ class QuantileEpsilon(Epsilon):
     def update(self, t, get_weighted_distances, get_all_records,
                acceptance_rate, acceptor_config):
         self._update(t, get_weighted_distances())
-        logger.debug(f"new eps, t={t}, eps={self._look_up[t]}")
 
     def _update(self, t, weighted_distances):
         d, w = _device_distances(weighted_distances)
@@ -107,7 +108,28 @@ class QuantileEpsilon(Epsilon):
             w = gpu.torch.ones_like(d)
         # the kernel normalises w by its sum (epsilon.py:215-219)
         q = gpu.weighted_quantile(d, w, self.alpha)
-        self._look_up[t] = float(q.cpu()[0]) * self.quantile_multiplier
+        # read back lazily: __call__(t) is the first consumer
+        self._look_up[t] = _PendingEps(gpu.HostFuture(q), self.quantile_multiplier)
+
+
+class _PendingEps:
+    """Quantile of the device kernel, resolved to a float on first use."""
+
+    def __init__(self, fut, multiplier):
+        self._fut = fut
+        self._mult = multiplier
+
+    def value(self):
+        return float(self._fut.get()[0]) * self._mult
+
+    def __float__(self):
+        return self.value()
+
+    def __deepcopy__(self, memo):
+        return self.value()
+
+    def __reduce__(self):
+        return (float, (self.value(),))
 
 
 class MedianEpsilon(QuantileEpsilon):

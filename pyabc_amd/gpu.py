@@ -60,6 +60,32 @@ def workspace(nbytes, slot="main"):
     return buf
 
 
+class HostFuture:
+    """Device -> pinned host copy enqueued on the current stream; .get()
+    waits for that copy only (no device-wide sync), so the host can keep
+    queueing work while the value is produced."""
+
+    def __init__(self, t):
+        self._h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        self._h.copy_(t, non_blocking=True)
+        self._ev = torch.cuda.Event()
+        self._ev.record()
+        self._v = None
+
+    def get(self):
+        if self._v is None:
+            self._ev.synchronize()
+            self._v = self._h.numpy().copy()
+            self._h = self._ev = None
+        return self._v
+
+    def __deepcopy__(self, memo):
+        return self          # the value is immutable once produced
+
+    def __getstate__(self):
+        return {"_v": self.get(), "_h": None, "_ev": None}
+
+
 def as_dev(a, dtype=None, device=None):
     """numpy / list / tensor -> contiguous device tensor."""
     dtype = dtype or F64

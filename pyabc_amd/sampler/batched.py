@@ -114,7 +114,8 @@ class BatchedGPUSampler(Sampler):
         if self.batch_size is not None:
             return int(self.batch_size)
         rate = self._acc_rate if self._acc_rate else 0.5
-        b = int(math.ceil(needed / max(rate, 1e-4) * 1.15 / ws)) + 256
+        # 30% margin: a second round costs more than the extra candidates
+        b = int(math.ceil(needed / max(rate, 1e-4) * 1.3 / ws)) + 256
         return int(min(max(b, 4096), self.max_batch_size))
 
     def sample_until_n_accepted(self, n, simulate_one, max_eval=np.inf,
@@ -158,7 +159,16 @@ class BatchedGPUSampler(Sampler):
                 dist = spec.distance.device_call(x, spec.x0vec, spec.t,
                                                  spec.sum_stat_keys)
                 idx, cnt = gpu.accept_compact(dist, spec.eps)
-                cnt_local = int(cnt.item())
+                if ws == 1:
+                    # one read: the count and the index of the n-th accepted
+                    # (meaningful only when this round completes the sample)
+                    kk = min(n - n_acc, B)
+                    tail = idx[kk - 1:kk] if idx.numel() >= kk else cnt.view(1)
+                    both = gpu.torch.cat([cnt.view(1), tail]).cpu()
+                    cnt_local = int(both[0])
+                    pos_hint = int(both[1])
+                else:
+                    cnt_local = int(cnt.item())
             counts = dd.allgather_counts(cnt_local, dev)
             keep = dd.cutoff(counts, n - n_acc)
             total_keep = int(keep.sum())
@@ -168,8 +178,11 @@ class BatchedGPUSampler(Sampler):
             rec_all = np.full(ws, B, dtype=np.int64)
             if n_acc + total_keep >= n:
                 c_rank = int(np.nonzero(keep)[0][-1])
-                pos = self._local_cutoff_pos(idx, keep[c_rank]) if rank == c_rank else -1
-                pos = dd.allgather_counts(pos, dev)[c_rank]
+                if ws == 1 and not (all_accepted or spec.distance is None):
+                    pos = pos_hint
+                else:
+                    pos = self._local_cutoff_pos(idx, keep[c_rank]) if rank == c_rank else -1
+                    pos = dd.allgather_counts(pos, dev)[c_rank]
                 evaluated = c_rank * B + pos + 1
                 rec_all[c_rank] = pos + 1
                 rec_all[c_rank + 1:] = 0

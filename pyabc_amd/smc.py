@@ -457,11 +457,14 @@ class ABCSMC:
                                            model_names)
             pop_size = len(population)
             acceptance_rate = pop_size / n_sim
-            ess = self._ess(population)
-            logger.info(f"Acceptance rate: {pop_size} / {n_sim} = "
-                        f"{acceptance_rate:.4e}, ESS={ess:.4e}.")
+            # the ESS is read after the next fit is queued (no host sync
+            # while the transition-density kernel is still running)
+            ess_read = self._ess_async(population)
             self._prepare_next_iteration(t + 1, sample, population,
                                          acceptance_rate)
+            ess = ess_read()
+            logger.info(f"Acceptance rate: {pop_size} / {n_sim} = "
+                        f"{acceptance_rate:.4e}, ESS={ess:.4e}.")
             self.generation_log.append(dict(
                 t=t, eps=float(current_eps), n_sim=int(n_sim), ess=float(ess),
                 seconds=(datetime.datetime.now() - t_start).total_seconds()))
@@ -480,6 +483,14 @@ class ABCSMC:
             t += 1
         self.history.done()
         return self.history
+
+    @staticmethod
+    def _ess_async(population):
+        if population.columns is not None:
+            fut = gpu.HostFuture(population._stats[1:2])
+            return lambda: float(fut.get()[0])
+        ess = ABCSMC._ess(population)
+        return lambda: ess
 
     @staticmethod
     def _ess(population):

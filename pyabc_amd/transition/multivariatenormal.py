@@ -137,33 +137,46 @@ class MultivariateNormalTransition(Transition):
         if self._prec == nat.ABC_PREC_X3 and psd["rank"] > self.X3_MAX_RANK:
             self._prec = nat.ABC_PREC_F64
         self._dev_packed = None
+        self._x3_range = None
         if self._mfma and self._prec == nat.ABC_PREC_X3:
             # exponents <= 0: shift by -log max w (one host read per fit)
             self._shift = -math.log(self._wmax)
             packed, rng = gpu.mvn_pack(Xd, wd, self._dev_mu, self._dev_U,
                                        self._shift, self._prec, with_range=True)
             # range = [max whitened norm, grid exponent E]; E <= 8 keeps the
-            # dropped limb products below 2^-19 (see abc_mvn_x3.hip)
-            ymax, E = rng.cpu().numpy()
-            if E <= 8:
-                self._dev_packed = packed
-            else:  # population too spread for the limb grid: fp64 MFMA
-                self._prec = nat.ABC_PREC_F64
+            # dropped limb products below 2^-19 (see abc_mvn_x3.hip).  Read
+            # back at the first density call, not here (no host sync in fit)
+            self._dev_packed = packed
+            self._x3_range = gpu.HostFuture(rng)
         if self._mfma and self._dev_packed is None:
-            self._shift = math.log(N)
-            self._dev_packed = gpu.mvn_pack(Xd, wd, self._dev_mu, self._dev_U,
-                                            self._shift, self._prec)
+            self._pack_f64()
         self._dev_flat_kind = gpu.as_dev(np.full(d, -1), dtype=gpu.torch.int32,
                                          device=dev)
         self._dev_flat_params = gpu.torch.zeros(4 * d, dtype=gpu.F64, device=dev)
         self._seed = int(np.random.randint(0, 2 ** 62))
         self._counter = 0
 
+    def _pack_f64(self):
+        self._shift = math.log(self._dev_X.shape[0])
+        self._dev_packed = gpu.mvn_pack(self._dev_X, self._dev_w, self._dev_mu,
+                                        self._dev_U, self._shift, self._prec)
+
+    def _check_x3_range(self):
+        rng = getattr(self, "_x3_range", None)
+        if rng is None:
+            return
+        self._x3_range = None
+        ymax, E = rng.get()
+        if E > 8:  # population too spread for the limb grid: fp64 MFMA
+            self._prec = nat.ABC_PREC_F64
+            self._pack_f64()
+
     # -- density -----------------------------------------------------------
     def logpdf_device(self, xd, out=None, hint=None):
         """log density at device points xd [M, d] (columns in fit order).
         hint: optional device int64 [M] rows of the fitted population near
         the points (the ancestors propose_device drew them from)."""
+        self._check_x3_range()
         if self._mfma:
             return gpu.mvn_logpdf(xd, self._dev_packed, self._dev_X.shape[0],
                                   self._dev_mu, self._dev_U, self._prec,
