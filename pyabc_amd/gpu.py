@@ -33,7 +33,8 @@ def require_device():
 
 
 def stream_ptr():
-    return torch.cuda.current_stream().cuda_stream
+    """Raw hipStream_t of the current torch stream (fast C-level query)."""
+    return torch._C._cuda_getCurrentRawStream(torch.cuda.current_device())
 
 
 def p(t):

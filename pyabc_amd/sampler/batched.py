@@ -266,11 +266,10 @@ class BatchedGPUSampler(Sampler):
                   all_accepted, keeps, acc_anc=()):
         rank, ws = dd.world()
         torch = gpu.torch
+        def cat(lst):
+            return lst[0] if len(lst) == 1 else torch.cat(lst, 0)
         if acc_theta:
-            theta = torch.cat(acc_theta, 0)
-            lp = torch.cat(acc_lp, 0)
-            dist = torch.cat(acc_d, 0)
-            x = torch.cat(acc_x, 0)
+            theta, lp, dist, x = cat(acc_theta), cat(acc_lp), cat(acc_d), cat(acc_x)
         else:
             S = len(spec.sum_stat_keys)
             theta = torch.empty((0, d), dtype=gpu.F64, device=dev)
@@ -283,7 +282,7 @@ class BatchedGPUSampler(Sampler):
         else:
             # ancestors of the accepted rows: population rows near them,
             # used by the x3 density kernel as exponent offsets
-            anc = (torch.cat(acc_anc, 0) if acc_anc and
+            anc = (cat(acc_anc) if acc_anc and
                    len(acc_anc) == len(acc_theta) else None)
             lt = spec.transition.logpdf_device(theta, hint=anc)
             w = gpu.importance_weights(lp, lt, spec.weight_scale)

@@ -542,7 +542,8 @@ class ABCSMC:
     def _adapt_population_size(self, t):
         if t == 0:
             return
-        w = self.history.get_model_probabilities(self.history.max_t)["p"].values
+        w = np.array(list(self.history.model_probabilities_dict(
+            self.history.max_t).values()))
         self.population_size.update(self.transitions, w, t)
 
     def _fit_transitions(self, t):

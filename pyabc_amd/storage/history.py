@@ -208,9 +208,15 @@ class History:
         mp = self._gens[t].model_probabilities()
         return pd.DataFrame({"p": list(mp.values())}, index=list(mp.keys()))
 
+    def model_probabilities_dict(self, t=None):
+        """{m: p_m} without building a DataFrame (hot loop)."""
+        t = self.max_t if t is None else t
+        if t not in self._gens:
+            return {}
+        return dict(self._gens[t].model_probabilities())
+
     def alive_models(self, t=None):
-        mp = self.get_model_probabilities(t)
-        return list(mp.index[mp.p > 0])
+        return [m for m, pm in self.model_probabilities_dict(t).items() if pm > 0]
 
     def nr_of_models_alive(self, t=None):
         return len(self.alive_models(t))

@@ -123,10 +123,20 @@ class MultivariateNormalTransition(Transition):
         dev = Xd.device
         self._dev_X = Xd
         self._dev_w = wd
-        self._dev_mu = gpu.as_dev(mean, device=dev)
-        self._dev_U = gpu.as_dev(psd["U"], device=dev) if psd["rank"] else None
-        self._dev_V = gpu.as_dev(psd["V"], device=dev) if psd["rank"] < d else None
-        self._dev_L = gpu.as_dev(psd["L"], device=dev)
+        # one host-to-device copy for all fit constants (mu, U, V, L)
+        parts = [np.asarray(mean, dtype=np.float64).ravel(),
+                 np.asarray(psd["U"], dtype=np.float64).ravel() if psd["rank"] else np.zeros(0),
+                 np.asarray(psd["V"], dtype=np.float64).ravel() if psd["rank"] < d else np.zeros(0),
+                 np.asarray(psd["L"], dtype=np.float64).ravel()]
+        blob = gpu.as_dev(np.concatenate(parts), device=dev)
+        views, o = [], 0
+        for a in parts:
+            views.append(blob[o:o + a.size])
+            o += a.size
+        self._dev_mu = views[0]
+        self._dev_U = views[1].view(d, psd["rank"]) if psd["rank"] else None
+        self._dev_V = views[2].view(d, d - psd["rank"]) if psd["rank"] < d else None
+        self._dev_L = views[3].view(d, d)
         self._dev_cdf = gpu.inclusive_scan(wd)
         self._rank = psd["rank"]
         self._support_tol = psd["tol"]
