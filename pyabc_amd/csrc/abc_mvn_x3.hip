@@ -465,61 +465,86 @@ __global__ void x3_combine_kernel(const double* __restrict__ part_o,
   out[i] = log_const + LN2 * lg;
 }
 
-// fp64 rescue of the listed candidates over the stored whitened population:
-// s_ij = lw_j - |z_i - y_j|^2 / 2 (log2 units, the same s as the MFMA path).
-// Grid (slice, candidate slot): block (sx, cy) takes candidates cy, cy + gy,
-// ... and population rows of slice sx; (max, sum) partials go to pm / pl
+// Rescue of the listed candidates over the stored whitened population:
+// s_ij = lw_j - |z_i - y_j|^2 / 2 (log2 units, the same s as the MFMA path)
+// in fp64, accumulated as an online (max, sum) pair in fp64 with f32 exp2 of
+// the fp64 difference (1e-7 relative per term).  Grid (slice, group): block
+// (sx, gy) takes groups of RQ candidates and the population rows of slice sx;
+// each row of Y is loaded once per group.  (max, sum) partials go to pm / pl
 // [slice][q] (the main kernel's partial arrays, free again after combine).
+constexpr int RQ = 8;
+
+__device__ __forceinline__ void online_add(double s, double& m, double& l) {
+  const double dl = s - m;
+  if (dl > 0.0) { l = l * (double)__builtin_amdgcn_exp2f((float)-dl) + 1.0; m = s; }
+  else l += (double)__builtin_amdgcn_exp2f((float)dl);
+}
+
+__device__ __forceinline__ void online_merge(double& m, double& l, double mo, double lo) {
+  if (!(lo > 0.0)) return;
+  if (!(l > 0.0)) { m = mo; l = lo; return; }
+  if (mo > m) { l = l * exp2(m - mo) + lo; m = mo; }
+  else l += lo * exp2(mo - m);
+}
+
 __global__ __launch_bounds__(256) void x3_rescue_kernel(
     const int64_t* __restrict__ rescue, const unsigned int* __restrict__ nrescue,
     const double* __restrict__ x, int d, const double* __restrict__ mu,
     const double* __restrict__ U, int r, const double* __restrict__ Y,
     const double* __restrict__ lw, int64_t N, double* __restrict__ pm,
     double* __restrict__ pl, int64_t Mpad) {
-  __shared__ double z[MAX_R];
-  __shared__ double sm[4], sl[4];
+  __shared__ double z[RQ][MAX_R];
+  __shared__ double sm[4][RQ], sl[4][RQ];
   const unsigned int n = *nrescue;
   const int64_t per = (N + gridDim.x - 1) / gridDim.x;
   const int64_t j0 = (int64_t)blockIdx.x * per;
   const int64_t j1 = j0 + per < N ? j0 + per : N;
-  for (unsigned int q = blockIdx.y; q < n; q += gridDim.y) {
-    const int64_t i = rescue[q];
-    if (threadIdx.x < r) {
-      const int k = threadIdx.x;
+  for (unsigned int q0 = blockIdx.y * RQ; q0 < n; q0 += gridDim.y * RQ) {
+    const int nq = (int)(n - q0 < (unsigned)RQ ? n - q0 : RQ);
+    for (int e = threadIdx.x; e < RQ * r; e += blockDim.x) {
+      const int c = e / r, k = e % r;
       double acc = 0.0;
-      for (int c = 0; c < d; ++c) acc += (x[i * d + c] - mu[c]) * U[c * r + k];
-      z[k] = acc * SQRT_LOG2E;
+      if (c < nq) {
+        const int64_t i = rescue[q0 + c];
+        for (int cc = 0; cc < d; ++cc) acc += (x[i * d + cc] - mu[cc]) * U[cc * r + k];
+      }
+      z[c][k] = acc * SQRT_LOG2E;
     }
     __syncthreads();
-    double m = -INFINITY, l = 0.0;
+    double m[RQ], l[RQ];
+#pragma unroll
+    for (int c = 0; c < RQ; ++c) { m[c] = -INFINITY; l[c] = 0.0; }
     for (int64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
       const double lwj = lw[j];
       if (!(lwj > -INFINITY)) continue;
-      double q2 = 0.0;
-      for (int k = 0; k < r; ++k) { const double t = z[k] - Y[j * r + k]; q2 += t * t; }
-      const double sj = lwj - 0.5 * q2;
-      if (sj > m) { l = l * exp2(m - sj) + 1.0; m = sj; }
-      else l += exp2(sj - m);
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      const double mo = __shfl_xor(m, o, 64), lo = __shfl_xor(l, o, 64);
-      const double mx = fmax(m, mo);
-      double t = 0.0;
-      if (l > 0.0) t += l * exp2(m - mx);
-      if (lo > 0.0) t += lo * exp2(mo - mx);
-      m = (l > 0.0 || lo > 0.0) ? mx : m;
-      l = t;
+      double q2[RQ];
+#pragma unroll
+      for (int c = 0; c < RQ; ++c) q2[c] = 0.0;
+      for (int k = 0; k < r; ++k) {
+        const double yk = Y[j * r + k];
+#pragma unroll
+        for (int c = 0; c < RQ; ++c) { const double t = z[c][k] - yk; q2[c] += t * t; }
+      }
+#pragma unroll
+      for (int c = 0; c < RQ; ++c) online_add(lwj - 0.5 * q2[c], m[c], l[c]);
     }
     const int wv = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { sm[wv] = m; sl[wv] = l; }
+#pragma unroll
+    for (int c = 0; c < RQ; ++c) {
+      double mc = m[c], lc = l[c];
+      for (int o = 32; o > 0; o >>= 1) {
+        const double mo = __shfl_xor(mc, o, 64), lo = __shfl_xor(lc, o, 64);
+        online_merge(mc, lc, mo, lo);
+      }
+      if ((threadIdx.x & 63) == 0) { sm[wv][c] = mc; sl[wv][c] = lc; }
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      double mx = -INFINITY;
-      for (int k = 0; k < 4; ++k) if (sl[k] > 0.0) mx = fmax(mx, sm[k]);
-      double t = 0.0;
-      for (int k = 0; k < 4; ++k) if (sl[k] > 0.0) t += sl[k] * exp2(sm[k] - mx);
-      pm[(int64_t)blockIdx.x * Mpad + q] = mx;
-      pl[(int64_t)blockIdx.x * Mpad + q] = t;
+    if (threadIdx.x < nq) {
+      const int c = threadIdx.x;
+      double mc = -INFINITY, lc = 0.0;
+      for (int k = 0; k < 4; ++k) online_merge(mc, lc, sm[k][c], sl[k][c]);
+      pm[(int64_t)blockIdx.x * Mpad + q0 + c] = mc;
+      pl[(int64_t)blockIdx.x * Mpad + q0 + c] = lc;
     }
     __syncthreads();
   }
@@ -713,7 +738,7 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
                      hint ? (const float*)cand_o : (const float*)nullptr, out,
                      rescue, nres);
   ABC_LAUNCHED();
-  const int gy = (int)(2048 / p.nchunk > 1 ? 2048 / p.nchunk : 1);
+  const int gy = (int)(1024 / p.nchunk > 1 ? 1024 / p.nchunk : 1);
   hipLaunchKernelGGL(x3_rescue_kernel, dim3((unsigned)p.nchunk, (unsigned)gy),
                      dim3(256), 0, s, rescue, nres, x, d, mu, U, r,
                      (const double*)x3_Y(packed, N, r),
