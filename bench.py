@@ -1,25 +1,28 @@
 """Benchmark: accepted particles / s per ABC-SMC generation on MI355X.
 
-Workload (BASELINE.json configs[1], "c2"): 10-D Gaussian model with the
+Workload (BASELINE.json configs[2], "c3"): 10-D Gaussian model with the
 vectorised simulator y_k = theta_k + 0.5 eps_k, prior N(0, 1)^10, x_0 = 1,
 MultivariateNormalTransition (x3 limb-split f16-MFMA transition density),
-PNormDistance
-p = 2, QuantileEpsilon(alpha = 0.5), population 1e5 per GPU.  A "step" is one
-full generation: batched candidate generation until N_pop are accepted,
-importance weights (the N_acc x N_pop transition density), fit of the next
-transition, epsilon quantile.  Inputs are synthetic and generated on the
-device; nothing is read from the host inside the timed region except the
-per-round accept counts.
+PNormDistance p = 2, QuantileEpsilon(alpha = 0.5), population 1e6 in total.
+A "step" is one full generation: batched candidate generation until N_pop
+are accepted, importance weights (the N_acc x N_pop transition density), fit
+of the next transition, epsilon quantile.  Inputs are synthetic and generated
+on the device; nothing is read from the host inside the timed region except
+the per-round accept counts.  `--pop 100000` runs configs[1] ("c2", the
+one-GPU config); both are reported in DESIGN.md.
 
 Multi-GPU (torch.distributed.run, one rank per GPU, nccl = RCCL): candidates
-are sharded by global index, the population (1e5 x n_gpus particles) is
-replicated by all-gather each generation ("scaling": "weak": per-GPU accepted
-particles fixed; the transition density per GPU grows with the population).
+are sharded by global index, each rank weights its own accepted rows against
+the replicated population, the accepted rows are all-gathered ("scaling":
+"strong": the population -- total work -- is fixed as N grows).  The c3
+population is the one the north star's 8-GPU target is stated on; at c2 size
+one generation is ~3 ms and too small to split over 8 GPUs.
 
 The JSON line also carries the roofline of the dominant kernel (the fused
 cross-term GEMM + exp2 + sum, mvn_x3_kernel) timed with HIP events recorded
-by libabcgpu on the launch stream around each launch, and a CPU baseline: the numpy oracle (oracle/) timed on a
-bounded sample of the same generation on this host.
+by libabcgpu on the launch stream around each launch, and a CPU baseline: the
+numpy oracle (oracle/) timed on a bounded sample of the same generation on
+this host.
 """
 import argparse
 import json
@@ -43,23 +46,30 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pop", type=int, default=100_000, help="per GPU")
+    ap.add_argument("--pop", type=int, default=1_000_000,
+                    help="total population (all GPUs)")
     ap.add_argument("--dim", type=int, default=10)
     ap.add_argument("--precision", default="x3", choices=["x3", "f64", "f32"])
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: functional multi-rank runs on one GPU (tests)")
     return ap.parse_args()
 
 
-def setup_dist():
+def setup_dist(backend="nccl"):
     import torch
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    dev = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev)
     if ws > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
     return rank, ws
 
 
@@ -109,7 +119,7 @@ def build_abc(args, rank, ws):
     prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
     tr = pa.MultivariateNormalTransition(precision=args.precision)
     abc = pa.ABCSMC(model, prior, pa.PNormDistance(p=2),
-                    population_size=args.pop * ws,
+                    population_size=args.pop,
                     transitions=tr, eps=pa.QuantileEpsilon(alpha=0.5),
                     sampler=pa.BatchedGPUSampler(seed=20251016))
     abc.new("sqlite://", {k: 1.0 for k in keys})
@@ -149,7 +159,7 @@ def cpu_baseline(args, population, cov, budget_s):
 def main():
     args = parse()
     import torch
-    rank, ws = setup_dist()
+    rank, ws = setup_dist(args.dist_backend)
     if ws != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {ws}", file=sys.stderr)
     import pyabc_amd as pa  # noqa: F401  (loads libabcgpu.so, fails loudly)
@@ -190,11 +200,12 @@ def main():
     n_before = clock["n0"]
     gens = abc.generation_log[n_before:n_before + args.steps]
     steps = len(gens)
-    t_local = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t_local = torch.tensor([elapsed], dtype=torch.float64,
+                           device="cuda" if args.dist_backend == "nccl" else "cpu")
     if ws > 1:
         torch.distributed.all_reduce(t_local, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t_local.item())
-    n_pop = args.pop * ws
+    n_pop = args.pop
     value = steps * n_pop / elapsed
     pair_evals = steps * n_pop * n_pop / elapsed
     # dominant kernel: the transition-density GEMM launches of the timed region
@@ -238,15 +249,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / max(steps, 1),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": {"x3": "f32 (f16x3-limb MFMA, f32-grade)", "f64": "f64",
                       "f32": "f32"}[args.precision],
             "data": "synthetic (device-generated, counter-based RNG)",
-            "config": {"workload": "c2: 10-D Gaussian, vectorised simulator, "
+            "config": {"workload": ("c3" if n_pop == 1_000_000 else
+                                    ("c2" if n_pop == 100_000 else "custom"))
+                                   + ": 10-D Gaussian, vectorised simulator, "
                                    "MVN transition, PNorm p=2, QuantileEpsilon(0.5)",
-                       "population": n_pop, "population_per_gpu": args.pop,
-                       "d": args.dim, "parallelism": f"candidate-sharded x{ws}"},
+                       "population": n_pop, "accepted_per_gpu": n_pop // ws,
+                       "d": args.dim, "parallelism": f"candidate-sharded x{ws}",
+                       "dist_backend": args.dist_backend if ws > 1 else None},
             "pair_evals_per_s": pair_evals,
             "acceptance_rate_last": n_pop / gens[-1]["n_sim"] if gens else None,
             "generation_ms": [round(1e3 * g["seconds"], 3) for g in gens],

@@ -377,29 +377,27 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
     return (__builtin_amdgcn_exp2f(v[0]) + __builtin_amdgcn_exp2f(v[1])) +
            (__builtin_amdgcn_exp2f(v[2]) + __builtin_amdgcn_exp2f(v[3]));
   };
-  // one tile: units (t, 0..CT-1); `carry` is the last unit of the previous
-  // tile (c = CT-1), summed under the MFMAs of unit (t, 0)
-  auto do_tile = [&](const half8 (&a)[KB], f32x4& carry, bool has_carry) {
+  // one tile: units (t, 0..CT-1); the exp2/sum of unit c - 1 is issued under
+  // the MFMA chain of unit c.  Every candidate slot c sums the same tiles in
+  // the same order, so a candidate's bits do not depend on where it sits in
+  // the launch (and so not on the sharding over ranks).
+  auto do_tile = [&](const half8 (&a)[KB]) {
     f32x4 prev = chain(a, 0);
-    if (has_carry) ls[CT - 1] += expsum(carry);
 #pragma unroll
     for (int c = 1; c < CT; ++c) {
       const f32x4 cur = chain(a, c);
       ls[c - 1] += expsum(prev);
       prev = cur;
     }
-    carry = prev;
+    ls[CT - 1] += expsum(prev);
   };
-  f32x4 carry = {0.f, 0.f, 0.f, 0.f};
-  bool has_carry = false;
   int nflush = 0;
   for (int64_t t = t_begin; t < t_end; t += 2) {
-    do_tile(a0, carry, has_carry);
-    has_carry = true;
+    do_tile(a0);
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) a0[kb] = Al[(tile(t + 2) + kb) * 64];
     if (t + 1 < t_end) {
-      do_tile(a1, carry, true);
+      do_tile(a1);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) a1[kb] = Al[(tile(t + 3) + kb) * 64];
     }
@@ -410,7 +408,6 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
       for (int c = 0; c < CT; ++c) { l64[c] += (double)ls[c]; ls[c] = 0.f; }
     }
   }
-  if (has_carry) ls[CT - 1] += expsum(carry);
 #pragma unroll
   for (int c = 0; c < CT; ++c) l64[c] += (double)ls[c];
   // lanes l, l^16, l^32, l^48 hold the same candidate column (same o)
@@ -584,13 +581,12 @@ PlanX3 make_plan_x3(int64_t M, int64_t N, int r) {
   p.groups = ceil_div(waves, 4);
   p.MTpad = p.groups * 4 * p.CT;
   p.Mpad = p.MTpad * 16;
-  // enough waves to fill 256 CUs (2 waves/SIMD) several times over, chunks
-  // of >= 32 population tiles
-  const int64_t want = ceil_div(8192, p.groups * 4);
-  const int64_t maxc = ceil_div(p.NT, 32);
-  int64_t nc = want < maxc ? want : maxc;
-  nc = ceil_div(nc < 1 ? 1 : nc, 8) * 8;
-  if (nc > 1024) nc = 1024;
+  // Population chunks depend on N only (8..32, a multiple of 8 for the
+  // XCD map): a candidate's summation order -- and so its bits -- does not
+  // depend on M or on its position, which keeps results identical for any
+  // candidate sharding over ranks.  32 chunks fill the chip from M ~ 1e4.
+  int64_t nc = ceil_div(ceil_div(p.NT, 128), 8) * 8;
+  nc = nc < 8 ? 8 : (nc > 32 ? 32 : nc);
   p.nchunk = (int)nc;
   p.tiles_per_chunk = ceil_div(p.NT, p.nchunk);
   return p;

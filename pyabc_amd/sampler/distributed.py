@@ -43,7 +43,7 @@ def allgather_counts(count, device):
     t = torch.tensor([int(count)], dtype=torch.int64, device=device)
     out = [torch.empty_like(t) for _ in range(ws)]
     dist.all_gather(out, t)
-    return np.array([int(o.item()) for o in out])
+    return torch.cat(out).cpu().numpy()      # one host read
 
 
 def cutoff(counts, needed):

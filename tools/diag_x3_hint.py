@@ -44,8 +44,7 @@ def main():
     groups = cdiv(cdiv(MT, CT), 4)
     MTpad = groups * 4 * CT
     Mpad = MTpad * 16
-    nc = min(cdiv(8192, groups * 4), cdiv(NT, 32))
-    nc = min(cdiv(max(nc, 1), 8) * 8, 1024)
+    nc = min(max(cdiv(cdiv(NT, 128), 8) * 8, 8), 32)
     off = 0
 
     def take(n, sz):
