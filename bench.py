@@ -156,6 +156,23 @@ def cpu_baseline(args, population, cov, budget_s):
     return t_cand, t_pdf, n_c, n_p
 
 
+def measured_traffic(args, n_pop):
+    """HBM bytes per launch of the dominant kernel from the committed
+    rocprofv3 --pmc passes (profiles/*_x3_traffic_*.json, written by
+    tools/traffic_from_pmc.py) when they were taken on this workload."""
+    import glob
+    if args.precision != "x3":
+        return None, None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_x3_traffic_*.json"))):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if t.get("population") == n_pop and t.get("d") == args.dim:
+            return t["traffic_bytes"], os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
     import torch
@@ -223,6 +240,12 @@ def main():
                    "f32 accumulation + exp2 + sum)",
              "f64": "mvn_lse_kernel<double> (f64 MFMA cross term + exp2 + LSE)",
              "f32": "mvn_lse_kernel<float> (f32 MFMA cross term + exp2 + LSE)"}
+    traffic, traffic_src = measured_traffic(args, n_pop)
+    # unique bytes one launch must move: the population and candidate
+    # operand images (KB blocks of 32 f16 per row) + the fp64 result
+    kb = kpad // 32 if args.precision == "x3" else None
+    avg_m = k_pairs / max(k_n, 1) / n_pop if k_n else 0
+    algo_bytes = ((n_pop + avg_m) * kb * 64 + avg_m * 8) if kb else None
     out = None
     if rank == 0:
         cpu = None
@@ -276,7 +299,9 @@ def main():
                          "executed_mfma_peak": exec_peak,
                          "executed_frac": executed / exec_peak,
                          "launches": k_n, "avg_launch_ms": avg_ms,
-                         "traffic": None},
+                         "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes": algo_bytes},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
