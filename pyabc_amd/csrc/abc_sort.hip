@@ -1,6 +1,6 @@
-// Stable segmented LSD radix sort of fp64 keys, and the statistics built on
-// it: QuantileEpsilon's weighted quantile and AdaptivePNormDistance's
-// per-column std / median absolute deviation.
+// Stable segmented LSD radix sort of fp64 keys and QuantileEpsilon's weighted
+// quantile built on it; AdaptivePNormDistance's per-column std (two-pass)
+// here and its median absolute deviation by radix select (abc_select.hip).
 //
 // Reference:
 //   weighted_quantile   pyabc/weighted_statistics.py:27-43 (argsort, cumsum,
@@ -36,17 +36,6 @@ __global__ void to_keys_kernel(const double* __restrict__ in, int64_t n,
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = f2key(in[i]);
 }
-// column-major keys from a row-major [R x S] matrix
-__global__ void to_keys_transpose_kernel(const double* __restrict__ X,
-                                         int64_t R, int S,
-                                         uint64_t* __restrict__ out) {
-  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= R * S) return;
-  int64_t r = e / S;
-  int c = (int)(e % S);
-  out[(int64_t)c * R + r] = f2key(X[e]);
-}
-
 // per-thread digit counts -> LDS cnt[16][256] -> exclusive prefix per digit
 // across threads; returns the block total per digit in tot[16] (LDS).
 __device__ void digit_prefix(int (&c)[RDIG], int* cnt, int* seg, int* tot) {
@@ -339,14 +328,30 @@ __global__ __launch_bounds__(256) void colsum_kernel(const double* __restrict__ 
                                                      const double* __restrict__ mean,
                                                      double* __restrict__ part) {
   // thread -> column (c = threadIdx.x + 256 h), rows strided by block
+  // 8 rows in flight per thread (independent partial sums, fixed order)
+  constexpr int U = 8;
+  const int64_t G = gridDim.x;
   for (int c = threadIdx.x; c < S; c += blockDim.x) {
-    double s = 0.0;
+    double acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = 0.0;
     const double m = mean ? mean[c] : 0.0;
-    for (int64_t r = blockIdx.x; r < R; r += gridDim.x) {
-      const double v = X[r * S + c];
-      s += mean ? (v - m) * (v - m) : v;
+    int64_t r = blockIdx.x;
+    for (; r + (U - 1) * G < R; r += U * G) {
+      double v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = X[(r + u * G) * S + c];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] += mean ? (v[u] - m) * (v[u] - m) : v[u];
     }
-    part[(int64_t)blockIdx.x * S + c] = s;
+    for (int u = 0; r < R; r += G, ++u) {
+      const double v = X[r * S + c];
+      acc[u] += mean ? (v - m) * (v - m) : v;
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) sum += acc[u];
+    part[(int64_t)blockIdx.x * S + c] = sum;
   }
 }
 __global__ void colsum_final(const double* __restrict__ part, int nblk, int S,
@@ -359,52 +364,13 @@ __global__ void colsum_final(const double* __restrict__ part, int nblk, int S,
   }
 }
 
-// ---- column MAD from sorted columns -------------------------------------------
-// k-th smallest (0-based) of {med - v_i : i < p} U {v_i - med : i >= p},
-// both increasing sequences (A_j = med - v[p-1-j], B_j = v[p+j] - med).
-__device__ double kth_two(const uint64_t* v, int64_t p, int64_t n, double med,
-                          int64_t k) {
-  const int64_t na = p, nb = n - p;
-  auto A = [&](int64_t j) { return med - key2f(v[p - 1 - j]); };
-  auto Bf = [&](int64_t j) { return key2f(v[p + j]) - med; };
-  // number i of elements taken from A among the first k+1: binary search
-  int64_t lo = (k + 1 - nb) > 0 ? (k + 1 - nb) : 0;
-  int64_t hi = (k + 1) < na ? (k + 1) : na;
-  while (lo < hi) {
-    const int64_t i = (lo + hi) >> 1;   // take i from A, k+1-i from B
-    const int64_t jb = k + 1 - i;
-    // need A[i] >= B[jb-1] (else take more from A)
-    if (i < na && jb > 0 && A(i) < Bf(jb - 1)) lo = i + 1; else hi = i;
-  }
-  const int64_t i = lo, jb = k + 1 - i;
-  double r = -INFINITY;
-  if (i > 0) r = fmax(r, A(i - 1));
-  if (jb > 0) r = fmax(r, Bf(jb - 1));
-  return r;
-}
-
-__global__ void column_mad_kernel(const uint64_t* __restrict__ sorted,
-                                  int64_t R, int S, double* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= S) return;
-  const uint64_t* v = sorted + (int64_t)c * R;
-  double med;
-  if (R & 1) med = key2f(v[R / 2]);
-  else med = (key2f(v[R / 2 - 1]) + key2f(v[R / 2])) / 2.0;
-  // p = first index with v >= med
-  int64_t lo = 0, hi = R;
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    if (key2f(v[mid]) >= med) hi = mid; else lo = mid + 1;
-  }
-  const int64_t p = lo;
-  double mad;
-  if (R & 1) mad = kth_two(v, p, R, med, R / 2);
-  else mad = (kth_two(v, p, R, med, R / 2 - 1) + kth_two(v, p, R, med, R / 2)) / 2.0;
-  out[c] = mad;
-}
-
 }  // namespace
+}  // namespace abc
+
+namespace abc {
+size_t select_ws_bytes(int64_t R, int S);
+int column_mad_select(const double* X, int64_t R, int S, double* out, void* ws,
+                      size_t ws_bytes, hipStream_t s);
 }  // namespace abc
 
 using namespace abc;
@@ -472,7 +438,7 @@ extern "C" int abc_weighted_quantile(const double* points, const double* w,
 }
 
 extern "C" size_t abc_column_stats_workspace(int64_t R, int S) {
-  size_t a = sort_ws_bytes(S, R, false);
+  size_t a = select_ws_bytes(R, S);
   size_t off = 0;
   size_only<double>(off, (size_t)CS_BLOCKS * S);
   size_only<double>(off, (size_t)S);
@@ -507,16 +473,7 @@ extern "C" int abc_column_mad(const double* X, int64_t R, int S, double* out,
   ABC_CHECK_ARG(X && out && ws, "column_mad: null pointer");
   if (ws_bytes < abc_column_stats_workspace(R, S))
     return set_error(ABC_ERR_WORKSPACE, "column_mad: workspace too small");
-  hipStream_t s = as_stream(stream);
-  Carver cv(ws, ws_bytes);
-  SortBufs b;
-  if (!carve_sort(cv, S, R, false, b)) return set_error(ABC_ERR_WORKSPACE, "column_mad: carve");
-  hipLaunchKernelGGL(to_keys_transpose_kernel, dim3((unsigned)ceil_div(R * S, 256)), dim3(256), 0, s,
-                     X, R, S, b.k0);
-  ABC_LAUNCHED();
-  int rc = run_sort(b, S, R, s);
-  if (rc) return rc;
-  hipLaunchKernelGGL(column_mad_kernel, dim3((unsigned)ceil_div(S, 64)), dim3(64), 0, s, b.k0, R, S, out);
-  ABC_LAUNCHED();
-  return ABC_OK;
+  // exact radix select per column (abc_select.hip): median, then the median
+  // of |x - median|; no full sort
+  return column_mad_select(X, R, S, out, ws, ws_bytes, as_stream(stream));
 }

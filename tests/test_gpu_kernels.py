@@ -255,6 +255,29 @@ def test_column_mad_large(dev):
         np.testing.assert_array_equal(mad, oracle.median_absolute_deviation(X))
 
 
+def test_column_mad_select_edges(dev):
+    """Radix-select MAD: R = 1, 2, 3, constant columns, +-0, sign mixes,
+    heavy ties, tiny/huge magnitudes, R across several select levels --
+    bit-exact against np.median(|x - np.median(x)|)."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(8)
+    cols = []
+    for R in (1, 2, 3, 4, 5, 1000, 4096, 65537):
+        X = np.empty((R, 9))
+        X[:, 0] = 3.25                                  # constant
+        X[:, 1] = rng.choice([-0.0, 0.0, 1.0, -1.0], R)  # signed zeros, ties
+        X[:, 2] = rng.standard_normal(R)                 # sign mix
+        X[:, 3] = np.round(rng.standard_normal(R) * 3)   # heavy ties
+        X[:, 4] = rng.standard_normal(R) * 1e-300        # subnormal-ish scale
+        X[:, 5] = rng.standard_normal(R) * 1e300
+        X[:, 6] = np.exp(rng.standard_normal(R) * 20)    # many exponents
+        X[:, 7] = 1.0 + rng.integers(0, 3, R) * 2.0 ** -52  # last-bit ties
+        X[:, 8] = -np.abs(rng.standard_normal(R))
+        mad = gpu.column_mad(T(X)).cpu().numpy()
+        np.testing.assert_array_equal(mad, oracle.median_absolute_deviation(X),
+                                      err_msg=f"R={R}")
+
+
 @pytest.mark.parametrize("N,d", [(10_001, 7), (10_001, 10), (1, 10), (300, 1),
                                  (100_000, 3), (77, 20)])
 def test_weighted_moments(dev, N, d):

@@ -1,0 +1,175 @@
+"""Per-component measurements of the §8 rows beside the transition density.
+
+    python tools/bench_components.py [--only c4,quantile,c5,sampler] [--reps 5]
+
+One JSON line per kernel: the BASELINE.json config it is measured on, the
+average time per call (torch.cuda.Event on the launch stream = torch's
+current stream, which libabcgpu launches on), the algorithmic bytes or FLOP
+per call and the fraction of the HBM (8 TB/s) or fp64 VALU
+peak.  Inputs are synthetic, generated on the device or from seeded numpy.
+
+  c4        AdaptivePNormDistance on 256-dim summary stats, pop 2e5:
+            pnorm over R candidates (R = 6.7e5 recorded at acceptance 0.3),
+            column std and MAD over the recorded [R x 256] matrix
+  quantile  QuantileEpsilon weighted quantile at N = 1e6 (c3) and 1e5 (c2)
+  c5        LocalTransition d = 5, N = 1e5: k-NN covariance fit (k = 50 and
+            the default k = N/4 = 25000), density of 1e5 candidates
+  sampler   propose + simulate + pnorm + accept at the c3 batch (4.6e6)
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+HBM_PEAK = 8.0e12          # B/s (MI355X_MICROARCH.md)
+F64_VALU_PEAK = 78.6e12    # FLOP/s fp64 vector (spec)
+
+
+def timed(fn, reps):
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def emit(component, config, ms, bytes_=None, flop=None, extra=None):
+    rec = {"component": component, "config": config, "ms": round(ms, 4)}
+    if bytes_ is not None:
+        bw = bytes_ / (ms * 1e-3)
+        rec.update(algorithmic_bytes=bytes_, achieved_GBps=round(bw / 1e9, 1),
+                   bound="hbm", frac=round(bw / HBM_PEAK, 4))
+    if flop is not None:
+        fl = flop / (ms * 1e-3)
+        rec.update(algorithmic_flop=flop, achieved_TFLOPs=round(fl / 1e12, 3),
+                   bound="fp64 valu", frac=round(fl / F64_VALU_PEAK, 4))
+    if extra:
+        rec.update(extra)
+    print(json.dumps(rec), flush=True)
+
+
+def c4(reps):
+    import torch
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(1234)
+    S, R = 256, 670_000
+    a = rng.uniform(0.5, 2.0, S)
+    sig = 10.0 ** rng.uniform(-2, 2, S)
+    theta = torch.randn(R, 4, dtype=torch.float64, device="cuda")
+    src = torch.as_tensor(np.arange(S) % 4, device="cuda")
+    X = theta[:, src] * torch.as_tensor(a, device="cuda") + \
+        torch.randn(R, S, dtype=torch.float64, device="cuda") * torch.as_tensor(sig, device="cuda")
+    X = X.contiguous()
+    x0 = gpu.as_dev(a * 0.5)
+    wf = gpu.as_dev(1.0 / sig)
+    out = torch.empty(R, dtype=torch.float64, device="cuda")
+    ms = timed(lambda: gpu.pnorm(X, x0, wf, 2.0, out=out), reps)
+    emit("pnorm (AdaptivePNormDistance.__call__)", "c4: S=256, 6.7e5 candidates",
+         ms, bytes_=R * (8 * S + 8))
+    ms = timed(lambda: gpu.column_std(X), reps)
+    emit("column std (scale update)", "c4: [6.7e5 x 256] recorded", ms,
+         bytes_=R * S * 8 * 2, extra={"note": "two-pass: mean, then squares"})
+    ms = timed(lambda: gpu.column_mad(X), max(1, reps // 2))
+    emit("column MAD (scale update)", "c4: [6.7e5 x 256] recorded", ms,
+         bytes_=R * S * 8 * 2,
+         extra={"note": "algorithmic = median pass + deviation pass, 8 B each"})
+
+
+def quantile(reps):
+    import torch
+    from pyabc_amd import gpu
+    for N, tag in ((1_000_000, "c3"), (100_000, "c2")):
+        d = torch.rand(N, dtype=torch.float64, device="cuda") * 4 + 1
+        w = torch.rand(N, dtype=torch.float64, device="cuda")
+        ms = timed(lambda: gpu.weighted_quantile(d, w, 0.5), reps)
+        emit("weighted quantile (QuantileEpsilon)", f"{tag}: N={N}", ms,
+             bytes_=N * 16)
+
+
+def c5(reps):
+    import torch
+    import pandas as pd
+    from pyabc_amd.transition import LocalTransition
+    rng = np.random.default_rng(99)
+    N, d = 100_000, 5
+    comp = rng.integers(0, 2, N)
+    A = rng.standard_normal((d, d)) * 0.3 + np.eye(d)
+    X = rng.standard_normal((N, d)) @ A.T + np.where(comp[:, None] == 1, 2.0, -1.0)
+    w = np.exp(0.5 * rng.standard_normal(N))
+    w /= w.sum()
+    cols = [f"p{k}" for k in range(d)]
+    for kw, tag in ((dict(k=50, k_fraction=None), "k=50"), (dict(), "k=N/4=25000")):
+        t = LocalTransition(**kw)
+        t.fit(pd.DataFrame(X, columns=cols), w.copy())
+        Xd, wd = t._dev_X, t._dev_w
+        ms = timed(lambda: t._fit_device_arrays(Xd, wd), 1)
+        pair_flop = 3 * d + 2 * (2 + d + d * (d + 1) // 2)
+        emit("LocalTransition.fit (k-NN covariances)", f"c5: N=1e5, d=5, {tag}", ms,
+             flop=N * N * pair_flop,
+             extra={"note": "per (n, j) pair: 3d distance + masked moments"})
+    x = t.propose_device(N)[0]
+    ms = timed(lambda: t.logpdf_device(x), reps)
+    emit("LocalTransition.pdf", "c5: 1e5 candidates x 1e5 particles", ms,
+         flop=N * N * (d * d + 2 * d + 4))
+
+
+def sampler(reps):
+    import torch
+    import pandas as pd
+    from pyabc_amd import gpu
+    from pyabc_amd.transition import MultivariateNormalTransition
+    rng = np.random.default_rng(5)
+    N, d, B = 1_000_000, 10, 4_600_000
+    X = 0.8 + np.sqrt(0.2) * rng.standard_normal((N, d))
+    w = np.exp(0.5 * rng.standard_normal(N))
+    w /= w.sum()
+    t = MultivariateNormalTransition()
+    t.fit(pd.DataFrame(X, columns=[f"p{k}" for k in range(d)]), w.copy())
+    kind = torch.zeros(d, dtype=torch.int32, device="cuda")
+    params = gpu.as_dev(np.tile([0.0, 1.0, 0.0, 0.0], d))
+    res = {}
+
+    def prop():
+        res["p"] = t.propose_device(B, kind, params, seed=3, generation=2,
+                                    idx0=0, max_attempts=100)
+    ms = timed(prop, reps)
+    emit("propose (MVN rvs + prior)", "c3 batch: 4.6e6 candidates", ms,
+         bytes_=B * (8 * d + 8 + 8 + 4 + 8 * d),
+         extra={"note": "theta/lp/ancestor/attempts written + ancestor row read"})
+    th = res["p"][0]
+    src = torch.arange(d, dtype=torch.int32, device="cuda")
+    one, half = gpu.as_dev(np.ones(d)), gpu.as_dev(np.full(d, 0.5))
+    xs = {}
+    ms = timed(lambda: xs.__setitem__("x", gpu.simulate_linear_gaussian(
+        th, src, one, half, 3, 2, 0)), reps)
+    emit("simulate (vectorised linear Gaussian)", "c3 batch", ms,
+         bytes_=B * 16 * d)
+    x = xs["x"]
+    dd = torch.empty(B, dtype=torch.float64, device="cuda")
+    ms = timed(lambda: gpu.pnorm(x, one, one, 2.0, out=dd), reps)
+    emit("pnorm (PNormDistance, S=10)", "c3 batch", ms, bytes_=B * (8 * d + 8))
+    eps = float(dd.median())
+    ms = timed(lambda: gpu.accept_compact(dd, eps), reps)
+    emit("accept + compaction", "c3 batch", ms, bytes_=B * 8 * 2)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="c4,quantile,c5,sampler")
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    for name in a.only.split(","):
+        globals()[name](a.reps)
+
+
+if __name__ == "__main__":
+    main()
