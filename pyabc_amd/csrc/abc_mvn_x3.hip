@@ -255,16 +255,19 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
   const int rl = (int)(row & 15);
   const int K0pad = 32 * KB0;
   const int Ktot = 32 * KB;
-  for (int k = 0; k < Ktot; ++k) {
-    const float val = slot_value<SIDE>(k, r, K0pad, E, L, S);
-    const int kb = k >> 5, kk = k & 31;
-    const int lane = rl + 16 * (kk >> 3), j = kk & 7;
-    img[(((t * KB + kb) * 64) + lane) * 8 + j] = (_Float16)val;
-  }
-  if (SIDE == 1 && hint) {  // B = -o in the offset slot (A = 1)
-    const int kb = koff >> 5, kk = koff & 31;
-    const int lane = rl + 16 * (kk >> 3), j = kk & 7;
-    img[(((t * KB + kb) * 64) + lane) * 8 + j] = (_Float16)(-hint_o);
+  // 8 consecutive K slots of this row form one lane's 16-byte fragment:
+  // assemble them in registers and store them as one vector
+  for (int g = 0; g < Ktot / 8; ++g) {
+    half8 frag;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = g * 8 + j;
+      float val = slot_value<SIDE>(k, r, K0pad, E, L, S);
+      if (SIDE == 1 && hint && k == koff) val = -hint_o;  // B = -o (A = 1)
+      frag[j] = (_Float16)val;
+    }
+    const int kb = g >> 2, lane = rl + 16 * (g & 3);
+    *reinterpret_cast<half8*>(img + (((t * KB + kb) * 64) + lane) * 8) = frag;
   }
 }
 
@@ -469,7 +472,7 @@ __global__ void x3_combine_kernel(const double* __restrict__ part_o,
 // (sx, gy) takes groups of RQ candidates and the population rows of slice sx;
 // each row of Y is loaded once per group.  (max, sum) partials go to pm / pl
 // [slice][q] (the main kernel's partial arrays, free again after combine).
-constexpr int RQ = 8;
+constexpr int RQ = 16;
 
 __device__ __forceinline__ void online_add(double s, double& m, double& l) {
   const double dl = s - m;
