@@ -220,10 +220,7 @@ class BatchedGPUSampler(Sampler):
             recorded = gpu.torch.cat(rec_x, 0) if rec_x else None
             if ws > 1 and recorded is not None:
                 recorded = dd.allgather_rows(recorded, dev)
-                perm = self.global_order(rec_keeps)
-                if perm.size and np.any(perm != np.arange(perm.size)):
-                    recorded = gpu.gather_rows(
-                        recorded, gpu.torch.as_tensor(perm, device=dev))
+                recorded = self.reorder(recorded, self.global_pieces(rec_keeps))
         elif cols is not None:
             recorded = cols.sum_stats
         return ColumnarSample(cols, recorded, spec.sum_stat_keys,
@@ -262,6 +259,28 @@ class BatchedGPUSampler(Sampler):
                          lens)
         return base + np.arange(tot, dtype=np.int64)
 
+    @staticmethod
+    def global_pieces(keeps):
+        """The permutation of global_order as contiguous pieces (start, len)
+        of the rank-major array, in global order (rounds x ranks pieces)."""
+        k = np.asarray(keeps, dtype=np.int64).reshape(len(keeps), -1)
+        if k.size == 0:
+            return []
+        rank_start = np.concatenate([[0], np.cumsum(k.sum(0))[:-1]])
+        round_off = np.cumsum(k, axis=0) - k
+        starts = (rank_start[None, :] + round_off).ravel()
+        return [(int(a), int(n)) for a, n in zip(starts, k.ravel()) if n > 0]
+
+    @staticmethod
+    def reorder(t, pieces):
+        """Rows of t in the order of the pieces (one concatenation)."""
+        if len(pieces) <= 1:
+            return t
+        if all(a == b[0] + b[1] for b, (a, _) in zip(pieces[:-1], pieces[1:])) \
+                and pieces[0][0] == 0:
+            return t          # already in order
+        return gpu.torch.cat([t[a:a + n] for a, n in pieces], 0)
+
     def _assemble(self, spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
                   all_accepted, keeps, acc_anc=()):
         rank, ws = dd.world()
@@ -294,13 +313,8 @@ class BatchedGPUSampler(Sampler):
             # rows arrive rank-major; restore global candidate-index order so
             # the population (and every later draw keyed on it) is the same
             # for any number of ranks
-            perm = self.global_order(keeps)
-            if perm.size and np.any(perm != np.arange(perm.size)):
-                pd_ = torch.as_tensor(perm, device=dev)
-                theta = gpu.gather_rows(theta, pd_)
-                w = gpu.gather_rows(w, pd_)
-                dist = gpu.gather_rows(dist, pd_)
-                x = gpu.gather_rows(x, pd_)
+            pieces = self.global_pieces(keeps)
+            theta, w, dist, x = (self.reorder(a, pieces) for a in (theta, w, dist, x))
         if theta.shape[0] == 0:
             return None
         return ColumnarParticles(theta.contiguous(), w.contiguous(),
