@@ -72,8 +72,8 @@ struct Header { double maxsq; int E; int ok; };
 
 __host__ __device__ constexpr int x3_k0(int r) { return r + 7; }
 __host__ __device__ constexpr int x3_k12(int r) { return 5 * r + 4; }
-__host__ __device__ inline int x3_kb0(int r) { return (x3_k0(r) + 31) / 32; }
-__host__ __device__ inline int x3_kb12(int r) { return (x3_k12(r) + 31) / 32; }
+__host__ __device__ constexpr int x3_kb0(int r) { return (x3_k0(r) + 31) / 32; }
+__host__ __device__ constexpr int x3_kb12(int r) { return (x3_k12(r) + 31) / 32; }
 
 struct Limbs3 { double a1, a2, a3; };  // integers
 struct Limbs5 { double c[5]; };        // integers
@@ -151,17 +151,28 @@ __device__ __forceinline__ float slot_value(int k, int r, int K0pad, int E,
 }
 
 // Whitened, log2-scaled point of row `row`; returns |v|^2 / 2.
+template <int RR = MAX_R>
 __device__ __forceinline__ double whiten(const double* __restrict__ P, int64_t row,
                                          int d, const double* __restrict__ mu,
                                          const double* __restrict__ U, int r,
                                          double* v) {
+  double acc[RR];
+#pragma unroll
+  for (int k = 0; k < RR; ++k) acc[k] = 0.0;
+  for (int q = 0; q < d; ++q) {  // each row element loaded once
+    const double xq = P[row * d + q] - mu[q];
+#pragma unroll
+    for (int k = 0; k < RR; ++k)
+      if (k < r) acc[k] += xq * U[q * r + k];
+  }
   double h = 0.0;
-  for (int k = 0; k < r; ++k) {
-    double acc = 0.0;
-    for (int q = 0; q < d; ++q) acc += (P[row * d + q] - mu[q]) * U[q * r + k];
-    acc *= SQRT_LOG2E;
-    v[k] = acc;
-    h += acc * acc;
+#pragma unroll
+  for (int k = 0; k < RR; ++k) {
+    if (k < r) {
+      const double a = acc[k] * SQRT_LOG2E;
+      v[k] = a;
+      h += a * a;
+    }
   }
   return 0.5 * h;
 }
@@ -195,36 +206,46 @@ __global__ void x3_setup_kernel(Header* __restrict__ hdr, int r,
 }
 
 // One thread per image row (population row or candidate column): computes the
-// limbs and scatters the K slot values into the fragment image.
-template <int SIDE>
+// limbs and scatters the K slot values into the fragment image.  R > 0 fixes
+// the rank at compile time (limb arrays in registers, slot loop unrolled);
+// R = 0 handles any r <= MAX_R with the arrays in scratch.
+template <int SIDE, int R>
 __global__ __launch_bounds__(128) void pack_x3_kernel(
     const double* __restrict__ P, const double* __restrict__ w, int64_t n,
-    int d, const double* __restrict__ mu, const double* __restrict__ U, int r,
-    double log_w_shift, int KB0, int KB, const Header* __restrict__ hdr,
+    int d, const double* __restrict__ mu, const double* __restrict__ U, int r_rt,
+    double log_w_shift, int KB0_rt, int KB_rt, const Header* __restrict__ hdr,
     _Float16* __restrict__ img, int64_t ntiles, int32_t* __restrict__ flags,
     double* __restrict__ Y, double* __restrict__ lw, int64_t Np,
     const int64_t* __restrict__ hint, float* __restrict__ cand_o, int koff) {
   // SIDE 0 writes the fp64 whitened population Y [n x r] and its log2
   // weights lw [n] (rescue + hints); SIDE 1 reads them for the hint rows
+  constexpr int RR = R > 0 ? R : MAX_R;
+  const int r = R > 0 ? R : r_rt;
+  const int KB0 = R > 0 ? x3_kb0(R) : KB0_rt;
+  const int KB = R > 0 ? x3_kb0(R) + x3_kb12(R) : KB_rt;
+  constexpr int NG = R > 0 ? (x3_kb0(R) + x3_kb12(R)) * 4 : 0;  // 8-slot groups
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= ntiles * 16) return;
   const int E = hdr->E;
   const bool ok = hdr->ok != 0;
   const double L2 = ldexp(1.0, 2 * E);  // 2^(2E): bound of |y|^2 and |c|
-  double v[MAX_R];
-  Limbs3 L[MAX_R];
+  double v[RR];
+  Limbs3 L[RR];
   double scalar = SIDE == 0 ? -L2 : 0.0;  // padding: c = -2^(2E), m = 0
   bool bad = false;
   float hint_o = O_MIN;
-  for (int k = 0; k < r; ++k) v[k] = 0.0;
+  #pragma unroll
+  for (int k = 0; k < RR; ++k) v[k] = 0.0;
   if (row < n) {
-    const double h = whiten(P, row, d, mu, U, r, v);
+    const double h = whiten<RR>(P, row, d, mu, U, r, v);
     if (SIDE == 0) {
       const double wj = w[row];
       bad = !(wj > 0.0) || !(2.0 * h <= L2);
       const double lwj = wj > 0.0 ? (log(wj) + log_w_shift) * LOG2E : -INFINITY;
       scalar = bad ? -L2 : fmax(lwj - h, -L2);
-      for (int k = 0; k < r; ++k) Y[row * r + k] = v[k];
+#pragma unroll
+      for (int k = 0; k < RR; ++k)
+        if (k < r) Y[row * r + k] = v[k];
       lw[row] = lwj;
     } else {
       bad = !ok || !(2.0 * h <= L2);
@@ -238,18 +259,22 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
           bad = true;
         } else {
           double q = 0.0;
-          for (int k = 0; k < r; ++k) { const double t = v[k] - Y[j * r + k]; q += t * t; }
+#pragma unroll
+          for (int k = 0; k < RR; ++k)
+            if (k < r) { const double t = v[k] - Y[j * r + k]; q += t * t; }
           hint_o = (float)fmax(ceil(lw[j] - 0.5 * q), (double)O_MIN);
         }
         scalar = bad ? -L2 : -h;
       }
     }
     if (bad)
-      for (int k = 0; k < r; ++k) v[k] = 0.0;
+      #pragma unroll
+  for (int k = 0; k < RR; ++k) v[k] = 0.0;
   }
   if (flags && row < n) flags[row] = bad ? 1 : 0;
   if (cand_o) cand_o[row] = hint_o;
-  for (int k = 0; k < r; ++k) L[k] = split_coord(v[k], E);
+#pragma unroll
+  for (int k = 0; k < RR; ++k) L[k] = split_coord(v[k], E);
   const Limbs5 S = split_scalar(scalar, E);
   const int64_t t = row >> 4;
   const int rl = (int)(row & 15);
@@ -257,7 +282,9 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
   const int Ktot = 32 * KB;
   // 8 consecutive K slots of this row form one lane's 16-byte fragment:
   // assemble them in registers and store them as one vector
-  for (int g = 0; g < Ktot / 8; ++g) {
+#pragma unroll
+  for (int g = 0; g < (R > 0 ? NG : 1 << 30); ++g) {
+    if (g >= Ktot / 8) break;
     half8 frag;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -568,6 +595,28 @@ __global__ void x3_rescue_final(const int64_t* __restrict__ rescue,
   out[rescue[q]] = t > 0.0 ? log_const + LN2 * (mx + log2(t)) : -INFINITY;
 }
 
+template <int SIDE>
+void launch_pack(int r, dim3 grid, hipStream_t s, const double* P, const double* w,
+                 int64_t n, int d, const double* mu, const double* U,
+                 double log_w_shift, int KB0, int KB, const Header* hdr,
+                 _Float16* img, int64_t ntiles, int32_t* flags, double* Y,
+                 double* lw, int64_t Np, const int64_t* hint, float* cand_o,
+                 int koff) {
+#define ABC_PACK_CASE(RC)                                                          \
+  case RC:                                                                         \
+    hipLaunchKernelGGL((pack_x3_kernel<SIDE, RC>), grid, dim3(128), 0, s, P, w, n, \
+                       d, mu, U, r, log_w_shift, KB0, KB, hdr, img, ntiles, flags, \
+                       Y, lw, Np, hint, cand_o, koff);                             \
+    break;
+  switch (r) {
+    ABC_PACK_CASE(1) ABC_PACK_CASE(2) ABC_PACK_CASE(3) ABC_PACK_CASE(4)
+    ABC_PACK_CASE(5) ABC_PACK_CASE(6) ABC_PACK_CASE(7) ABC_PACK_CASE(8)
+    ABC_PACK_CASE(9) ABC_PACK_CASE(10) ABC_PACK_CASE(12) ABC_PACK_CASE(16)
+    default: ABC_PACK_CASE(0)
+  }
+#undef ABC_PACK_CASE
+}
+
 struct PlanX3 {
   int KB0, KB, CT, nchunk;
   int64_t MT, NT, MTpad, groups, tiles_per_chunk, Mpad;
@@ -684,12 +733,11 @@ int x3_pack_population(const double* X, const double* w, int64_t N, int d,
   }
   hipLaunchKernelGGL(x3_setup_kernel, dim3(1), dim3(1), 0, s, hdr, r, range);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(pack_x3_kernel<0>, dim3((unsigned)ceil_div(NT * 16, 128)),
-                     dim3(128), 0, s, X, w, N, d, mu, U, r, log_w_shift,
-                     x3_kb0(r), x3_kb0(r) + x3_kb12(r), (const Header*)hdr,
-                     (_Float16*)((char*)packed + HDR), NT, (int32_t*)nullptr,
-                     x3_Y(packed, N, r), x3_lw(packed, N, r), N,
-                     (const int64_t*)nullptr, (float*)nullptr, 0);
+  launch_pack<0>(r, dim3((unsigned)ceil_div(NT * 16, 128)), s, X, w, N, d, mu, U,
+                 log_w_shift, x3_kb0(r), x3_kb0(r) + x3_kb12(r), (const Header*)hdr,
+                 (_Float16*)((char*)packed + HDR), NT, (int32_t*)nullptr,
+                 x3_Y(packed, N, r), x3_lw(packed, N, r), N, (const int64_t*)nullptr,
+                 (float*)nullptr, 0);
   ABC_LAUNCHED();
   return ABC_OK;
 }
@@ -721,11 +769,10 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
   const Header* hdr = (const Header*)packed;
   const half8* Aimg = (const half8*)((const char*)packed + HDR);
   ABC_HIP(hipMemsetAsync(nres, 0, sizeof(unsigned int), s));
-  hipLaunchKernelGGL(pack_x3_kernel<1>, dim3((unsigned)ceil_div(p.MTpad * 16, 128)),
-                     dim3(128), 0, s, x, (const double*)nullptr, M, d, mu, U, r,
-                     log_norm - log_const, p.KB0, p.KB, hdr, Bimg, p.MTpad, cflags,
-                     x3_Y(packed, N, r), x3_lw(packed, N, r), N, hint,
-                     hint ? cand_o : (float*)nullptr, r + 6);
+  launch_pack<1>(r, dim3((unsigned)ceil_div(p.MTpad * 16, 128)), s, x,
+                 (const double*)nullptr, M, d, mu, U, log_norm - log_const, p.KB0,
+                 p.KB, hdr, Bimg, p.MTpad, cflags, x3_Y(packed, N, r),
+                 x3_lw(packed, N, r), N, hint, hint ? cand_o : (float*)nullptr, r + 6);
   ABC_LAUNCHED();
   profile_start(s);
   int rc = dispatch_x3(p, Aimg, (const half8*)Bimg, r + 6, po, pl, hint == nullptr, s);
