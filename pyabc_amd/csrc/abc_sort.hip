@@ -8,9 +8,8 @@
 //                       pyabc/epsilon/epsilon.py:202-228
 //   std / MAD scales    pyabc/distance/scale.py:38-65 via
 //                       AdaptivePNormDistance._update distance.py:263-307
-// Keys are mapped to order-preserving u64; 4-bit digits, 16 passes, 2048-item
-// tiles; each thread owns 8 consecutive items, so per-digit thread prefixes
-// make the scatter stable.  Segments (columns) are sorted independently: the
+// Keys are mapped to order-preserving u64; 8-bit digits, 8 passes, 2048-item
+// tiles; stable per-wave ranks by ballot multi-split (radix_scatter_kernel).  Segments (columns) are sorted independently: the
 // histogram is laid out [segment][digit][tile], and one global exclusive scan
 // over it yields per-segment offsets because every segment holds exactly
 // seg_len items.
@@ -19,7 +18,7 @@
 namespace abc {
 namespace {
 
-constexpr int RT = 256, RI = 8, RTILE = RT * RI, RBITS = 4, RDIG = 16;
+constexpr int RT = 256, RI = 8, RTILE = RT * RI, RBITS = 8, RDIG = 256;
 
 __device__ __forceinline__ uint64_t f2key(double v) {
   if (v == 0.0) v = 0.0;  // -0.0 ties with +0.0, as in numpy's comparisons
@@ -36,62 +35,49 @@ __global__ void to_keys_kernel(const double* __restrict__ in, int64_t n,
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = f2key(in[i]);
 }
-// per-thread digit counts -> LDS cnt[16][256] -> exclusive prefix per digit
-// across threads; returns the block total per digit in tot[16] (LDS).
-__device__ void digit_prefix(int (&c)[RDIG], int* cnt, int* seg, int* tot) {
-  const int t = threadIdx.x;
+// ---- one LSD pass: 8-bit digits, wave multi-split ranking -------------------
+// Tile = 2048 items; item i of lane l in wave w sits at tile position
+// 512 w + 64 i + l (coalesced loads).  Stable ranks: for each item slot i in
+// order, the lanes holding the same digit find each other with 8 ballots
+// (one per digit bit); a lane's rank is the running per-wave count of its
+// digit (LDS) plus the number of lower lanes with that digit.  Per-wave counts
+// then become per-wave prefixes, and the global offset of (segment, digit,
+// tile) comes from one exclusive scan over the [segment][digit][tile] table.
+constexpr int RW = RT / 64;  // waves per block
+
+__device__ __forceinline__ uint64_t digit_peers(int dg, uint64_t valid) {
+  uint64_t peers = valid;
 #pragma unroll
-  for (int dg = 0; dg < RDIG; ++dg) cnt[dg * RT + t] = c[dg];
-  __syncthreads();
-  {
-    const int dg = t >> 4, sg = t & 15;
-    int s = 0;
-    for (int i = 0; i < 16; ++i) s += cnt[dg * RT + sg * 16 + i];
-    seg[dg * 16 + sg] = s;
+  for (int bit = 0; bit < RBITS; ++bit) {
+    const uint64_t bal = __ballot((dg >> bit) & 1);
+    peers &= ((dg >> bit) & 1) ? bal : ~bal;
   }
-  __syncthreads();
-  if (t < RDIG) {
-    int run = 0;
-    for (int sg = 0; sg < 16; ++sg) { int v = seg[t * 16 + sg]; seg[t * 16 + sg] = run; run += v; }
-    tot[t] = run;
-  }
-  __syncthreads();
-  {
-    const int dg = t >> 4, sg = t & 15;
-    int run = seg[dg * 16 + sg];
-    for (int i = 0; i < 16; ++i) {
-      int v = cnt[dg * RT + sg * 16 + i];
-      cnt[dg * RT + sg * 16 + i] = run;
-      run += v;
-    }
-  }
-  __syncthreads();
+  return peers;
 }
 
 __global__ __launch_bounds__(RT) void radix_hist_kernel(
     const uint64_t* __restrict__ keys, int64_t seg_len, int64_t tps, int shift,
     int64_t* __restrict__ hist) {
-  __shared__ int cnt[RDIG * RT];
-  __shared__ int seg[RDIG * 16];
-  __shared__ int tot[RDIG];
+  __shared__ int cnt[RW][RDIG];
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  for (int e = t; e < RW * RDIG; e += RT) (&cnt[0][0])[e] = 0;
+  __syncthreads();
   const int64_t tile = blockIdx.x;
   const int64_t sgi = tile / tps, tis = tile % tps;
   const int64_t base = sgi * seg_len + tis * RTILE;
   const int64_t lim = seg_len - tis * RTILE;
-  int c[RDIG];
 #pragma unroll
-  for (int dg = 0; dg < RDIG; ++dg) c[dg] = 0;
-  for (int k = 0; k < RI; ++k) {
-    const int64_t o = (int64_t)threadIdx.x * RI + k;
-    if (o < lim) {
-      const int dgt = (int)((keys[base + o] >> shift) & (RDIG - 1));
-#pragma unroll
-      for (int dg = 0; dg < RDIG; ++dg) c[dg] += (dgt == dg);
-    }
+  for (int i = 0; i < RI; ++i) {
+    const int64_t o = (int64_t)wave * (64 * RI) + i * 64 + lane;
+    if (o < lim) atomicAdd(&cnt[wave][(int)((keys[base + o] >> shift) & (RDIG - 1))], 1);
   }
-  digit_prefix(c, cnt, seg, tot);
-  if (threadIdx.x < RDIG)
-    hist[(sgi * RDIG + threadIdx.x) * tps + tis] = tot[threadIdx.x];
+  __syncthreads();
+  for (int dg = t; dg < RDIG; dg += RT) {
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < RW; ++w) tot += cnt[w][dg];
+    hist[(sgi * RDIG + dg) * tps + tis] = tot;
+  }
 }
 
 template <bool VALS>
@@ -99,43 +85,50 @@ __global__ __launch_bounds__(RT) void radix_scatter_kernel(
     const uint64_t* __restrict__ keys, const double* __restrict__ vals,
     int64_t seg_len, int64_t tps, int shift, const int64_t* __restrict__ off,
     uint64_t* __restrict__ keys_out, double* __restrict__ vals_out) {
-  __shared__ int cnt[RDIG * RT];
-  __shared__ int seg[RDIG * 16];
-  __shared__ int tot[RDIG];
+  __shared__ int cnt[RW][RDIG];
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  for (int e = t; e < RW * RDIG; e += RT) (&cnt[0][0])[e] = 0;
+  __syncthreads();
   const int64_t tile = blockIdx.x;
   const int64_t sgi = tile / tps, tis = tile % tps;
   const int64_t base = sgi * seg_len + tis * RTILE;
   const int64_t lim = seg_len - tis * RTILE;
+  const uint64_t lt = (1ull << lane) - 1;
   uint64_t kv[RI];
-  int c[RDIG];
+  double vv[RI];
+  int dg[RI], pos[RI];
 #pragma unroll
-  for (int dg = 0; dg < RDIG; ++dg) c[dg] = 0;
+  for (int i = 0; i < RI; ++i) {
+    const int64_t o = (int64_t)wave * (64 * RI) + i * 64 + lane;
+    const bool ok = o < lim;
+    kv[i] = ok ? keys[base + o] : 0;
+    if (VALS) vv[i] = ok ? vals[base + o] : 0.0;
+    dg[i] = (int)((kv[i] >> shift) & (RDIG - 1));
+    const uint64_t valid = __ballot(ok);
+    const uint64_t peers = digit_peers(dg[i], valid);
+    int before = 0;
+    if (ok) before = cnt[wave][dg[i]];
+    pos[i] = ok ? before + __popcll(peers & lt) : -1;
+    if (ok && (peers & lt) == 0) cnt[wave][dg[i]] = before + __popcll(peers);
+  }
+  __syncthreads();
+  // per-wave counts -> global start of each wave's run of each digit
+  for (int d = t; d < RDIG; d += RT) {
+    int64_t run = off[(sgi * RDIG + d) * tps + tis];
 #pragma unroll
-  for (int k = 0; k < RI; ++k) {
-    const int64_t o = (int64_t)threadIdx.x * RI + k;
-    kv[k] = (o < lim) ? keys[base + o] : 0;
-    if (o < lim) {
-      const int dgt = (int)((kv[k] >> shift) & (RDIG - 1));
-#pragma unroll
-      for (int dg = 0; dg < RDIG; ++dg) c[dg] += (dgt == dg);
+    for (int w = 0; w < RW; ++w) {
+      const int c = cnt[w][d];
+      cnt[w][d] = (int)(run - sgi * seg_len);  // segment-relative (fits int)
+      run += c;
     }
   }
-  digit_prefix(c, cnt, seg, tot);
-  int64_t pos[RDIG];
+  __syncthreads();
 #pragma unroll
-  for (int dg = 0; dg < RDIG; ++dg)
-    pos[dg] = off[(sgi * RDIG + dg) * tps + tis] + cnt[dg * RT + threadIdx.x];
-#pragma unroll
-  for (int k = 0; k < RI; ++k) {
-    const int64_t o = (int64_t)threadIdx.x * RI + k;
-    if (o < lim) {
-      const int dgt = (int)((kv[k] >> shift) & (RDIG - 1));
-      int64_t p = 0;
-#pragma unroll
-      for (int dg = 0; dg < RDIG; ++dg)
-        if (dg == dgt) { p = pos[dg]; pos[dg] = p + 1; }
-      keys_out[p] = kv[k];
-      if (VALS) vals_out[p] = vals[base + o];
+  for (int i = 0; i < RI; ++i) {
+    if (pos[i] >= 0) {
+      const int64_t p = sgi * seg_len + cnt[wave][dg[i]] + pos[i];
+      keys_out[p] = kv[i];
+      if (VALS) vals_out[p] = vv[i];
     }
   }
 }
@@ -195,21 +188,39 @@ __global__ __launch_bounds__(ST) void exscan_apply(const int64_t* __restrict__ i
   for (int k = 0; k < SI; ++k) { if (b + k < n) out[b + k] = run; run += v[k]; }
 }
 
-// single-workgroup exclusive scan for small histograms (n <= SCAN1_MAX):
-// one launch instead of three; fixed order, deterministic
-constexpr int64_t SCAN1_MAX = 1 << 14;
-__global__ __launch_bounds__(ST) void exscan_single(const int64_t* __restrict__ in,
-                                                    int64_t n,
-                                                    int64_t* __restrict__ out) {
-  __shared__ int64_t sh[ST];
-  const int64_t per = (n + ST - 1) / ST;
-  const int64_t b0 = threadIdx.x * per;
+// single-workgroup exclusive scan for histograms up to SCAN1_MAX entries: one
+// launch instead of three.  1024 threads, each with S1_PER consecutive
+// entries loaded up front (all loads in flight together), wave-shuffle scan of
+// the thread sums, LDS across the 16 waves; fixed order, deterministic.
+constexpr int S1_T = 1024, S1_PER = 16;
+constexpr int64_t SCAN1_MAX = (int64_t)S1_T * S1_PER;
+__global__ __launch_bounds__(S1_T) void exscan_single(const int64_t* __restrict__ in,
+                                                      int64_t n,
+                                                      int64_t* __restrict__ out) {
+  __shared__ int64_t wsum[S1_T / 64];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t per = (n + S1_T - 1) / S1_T;  // <= S1_PER
+  const int64_t b0 = (int64_t)t * per;
+  int64_t v[S1_PER];
   int64_t s = 0;
-  for (int64_t k = 0; k < per; ++k) if (b0 + k < n) s += in[b0 + k];
-  int64_t tot;
-  int64_t run = block_exscan(s, sh, tot);
-  for (int64_t k = 0; k < per; ++k)
-    if (b0 + k < n) { const int64_t v = in[b0 + k]; out[b0 + k] = run; run += v; }
+#pragma unroll
+  for (int k = 0; k < S1_PER; ++k) {
+    v[k] = (k < per && b0 + k < n) ? in[b0 + k] : 0;
+    s += v[k];
+  }
+  int64_t incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  int64_t run = incl - s;
+  for (int w = 0; w < wv; ++w) run += wsum[w];
+#pragma unroll
+  for (int k = 0; k < S1_PER; ++k)
+    if (k < per && b0 + k < n) { out[b0 + k] = run; run += v[k]; }
 }
 
 struct SortBufs {
@@ -246,7 +257,7 @@ bool carve_sort(Carver& cv, int64_t nseg, int64_t seg_len, bool vals, SortBufs& 
 }
 
 // Sorts keys (already in b.k0, values in b.v0); result lands in b.k0/b.v0
-// (16 passes = even number of swaps).
+// (8 passes = even number of swaps).
 int run_sort(SortBufs& b, int64_t nseg, int64_t seg_len, hipStream_t s) {
   const int64_t tps = ceil_div(seg_len > 0 ? seg_len : 1, RTILE);
   const int64_t ntile = nseg * tps;
@@ -258,7 +269,7 @@ int run_sort(SortBufs& b, int64_t nseg, int64_t seg_len, hipStream_t s) {
                        seg_len, tps, shift, b.hist);
     ABC_LAUNCHED();
     if (nh <= SCAN1_MAX) {
-      hipLaunchKernelGGL(exscan_single, dim3(1), dim3(ST), 0, s, b.hist, nh, b.off);
+      hipLaunchKernelGGL(exscan_single, dim3(1), dim3(S1_T), 0, s, b.hist, nh, b.off);
       ABC_LAUNCHED();
     } else {
       hipLaunchKernelGGL(exscan_sums, dim3((unsigned)nsum), dim3(ST), 0, s, b.hist, nh,
