@@ -22,14 +22,25 @@ namespace abc {
 namespace {
 
 constexpr double LOG_2PI = 1.8378770664093454836;
+constexpr double LOG2E_L = 1.4426950408889634074;
+constexpr double LN2_L = 0.69314718055994530942;
 
+// squared distance with explicit fma: the select and accumulate kernels must
+// produce bit-identical keys
+template <int D>
+__device__ __forceinline__ double dist2v(const double (&xj)[D], const double* xn) {
+  double s = 0.0;
+#pragma unroll
+  for (int q = 0; q < D; ++q) { const double t = xj[q] - xn[q]; s = __builtin_fma(t, t, s); }
+  return s;
+}
 template <int D>
 __device__ __forceinline__ double dist2(const double* __restrict__ X, int64_t j,
                                         const double (&xn)[D]) {
-  double s = 0.0;
+  double xj[D];
 #pragma unroll
-  for (int q = 0; q < D; ++q) { double t = X[j * D + q] - xn[q]; s += t * t; }
-  return s;
+  for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
+  return dist2v<D>(xj, xn);
 }
 
 template <int D>
@@ -108,109 +119,206 @@ __device__ void cholesky(const double (&a)[D][D], double (&L)[D][D]) {
       for (int j = 0; j < D; ++j) L[i][j] = (i == j) ? sqrt(fabs(a[i][i])) : 0.0;
 }
 
-template <int D>
+// k-NN selection for PB particles per block: MSD radix select (8 passes of
+// 8 bits) of the rank nq-1 squared distance, every streamed row X[j] shared by
+// the block's PB particles (PB x less L2 traffic than one particle per block).
+// Writes, per particle, the key v* of rank nq-1, how many keys equal to v*
+// are inside the k+1 nearest (ties taken by index), and the rank-0 index (the
+// smallest index at distance 0, dropped like indices[n, 1:] in the reference).
+template <int D, int PB>
+__global__ __launch_bounds__(256) void local_select_kernel(
+    const double* __restrict__ X, int64_t N, int64_t nq,
+    unsigned long long* __restrict__ sel_v, long long* __restrict__ sel_jcut,
+    long long* __restrict__ sel_rank0) {
+  __shared__ unsigned hist[PB][256];
+  __shared__ long long s_tot[PB];
+  __shared__ int s_cnt[4];
+  __shared__ double xn[PB][D];
+  __shared__ unsigned long long s_prefix[PB], s_rank0[PB];
+  __shared__ long long s_rank[PB];
+  const int tid = threadIdx.x;
+  const int64_t n0 = (int64_t)blockIdx.x * PB;
+  for (int e = tid; e < PB * D; e += 256) {
+    const int p = e / D, q = e % D;
+    const int64_t n = n0 + p < N ? n0 + p : N - 1;  // pad: duplicate, not written
+    xn[p][q] = X[n * D + q];
+  }
+  if (tid < PB) { s_prefix[tid] = 0ull; s_rank[tid] = nq - 1; s_rank0[tid] = (unsigned long long)N; }
+  __syncthreads();
+  double xr[PB][D];  // the block's particles in registers (no LDS reads per pair)
+#pragma unroll
+  for (int p = 0; p < PB; ++p)
+#pragma unroll
+    for (int q = 0; q < D; ++q) xr[p][q] = xn[p][q];
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+    for (int e = tid; e < PB * 256; e += 256) (&hist[0][0])[e] = 0u;
+    unsigned long long pre[PB];
+#pragma unroll
+    for (int p = 0; p < PB; ++p) pre[p] = s_prefix[p];
+    __syncthreads();
+    for (int64_t j = tid; j < N; j += 256) {
+      double xj[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
+#pragma unroll
+      for (int p = 0; p < PB; ++p) {
+        const unsigned long long key =
+            (unsigned long long)__double_as_longlong(dist2v<D>(xj, xr[p]));
+        const bool match = (pass == 0) || ((key >> (shift + 8)) == pre[p]);
+        if (match) atomicAdd(&hist[p][(key >> shift) & 255ull], 1u);
+        if (pass == 0 && key == 0ull) atomicMin(&s_rank0[p], (unsigned long long)j);
+      }
+    }
+    __syncthreads();
+    if (tid < PB) {
+      long long r = s_rank[tid];
+      int b = 0;
+      for (; b < 256; ++b) {
+        if (r < (long long)hist[tid][b]) break;
+        r -= hist[tid][b];
+      }
+      s_rank[tid] = r;
+      s_prefix[tid] = (pre[tid] << 8) | (unsigned long long)b;
+      s_tot[tid] = hist[tid][b];  // last pass: number of keys equal to v*
+    }
+    __syncthreads();
+  }
+  // keys equal to v* enter in index order: ties_in = s_rank + 1 of s_tot.  If
+  // not all of them do, find the index cutoff with an ordered sweep (rare:
+  // only duplicated distances)
+  for (int p = 0; p < PB; ++p) {
+    const long long ties_in = s_rank[p] + 1;
+    long long jcut = N;
+    if (ties_in < s_tot[p]) {
+      const unsigned long long vs = s_prefix[p];
+      long long seen = 0;
+      jcut = -1;
+      for (int64_t c0 = 0; c0 < N && jcut < 0; c0 += 256) {
+        const int64_t j = c0 + tid;
+        double xj[D];
+#pragma unroll
+        for (int q = 0; q < D; ++q) xj[q] = j < N ? X[j * D + q] : 0.0;
+        const bool tie = j < N &&
+            (unsigned long long)__double_as_longlong(dist2v<D>(xj, xn[p])) == vs;
+        const unsigned long long bal = __ballot(tie);
+        const int lane = tid & 63, wv = tid >> 6;
+        if (lane == 0) s_cnt[wv] = __popcll(bal);
+        __syncthreads();
+        int before = __popcll(bal & ((1ull << lane) - 1ull)), total = 0;
+        for (int t = 0; t < 4; ++t) { const int v = s_cnt[t]; if (t < wv) before += v; total += v; }
+        // the ties_in-th tie (0-based ties_in - 1) sets the cutoff
+        if (tie && seen + before == ties_in - 1) s_rank[p] = j + 1;
+        __syncthreads();
+        seen += total;
+        if (seen >= ties_in) jcut = s_rank[p];
+        __syncthreads();
+      }
+    }
+    if (tid == 0 && n0 + p < N) {
+      sel_v[n0 + p] = s_prefix[p];
+      sel_jcut[n0 + p] = jcut;
+      sel_rank0[n0 + p] = (long long)s_rank0[p];
+    }
+  }
+}
+
+// Covariance of the selected neighbours of PB particles per block: the rows
+// are streamed once per block, neighbour membership is order free
+// (key < v*, or key == v* and j < jcut; the rank-0 index excluded), the
+// moments (sum a, sum a^2, sum a d, upper triangle of sum a d d^T with a the
+// neighbour's weight) sit in registers, blocks reduce in a fixed order.  Thread
+// p < PB then applies the reference's fix-ups and factorisations.
+template <int D, int PB>
 __global__ __launch_bounds__(256) void local_fit_kernel(
     const double* __restrict__ X, const double* __restrict__ w, int64_t N,
-    int64_t nq, double scaling, double eps, double* __restrict__ covs,
+    int64_t nq, double scaling, double eps,
+    const unsigned long long* __restrict__ sel_v,
+    const long long* __restrict__ sel_jcut,
+    const long long* __restrict__ sel_rank0, double* __restrict__ covs,
     double* __restrict__ invs, double* __restrict__ dets,
     double* __restrict__ chol, double* __restrict__ lnorm) {
-  constexpr int NM = 2 + D + D * D;  // sum lw, sum lw^2, sum lw d, sum lw dd^T
-  __shared__ unsigned hist[256];
-  __shared__ unsigned long long sh_prefix;
-  __shared__ long long sh_rank;
-  __shared__ unsigned long long sh_rank0;
-  __shared__ double red[NM][4];
-  __shared__ int sh_ties[4];
-  const int64_t n = blockIdx.x;
+  constexpr int NT = D * (D + 1) / 2;
+  constexpr int NM = 2 + D + NT;
+  __shared__ double red[PB][NM][4];
+  __shared__ double xn[PB][D];
   const int tid = threadIdx.x;
-  double xn[D];
+  const int64_t n0 = (int64_t)blockIdx.x * PB;
+  for (int e = tid; e < PB * D; e += 256) {
+    const int p = e / D, q = e % D;
+    const int64_t n = n0 + p < N ? n0 + p : N - 1;
+    xn[p][q] = X[n * D + q];
+  }
+  __syncthreads();
+  unsigned long long vs[PB];
+  long long jcut[PB], r0[PB];
 #pragma unroll
-  for (int q = 0; q < D; ++q) xn[q] = X[n * D + q];
-
+  for (int p = 0; p < PB; ++p) {
+    const int64_t n = n0 + p < N ? n0 + p : N - 1;
+    vs[p] = N > 1 ? sel_v[n] : 0ull;
+    jcut[p] = N > 1 ? sel_jcut[n] : 0;
+    r0[p] = N > 1 ? sel_rank0[n] : -1;
+  }
+  double m[PB][NM];
+#pragma unroll
+  for (int p = 0; p < PB; ++p)
+#pragma unroll
+    for (int t = 0; t < NM; ++t) m[p][t] = 0.0;
+  if (N > 1) {
+    for (int64_t j = tid; j < N; j += 256) {
+      double xj[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
+      const double lw = w[j];
+#pragma unroll
+      for (int p = 0; p < PB; ++p) {
+        const unsigned long long key =
+            (unsigned long long)__double_as_longlong(dist2v<D>(xj, xn[p]));
+        const bool inc = (key < vs[p] || (key == vs[p] && j < jcut[p])) && j != r0[p];
+        if (inc) {
+          double dj[D];
+#pragma unroll
+          for (int q = 0; q < D; ++q) dj[q] = xj[q] - xn[p][q];
+          m[p][0] += lw;
+          m[p][1] += lw * lw;
+          int c = 2 + D;
+#pragma unroll
+          for (int a = 0; a < D; ++a) {
+            m[p][2 + a] += lw * dj[a];
+#pragma unroll
+            for (int b = a; b < D; ++b) m[p][c++] += lw * dj[a] * dj[b];
+          }
+        }
+      }
+    }
+  }
+  // deterministic block reduction: wave shuffle, then the 4 waves in order
+#pragma unroll
+  for (int p = 0; p < PB; ++p)
+#pragma unroll
+    for (int t = 0; t < NM; ++t) {
+      const double v = wave_sum(m[p][t]);
+      if ((tid & 63) == 0) red[p][t][tid >> 6] = v;
+    }
+  __syncthreads();
+  if (tid >= PB || n0 + tid >= N) return;
+  const int p = tid;
+  const int64_t n = n0 + p;
   double cov[D][D];
   if (N == 1) {
     // indices is 1-D -> deltas = |X|, one sample -> diag(|X[0]|)
     for (int a = 0; a < D; ++a)
       for (int b = 0; b < D; ++b) cov[a][b] = (a == b) ? fabs(X[a]) : 0.0;
   } else {
-    if (tid == 0) { sh_prefix = 0ull; sh_rank = nq - 1; sh_rank0 = (unsigned long long)N; }
-    __syncthreads();
-    // MSD radix select of the element at rank nq-1
-    for (int pass = 0; pass < 8; ++pass) {
-      const int shift = 56 - 8 * pass;
-      hist[tid] = 0u;
-      __syncthreads();
-      const unsigned long long pre = sh_prefix;
-      for (int64_t j = tid; j < N; j += 256) {
-        const unsigned long long key = (unsigned long long)__double_as_longlong(dist2<D>(X, j, xn));
-        const bool match = (pass == 0) || ((key >> (shift + 8)) == pre);
-        if (match) atomicAdd(&hist[(key >> shift) & 255ull], 1u);
-        // rank-0 element: smallest index at squared distance 0
-        if (pass == 0 && key == 0ull) atomicMin(&sh_rank0, (unsigned long long)j);
-      }
-      __syncthreads();
-      if (tid == 0) {
-        long long r = sh_rank;
-        int b = 0;
-        for (; b < 256; ++b) {
-          if (r < (long long)hist[b]) break;
-          r -= hist[b];
-        }
-        sh_rank = r;
-        sh_prefix = (pre << 8) | (unsigned long long)b;
-      }
-      __syncthreads();
-    }
-    const unsigned long long vstar = sh_prefix;
-    const long long ties_in = sh_rank + 1;  // ties at vstar included (by index)
-    const long long rank0 = (long long)sh_rank0;
-    // ordered accumulation pass
-    double m[NM];
-#pragma unroll
-    for (int t = 0; t < NM; ++t) m[t] = 0.0;
-    long long ties_before = 0;
-    for (int64_t c0 = 0; c0 < N; c0 += 256) {
-      const int64_t j = c0 + tid;
-      unsigned long long key = ~0ull;
-      double dj[D];
-      if (j < N) {
-#pragma unroll
-        for (int q = 0; q < D; ++q) dj[q] = X[j * D + q] - xn[q];
-        key = (unsigned long long)__double_as_longlong(dist2<D>(X, j, xn));
-      }
-      const int tie = (j < N && key == vstar) ? 1 : 0;
-      // exclusive prefix of ties in index order within the chunk (ballots)
-      const unsigned long long bal = __ballot(tie);
-      const int lane = tid & 63, wv = tid >> 6;
-      if (lane == 0) sh_ties[wv] = __popcll(bal);
-      __syncthreads();
-      int before = __popcll(bal & ((1ull << lane) - 1ull)), total = 0;
-      for (int t = 0; t < 4; ++t) { const int v = sh_ties[t]; if (t < wv) before += v; total += v; }
-      __syncthreads();
-      bool inc = (j < N) && (key < vstar || (tie && ties_before + before < ties_in));
-      if (j == rank0) inc = false;
-      if (inc) {
-        const double lw = w[j];
-        m[0] += lw; m[1] += lw * lw;
-#pragma unroll
-        for (int a = 0; a < D; ++a) {
-          m[2 + a] += lw * dj[a];
-#pragma unroll
-          for (int b = 0; b < D; ++b) m[2 + D + a * D + b] += lw * dj[a] * dj[b];
-        }
-      }
-      ties_before += total;
-    }
-    // deterministic block reduction: wave shuffle, then 4 waves in order
-#pragma unroll
-    for (int t = 0; t < NM; ++t) {
-      double v = wave_sum(m[t]);
-      if ((tid & 63) == 0) red[t][tid >> 6] = v;
-    }
-    __syncthreads();
-    if (tid != 0) return;
     double M[NM];
-    for (int t = 0; t < NM; ++t) M[t] = ((red[t][0] + red[t][1]) + red[t][2]) + red[t][3];
+    for (int t = 0; t < NM; ++t)
+      M[t] = ((red[p][t][0] + red[p][t][1]) + red[p][t][2]) + red[p][t][3];
+    double S2[D][D];
+    {
+      int c = 2 + D;
+      for (int a = 0; a < D; ++a)
+        for (int b = a; b < D; ++b) { S2[a][b] = M[c]; S2[b][a] = M[c]; ++c; }
+    }
     const long long nnb = nq - 1;
     if (nnb == 1) {
       // one neighbour: smart_cov -> diag(|delta|); delta = sum lw d / lw
@@ -225,10 +333,9 @@ __global__ __launch_bounds__(256) void local_fit_kernel(
       for (int a = 0; a < D; ++a) mean[a] = M[2 + a] / sw;
       for (int a = 0; a < D; ++a)
         for (int b = 0; b < D; ++b)
-          cov[a][b] = (M[2 + D + a * D + b] / sw - mean[a] * mean[b]) / (1.0 - sa2);
+          cov[a][b] = (S2[a][b] / sw - mean[a] * mean[b]) / (1.0 - sa2);
     }
   }
-  if (tid != 0) return;
   double csum = 0.0;
   for (int a = 0; a < D; ++a)
     for (int b = 0; b < D; ++b) csum += cov[a][b];
@@ -254,7 +361,9 @@ __global__ __launch_bounds__(256) void local_fit_kernel(
   lnorm[n] = 0.5 * (D * LOG_2PI + log(det));
 }
 
-// density: block of 256 candidates, population staged through LDS in tiles
+// density: block of 256 candidates, population staged through LDS in tiles;
+// exponents in fp64, the online log-sum-exp in log2 units with f32 exp2
+// (~1e-7 relative, the north star's fp32 bar is 1e-5)
 template <int D>
 __global__ __launch_bounds__(256) void local_pdf_kernel(
     const double* __restrict__ x, int64_t M, const double* __restrict__ X,
@@ -276,9 +385,10 @@ __global__ __launch_bounds__(256) void local_pdf_kernel(
       const int jj = e / REC, f = e % REC;
       const int64_t j = j0 + jj;
       double v;
+      // log2 units: the exponent sums run on the f32 exp2 unit
       if (f < D) v = X[j * D + f];
-      else if (f < D + D * D) v = invs[j * D * D + (f - D)];
-      else { const double wj = w[j]; v = (wj > 0.0) ? log(wj) - lnorm[j] : -INFINITY; }
+      else if (f < D + D * D) v = invs[j * D * D + (f - D)] * (0.5 * LOG2E_L);
+      else { const double wj = w[j]; v = (wj > 0.0) ? (log(wj) - lnorm[j]) * LOG2E_L : -INFINITY; }
       tile[jj * REC + f] = v;
     }
     __syncthreads();
@@ -295,9 +405,11 @@ __global__ __launch_bounds__(256) void local_pdf_kernel(
         for (int b = 0; b < D; ++b) t += r[D + a * D + b] * dv[b];
         md += dv[a] * t;
       }
-      const double s = r[D + D * D] - 0.5 * md;
-      if (s > m) { l = l * exp(m - s) + 1.0; m = s; }
-      else if (s > -INFINITY) l += exp(s - m);
+      // s in fp64 (log2 units); 2^(s - m) on v_exp_f32 (1e-7 per term)
+      const double s = r[D + D * D] - md;
+      const double dl = s - m;
+      if (dl > 0.0) { l = l * (double)__builtin_amdgcn_exp2f((float)-dl) + 1.0; m = s; }
+      else if (s > -INFINITY) l += (double)__builtin_amdgcn_exp2f((float)dl);
     }
   }
   // sum of weights (np.average denominator), same for every candidate
@@ -307,15 +419,31 @@ __global__ __launch_bounds__(256) void local_pdf_kernel(
   if ((threadIdx.x & 63) == 0) wsum_sh[threadIdx.x >> 6] = ws;
   __syncthreads();
   wsum = ((wsum_sh[0] + wsum_sh[1]) + wsum_sh[2]) + wsum_sh[3];
-  if (i < M) out[i] = (l > 0.0) ? m + log(l) - log(wsum) : -INFINITY;
+  if (i < M) out[i] = (l > 0.0) ? LN2_L * (m + log2(l)) - log(wsum) : -INFINITY;
 }
+
+constexpr int SEL_PB = 8;  // particles per selection block (in registers)
 
 template <int D>
 int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
                double scaling, double eps, double* covs, double* inv,
-               double* dets, double* chol, double* lnorm, hipStream_t s) {
-  hipLaunchKernelGGL(local_fit_kernel<D>, dim3((unsigned)N), dim3(256), 0, s, X, w, N, nq,
-                     scaling, eps, covs, inv, dets, chol, lnorm);
+               double* dets, double* chol, double* lnorm, void* ws,
+               size_t ws_bytes, hipStream_t s) {
+  Carver cv(ws, ws_bytes);
+  unsigned long long* sel_v = cv.take<unsigned long long>((size_t)N);
+  long long* sel_ties = cv.take<long long>((size_t)N);  // index cutoff of the ties
+  long long* sel_rank0 = cv.take<long long>((size_t)N);
+  if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
+  if (N > 1) {
+    hipLaunchKernelGGL((local_select_kernel<D, SEL_PB>), dim3((unsigned)ceil_div(N, SEL_PB)),
+                       dim3(256), 0, s, X, N, nq, sel_v, sel_ties, sel_rank0);
+    ABC_LAUNCHED();
+  }
+  constexpr int FPB = D <= 5 ? 4 : 2;  // particles per accumulation block
+  hipLaunchKernelGGL((local_fit_kernel<D, FPB>), dim3((unsigned)ceil_div(N, FPB)), dim3(256),
+                     0, s, X, w, N, nq, scaling, eps, (const unsigned long long*)sel_v,
+                     (const long long*)sel_ties, (const long long*)sel_rank0, covs, inv,
+                     dets, chol, lnorm);
   ABC_LAUNCHED();
   return ABC_OK;
 }
@@ -336,8 +464,10 @@ int launch_pdf(const double* x, int64_t M, const double* X, const double* w,
 using namespace abc;
 
 extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
-  (void)N; (void)d;
-  return 0;
+  (void)d;
+  size_t off = 0;
+  for (int i = 0; i < 3; ++i) size_only<int64_t>(off, (size_t)(N > 0 ? N : 1));
+  return off + 256;
 }
 
 extern "C" int abc_local_fit(const double* X, const double* w, int64_t N,
@@ -345,13 +475,13 @@ extern "C" int abc_local_fit(const double* X, const double* w, int64_t N,
                              double* covs, double* inv_covs, double* dets,
                              double* chol, double* log_norm, void* ws,
                              size_t ws_bytes, void* stream) {
-  (void)ws; (void)ws_bytes;
   ABC_CHECK_ARG(N >= 1 && d >= 1 && d <= 8 && k >= 1, "local_fit: bad N/d/k (d <= 8)");
+  ABC_CHECK_ARG(ws && ws_bytes >= abc_local_fit_workspace(N, d), "local_fit: workspace");
   ABC_CHECK_ARG(X && w && covs && inv_covs && dets && chol && log_norm, "local_fit: null pointer");
   const int64_t nq = (k + 1) < N ? (k + 1) : N;
   hipStream_t s = as_stream(stream);
   switch (d) {
-#define ABC_D(n) case n: return launch_fit<n>(X, w, N, nq, scaling, eps, covs, inv_covs, dets, chol, log_norm, s);
+#define ABC_D(n) case n: return launch_fit<n>(X, w, N, nq, scaling, eps, covs, inv_covs, dets, chol, log_norm, ws, ws_bytes, s);
     ABC_D(1) ABC_D(2) ABC_D(3) ABC_D(4) ABC_D(5) ABC_D(6) ABC_D(7) ABC_D(8)
 #undef ABC_D
   }

@@ -308,9 +308,11 @@ def local_fit(X, w, k, scaling, eps):
     chol = torch.empty_like(covs)
     dets = torch.empty(N, dtype=F64, device=dev)
     lnorm = torch.empty(N, dtype=F64, device=dev)
+    nb = nat.query("abc_local_fit_workspace", N, d)
+    ws = workspace(nb, "local")
     nat.call("abc_local_fit", p(X), p(w), N, d, int(k), float(scaling),
-             float(eps), p(covs), p(inv), p(dets), p(chol), p(lnorm), None, 0,
-             stream_ptr())
+             float(eps), p(covs), p(inv), p(dets), p(chol), p(lnorm), p(ws),
+             ws.numel(), stream_ptr())
     return covs, inv, dets, chol, lnorm
 
 

@@ -191,7 +191,9 @@ def test_local_golden(dev, tag, kw):
     np.testing.assert_allclose(t.determinants, gg["dets"], rtol=1e-8)
     np.testing.assert_allclose(t.inv_covs, gg["inv_covs"], rtol=1e-8, atol=1e-10)
     pdf = t.pdf(pd.DataFrame(gg["x"], columns=cols))
-    np.testing.assert_allclose(pdf, gg["pdf"], rtol=1e-9)
+    # the density's log-sum-exp runs on the f32 exp2 unit (exponents fp64):
+    # ~1e-7 relative; the north star's fp32 bar is 1e-5
+    np.testing.assert_allclose(pdf, gg["pdf"], rtol=1e-6)
 
 
 def test_pnorm_golden(dev):
