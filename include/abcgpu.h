@@ -179,6 +179,15 @@ int abc_accept_compact(const double* d, int64_t B, double eps, int64_t* idx,
 /* Gather rows: out[i, :] = in[idx[i], :] (row width `cols` doubles). */
 int abc_gather_rows(const double* in, const int64_t* idx, int64_t n, int cols,
                     double* out, void* stream);
+/* The same for up to 8 arrays sharing one index list, in one launch:
+ * outs[a][(out_row0[a] + i) * cols[a] + c] = ins[a][idx[i] * cols[a] + c].
+ * ins/outs/cols/out_row0 are HOST arrays of n_arrays entries (the pointers
+ * they hold are device memory); 8-byte elements (int64 columns travel as
+ * their bit patterns). */
+int abc_gather_rows_batch(int n_arrays, const double* const* ins,
+                          const int* cols, double* const* outs,
+                          const int64_t* out_row0, const int64_t* idx,
+                          int64_t n, void* stream);
 
 /* ---- importance weight (smc.py:768-811, single model) --------------------
  * w[i] = exp(prior_logpdf[i] - trans_logpdf[i]) * scale  (t > 0). */

@@ -48,6 +48,7 @@ SIGNATURES = {
     "abc_compact_workspace": (SZ, [I64]),
     "abc_accept_compact": (I32, [P, I64, D, P, P, P, SZ, P]),
     "abc_gather_rows": (I32, [P, P, I64, I32, P, P]),
+    "abc_gather_rows_batch": (I32, [I32, P, P, P, P, P, I64, P]),
     "abc_importance_weights": (I32, [P, P, I64, D, P, P]),
     "abc_sort_pairs_workspace": (SZ, [I64]),
     "abc_sort_pairs_f64": (I32, [P, P, I64, P, P, P, SZ, P]),

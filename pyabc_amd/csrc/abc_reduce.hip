@@ -343,6 +343,29 @@ __global__ void gather_rows_kernel(const double* __restrict__ in,
   out[e] = in[idx[i] * cols + c];
 }
 
+constexpr int GB_MAX = 8;
+struct GatherBatch {
+  const double* in[GB_MAX];
+  double* out[GB_MAX];
+  int cols[GB_MAX];
+  int64_t row0[GB_MAX];  // first output row
+  int n_arrays, total_cols;
+};
+
+// several row gathers with the same index list in one launch: thread ->
+// (row i, column c over the concatenated columns of all arrays)
+__global__ void gather_batch_kernel(GatherBatch g, const int64_t* __restrict__ idx,
+                                    int64_t n) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * g.total_cols) return;
+  const int64_t i = e / g.total_cols;
+  int c = (int)(e % g.total_cols);
+  int a = 0;
+  while (a < g.n_arrays - 1 && c >= g.cols[a]) { c -= g.cols[a]; ++a; }
+  const int64_t src = idx[i];
+  g.out[a][(g.row0[a] + i) * g.cols[a] + c] = g.in[a][src * g.cols[a] + c];
+}
+
 __global__ void importance_weights_kernel(const double* __restrict__ lp,
                                           const double* __restrict__ lt,
                                           int64_t A, double scale,
@@ -469,6 +492,32 @@ extern "C" int abc_gather_rows(const double* in, const int64_t* idx, int64_t n,
   ABC_CHECK_ARG(in && idx && out, "gather: null pointer");
   hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)ceil_div(n * cols, 256)), dim3(256),
                      0, as_stream(stream), in, idx, n, cols, out);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
+extern "C" int abc_gather_rows_batch(int n_arrays, const double* const* ins,
+                                     const int* cols, double* const* outs,
+                                     const int64_t* out_row0, const int64_t* idx,
+                                     int64_t n, void* stream) {
+  ABC_CHECK_ARG(n_arrays >= 1 && n_arrays <= GB_MAX && n >= 0, "gather_batch: bad sizes");
+  if (n == 0) return ABC_OK;
+  ABC_CHECK_ARG(ins && cols && outs && out_row0 && idx, "gather_batch: null pointer");
+  GatherBatch g{};
+  g.n_arrays = n_arrays;
+  g.total_cols = 0;
+  for (int a = 0; a < n_arrays; ++a) {
+    ABC_CHECK_ARG(ins[a] && outs[a] && cols[a] >= 1 && out_row0[a] >= 0,
+                  "gather_batch: array %d", a);
+    g.in[a] = ins[a];
+    g.out[a] = outs[a];
+    g.cols[a] = cols[a];
+    g.row0[a] = out_row0[a];
+    g.total_cols += cols[a];
+  }
+  hipLaunchKernelGGL(gather_batch_kernel,
+                     dim3((unsigned)ceil_div(n * g.total_cols, 256)), dim3(256), 0,
+                     as_stream(stream), g, idx, n);
   ABC_LAUNCHED();
   return ABC_OK;
 }

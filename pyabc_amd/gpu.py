@@ -87,6 +87,19 @@ class HostFuture:
         return {"_v": self.get(), "_h": None, "_ev": None}
 
 
+_flat = {}
+
+
+def flat_prior(d, device):
+    """Device (kind, params) of a flat prior over d parameters (cached):
+    the proposal kernels' "no prior" arguments for a plain Transition.rvs."""
+    key = (int(d), str(device))
+    if key not in _flat:
+        _flat[key] = (as_dev(np.full(d, -1), dtype=torch.int32, device=device),
+                      torch.zeros(4 * d, dtype=F64, device=device))
+    return _flat[key]
+
+
 def as_dev(a, dtype=None, device=None):
     """numpy / list / tensor -> contiguous device tensor."""
     dtype = dtype or F64
@@ -143,7 +156,7 @@ def mvn_pack(X, w, mu, U, shift, prec, with_range=False):
     r = U.shape[1]
     nb = nat.query("abc_mvn_packed_bytes", N, r, prec)
     packed = torch.empty(nb, dtype=torch.uint8, device=X.device)
-    rng = torch.zeros(2, dtype=F64, device=X.device) if with_range else None
+    rng = torch.empty(2, dtype=F64, device=X.device) if with_range else None
     nat.call("abc_mvn_pack_population", p(X), p(w), N, d, p(mu), p(U), r,
              float(shift), prec, p(packed), p(rng), stream_ptr())
     return (packed, rng) if with_range else packed
@@ -247,6 +260,25 @@ def gather_rows(x, idx, n=None):
                       device=x.device)
     nat.call("abc_gather_rows", p(x), p(idx), n, cols, p(out), stream_ptr())
     return out
+
+
+def gather_rows_batch(arrays, idx, n=None):
+    """[a[idx[:n]] for a in arrays] in one launch (8-byte dtypes; 1-D arrays
+    are treated as one column)."""
+    import ctypes as C
+    n = idx.numel() if n is None else int(n)
+    outs = [torch.empty((n,) + tuple(a.shape[1:]), dtype=a.dtype, device=a.device)
+            for a in arrays]
+    if n == 0:
+        return outs
+    k = len(arrays)
+    ins_c = (C.c_void_p * k)(*[p(a) for a in arrays])
+    outs_c = (C.c_void_p * k)(*[p(o) for o in outs])
+    cols_c = (C.c_int * k)(*[1 if a.dim() == 1 else int(a.shape[1]) for a in arrays])
+    row0_c = (C.c_int64 * k)(*([0] * k))
+    nat.call("abc_gather_rows_batch", k, C.addressof(ins_c), C.addressof(cols_c),
+             C.addressof(outs_c), C.addressof(row0_c), p(idx), n, stream_ptr())
+    return outs
 
 
 def importance_weights(prior_lp, trans_lp, scale=1.0):

@@ -191,13 +191,14 @@ class BatchedGPUSampler(Sampler):
             rec_rows = int(rec_all[rank])
             if k_mine:
                 sel = idx[:k_mine]
-                acc_theta.append(gpu.gather_rows(theta, sel))
-                acc_lp.append(gpu.gather_rows(lp, sel))
-                acc_d.append(gpu.gather_rows(dist, sel))
-                acc_x.append(gpu.gather_rows(x, sel))
-                if anc is not None:   # int64 rows moved as 8-byte words
-                    acc_anc.append(gpu.gather_rows(
-                        anc.view(gpu.F64), sel).view(gpu.I64))
+                cols = [theta, lp, dist, x] + ([anc] if anc is not None else [])
+                got = gpu.gather_rows_batch(cols, sel)   # one launch
+                acc_theta.append(got[0])
+                acc_lp.append(got[1])
+                acc_d.append(got[2])
+                acc_x.append(got[3])
+                if anc is not None:
+                    acc_anc.append(got[4])
             if record:
                 rec_x.append(x[:rec_rows])
                 rec_keeps.append(rec_all)

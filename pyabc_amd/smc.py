@@ -88,11 +88,19 @@ class GenerationSpec:
         self.why_not = "; ".join(why)
         self.batched_capable = not why
         if self.batched_capable:
-            dev = gpu.require_device()
-            self.prior_kind = gpu.as_dev(spec[0], dtype=gpu.torch.int32, device=dev)
-            self.prior_params = gpu.as_dev(spec[1], device=dev)
-            self.x0vec = gpu.as_dev(np.array([abc.x_0[k] for k in self.sum_stat_keys],
-                                             dtype=np.float64), device=dev)
+            # prior and x_0 device constants: uploaded once per run, reused
+            # by every generation (they change only if the prior or x_0 do)
+            x0 = np.array([abc.x_0[k] for k in self.sum_stat_keys], dtype=np.float64)
+            key = (np.asarray(spec[0]).tobytes(), np.asarray(spec[1]).tobytes(),
+                   x0.tobytes())
+            cache = abc.__dict__.setdefault("_device_consts", {})
+            if key not in cache:
+                dev = gpu.require_device()
+                cache.clear()
+                cache[key] = (gpu.as_dev(spec[0], dtype=gpu.torch.int32, device=dev),
+                              gpu.as_dev(spec[1], device=dev),
+                              gpu.as_dev(x0, device=dev))
+            self.prior_kind, self.prior_params, self.x0vec = cache[key]
 
     def __call__(self):
         if self._closure is None:
@@ -172,6 +180,7 @@ class ABCSMC:
     def __getstate__(self):
         state = self.__dict__.copy()
         del state['sampler']
+        state.pop("_device_consts", None)   # device tensors stay per process
         return state
 
     # -- history ------------------------------------------------------------

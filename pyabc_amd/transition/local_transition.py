@@ -77,10 +77,7 @@ class LocalTransition(Transition):
         self._dev_covs, self._dev_inv, self._dev_dets = covs, inv, dets
         self._dev_chol, self._dev_lnorm = chol, lnorm
         self._dev_cdf = gpu.inclusive_scan(wd)
-        self._dev_flat_kind = gpu.as_dev(np.full(d, -1), dtype=gpu.torch.int32,
-                                         device=Xd.device)
-        self._dev_flat_params = gpu.torch.zeros(4 * d, dtype=gpu.F64,
-                                                device=Xd.device)
+        self._dev_flat_kind, self._dev_flat_params = gpu.flat_prior(d, Xd.device)
         self._seed = int(np.random.randint(0, 2 ** 62))
         self._counter = 0
         self._host = None

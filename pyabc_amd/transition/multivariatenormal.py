@@ -160,9 +160,7 @@ class MultivariateNormalTransition(Transition):
             self._x3_range = gpu.HostFuture(rng)
         if self._mfma and self._dev_packed is None:
             self._pack_f64()
-        self._dev_flat_kind = gpu.as_dev(np.full(d, -1), dtype=gpu.torch.int32,
-                                         device=dev)
-        self._dev_flat_params = gpu.torch.zeros(4 * d, dtype=gpu.F64, device=dev)
+        self._dev_flat_kind, self._dev_flat_params = gpu.flat_prior(d, dev)
         self._seed = int(np.random.randint(0, 2 ** 62))
         self._counter = 0
 

@@ -105,12 +105,16 @@ def _install_cpu_doubles(monkeypatch_like):
     def gather_rows(x, idx, n=None):
         return x.index_select(0, idx)
 
+    def gather_rows_batch(arrays, idx, n=None):
+        return [a.index_select(0, idx) for a in arrays]
+
     def importance_weights(lp, lt, scale=1.0):
         return torch.exp(lp - lt) * scale
 
     monkeypatch_like(g, "require_device", lambda: torch.device("cpu"))
     monkeypatch_like(g, "accept_compact", accept_compact)
     monkeypatch_like(g, "gather_rows", gather_rows)
+    monkeypatch_like(g, "gather_rows_batch", gather_rows_batch)
     monkeypatch_like(g, "importance_weights", importance_weights)
 
 

@@ -410,3 +410,20 @@ def test_step_golden(dev):
     lt = t.logpdf_device(theta)
     wts = gpu.importance_weights(lp, lt).cpu().numpy()
     np.testing.assert_allclose(wts[acc], gg["weight"][acc], rtol=2e-6)
+
+
+def test_gather_rows_batch(dev):
+    """One-launch gather of several column groups (fp64 matrices, fp64
+    vectors, int64 ancestors) == index_select, for ragged sizes."""
+    from pyabc_amd import gpu
+    g = torch.Generator(device="cpu").manual_seed(3)
+    for B, n in ((1, 1), (1000, 0), (4097, 1234), (100_000, 65_537)):
+        th = torch.randn(B, 10, dtype=torch.float64, generator=g).to(dev)
+        lp = torch.randn(B, dtype=torch.float64, generator=g).to(dev)
+        x = torch.randn(B, 3, dtype=torch.float64, generator=g).to(dev)
+        anc = torch.randint(0, 1 << 40, (B,), generator=g).to(dev)
+        idx = torch.randperm(B, generator=g)[:n].sort().values.to(dev)
+        got = gpu.gather_rows_batch([th, lp, x, anc], idx)
+        for a, b in zip(got, (th, lp, x, anc)):
+            assert a.dtype == b.dtype and a.shape == (n,) + tuple(b.shape[1:])
+            assert torch.equal(a, b.index_select(0, idx))
