@@ -67,6 +67,7 @@ constexpr int MAX_R = 25;       // K0 = r + 7 <= 32
 constexpr int E_MIN = 3, E_MAX = 8;
 constexpr float O_MIN = -64.f;  // offsets below this: density < 2^-60 -> rescue
 constexpr size_t HDR = 256;     // image header bytes
+constexpr int X3_PAD = 8;       // pad tiles after the population fragments
 
 struct Header { double maxsq; int E; int ok; };
 
@@ -338,9 +339,12 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
   }
   const int64_t t_begin = (int64_t)chunk * tiles_per_chunk;
   const int64_t t_end = t_begin + tiles_per_chunk < NT ? t_begin + tiles_per_chunk : NT;
-  const int64_t t_last = t_end - 1;
   const half8* __restrict__ Al = A + lane;
-  auto tile = [&](int64_t t) { return (t < t_end ? t : t_last) * KB; };
+  // prefetches run up to 7 tiles past the chunk end (t_end <= NT); the image
+  // carries X3_PAD = 8 pad tiles, so no clamp is needed (pad data is loaded,
+  // never used).  A chunk starting at or past NT (small N) loads nothing.
+  static_assert(X3_PAD >= 7, "pad must cover the prefetch distance");
+  auto tile = [&](int64_t t) { return t * KB; };
 
   // ---- pass 1: exact s_hi (offset slot still 0) -> column max -> o.
   // Block-0 fragments through a ring of 4 registers (prefetch distance 4).
@@ -391,10 +395,12 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
 #pragma unroll
   for (int c = 0; c < CT; ++c) { l64[c] = 0.0; ls[c] = 0.f; }
   half8 a0[KB], a1[KB];
+  if (t_begin < t_end) {
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    a0[kb] = Al[(tile(t_begin) + kb) * 64];
-    a1[kb] = Al[(tile(t_begin + 1) + kb) * 64];
+    for (int kb = 0; kb < KB; ++kb) {
+      a0[kb] = Al[(tile(t_begin) + kb) * 64];
+      a1[kb] = Al[(tile(t_begin + 1) + kb) * 64];
+    }
   }
   auto chain = [&](const half8 (&a)[KB], int c) {
     f32x4 r = {0.f, 0.f, 0.f, 0.f};
@@ -701,7 +707,7 @@ int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
 // image = header | fragments [NT][KB][64][8] f16 | Y [N x r] f64 | lw [N] f64
 size_t x3_frag_bytes(int64_t N, int r) {
   const int KB = x3_kb0(r) + x3_kb12(r);
-  const int64_t NT = ceil_div(N > 0 ? N : 1, 16);
+  const int64_t NT = ceil_div(N > 0 ? N : 1, 16) + X3_PAD;
   return align_up((size_t)NT * KB * 64 * 8 * sizeof(_Float16), 256);
 }
 double* x3_Y(const void* packed, int64_t N, int r) {
