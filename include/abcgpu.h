@@ -141,8 +141,13 @@ int abc_mvn_logpdf_direct(const double* x, int64_t M, const double* X,
  * (attempts > max_attempts means "gave up").  With X == NULL it samples the
  * prior itself (t = 0, smc.py:631-634).
  * Prior: per dimension kind[k] (ABC_PRIOR_*) and params[4k .. 4k+4). */
-int abc_propose(const double* X, const double* cdf, int64_t N, int d,
-                const double* L, const int32_t* prior_kind,
+/* Guide table for the ancestor draw: guide[k] = first index with
+ * cdf > k * cdf[N-1] / N (k < N; int32 [N]).  Built once per fit; with it the
+ * proposal's inverse-CDF search starts in a bracket of ~3 table bins. */
+int abc_cdf_guide(const double* cdf, int64_t N, int32_t* guide, void* stream);
+/* guide: nullable (binary search over the whole cdf). */
+int abc_propose(const double* X, const double* cdf, const int32_t* guide,
+                int64_t N, int d, const double* L, const int32_t* prior_kind,
                 const double* prior_params, uint64_t seed, uint32_t generation,
                 int64_t idx0, int64_t B, int max_attempts, double* theta,
                 double* prior_logpdf, int64_t* ancestor, int32_t* attempts,
@@ -237,7 +242,8 @@ int abc_local_logpdf(const double* x, int64_t M, const double* X,
                      const double* log_norm, double* out, void* stream);
 /* rvs: ancestor j ~ Cat(w) (cdf), theta = X_j + chol_j n; same Philox keying
  * and prior re-draw loop as abc_propose. */
-int abc_local_propose(const double* X, const double* cdf, int64_t N, int d,
+int abc_local_propose(const double* X, const double* cdf,
+                      const int32_t* guide, int64_t N, int d,
                       const double* chol, const int32_t* prior_kind,
                       const double* prior_params, uint64_t seed,
                       uint32_t generation, int64_t idx0, int64_t B,

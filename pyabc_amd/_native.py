@@ -39,7 +39,8 @@ SIGNATURES = {
                              P, P, P, SZ, P]),
     "abc_mvn_logpdf_direct": (I32, [P, I64, P, P, I64, I32, P, I32, P, I32,
                                     D, D, P, P]),
-    "abc_propose": (I32, [P, P, I64, I32, P, P, P, U64, U32, I64, I64, I32,
+    "abc_cdf_guide": (I32, [P, I64, P, P]),
+    "abc_propose": (I32, [P, P, P, I64, I32, P, P, P, U64, U32, I64, I64, I32,
                           P, P, P, P, P]),
     "abc_prior_logpdf": (I32, [P, I64, I32, P, P, P, P]),
     "abc_simulate_linear_gaussian": (I32, [P, I64, I32, I32, P, P, P, U64,
@@ -61,8 +62,8 @@ SIGNATURES = {
     "abc_local_fit": (I32, [P, P, I64, I32, I64, D, D, P, P, P, P, P, P, SZ,
                             P]),
     "abc_local_logpdf": (I32, [P, I64, P, P, I64, I32, P, P, P, P]),
-    "abc_local_propose": (I32, [P, P, I64, I32, P, P, P, U64, U32, I64, I64,
-                                I32, P, P, P, P, P]),
+    "abc_local_propose": (I32, [P, P, P, I64, I32, P, P, P, U64, U32, I64,
+                                I64, I32, P, P, P, P, P]),
 }
 
 # C error codes (include/abcgpu.h)

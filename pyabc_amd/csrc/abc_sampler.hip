@@ -150,9 +150,40 @@ __device__ __forceinline__ int64_t upper_bound(const double* cdf, int64_t N,
 // per_particle_L, the LocalTransition Cholesky factors).  D > 0 fixes d at
 // compile time so the per-candidate vectors live in registers (D = 0: any
 // d <= 64, arrays in scratch).
+// Ancestor = first index with cdf > target (np.searchsorted side="right",
+// clamped to N - 1).  With a guide table (guide[k] = that index for the
+// target k * total / N, abc_cdf_guide) the search starts in a bracket of
+// ~3 table bins: O(1) expected instead of log2 N dependent loads.
+__device__ __forceinline__ int64_t ancestor_search(const double* __restrict__ cdf,
+                                                   const int32_t* __restrict__ guide,
+                                                   int64_t N, double total,
+                                                   double target) {
+  if (guide == nullptr) return upper_bound(cdf, N, target);
+  const double step = total / (double)N;
+  int64_t k = (int64_t)floor(target / step) - 1;  // t_k < target (one-bin margin)
+  k = k < 0 ? 0 : (k > N - 1 ? N - 1 : k);
+  int64_t lo = guide[k];
+  int64_t hi = k + 3 < N ? (int64_t)guide[k + 3] + 1 : N;  // t_{k+3} > target
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (cdf[mid] > target) hi = mid; else lo = mid + 1;
+  }
+  return lo < N ? lo : N - 1;
+}
+
+__global__ void cdf_guide_kernel(const double* __restrict__ cdf, int64_t N,
+                                 int32_t* __restrict__ guide) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= N) return;
+  const double total = cdf[N - 1];
+  const double t = (double)k * (total / (double)N);
+  guide[k] = (int32_t)upper_bound(cdf, N, t);
+}
+
 template <int D, bool PER_PARTICLE_L>
 __global__ __launch_bounds__(256) void propose_kernel(
-    const double* __restrict__ X, const double* __restrict__ cdf, int64_t N,
+    const double* __restrict__ X, const double* __restrict__ cdf,
+    const int32_t* __restrict__ guide, int64_t N,
     int d_rt, const double* __restrict__ L, const int32_t* __restrict__ kind,
     const double* __restrict__ params, uint64_t seed, uint32_t gen,
     int64_t idx0, int64_t B, int max_attempts, double* __restrict__ theta,
@@ -177,7 +208,7 @@ __global__ __launch_bounds__(256) void propose_kernel(
           th[k] = prior_draw1(kind[k], params + 4 * k, g, s0 + SLOT_PRIOR + 512u * k, gen, seed);
     } else {
       u32x4 r = philox(g, s0 + SLOT_ANCESTOR, gen, seed);
-      j = upper_bound(cdf, N, uniform53(r.x, r.y) * total);
+      j = ancestor_search(cdf, guide, N, total, uniform53(r.x, r.y) * total);
       double n[(DM + 3) / 4 * 4];
 #pragma unroll
       for (int q = 0; q < DM; q += 4) {
@@ -216,15 +247,15 @@ __global__ __launch_bounds__(256) void propose_kernel(
 
 template <bool PPL>
 void launch_propose(int d, dim3 grid, hipStream_t s, const double* X,
-                    const double* cdf, int64_t N, const double* L,
+                    const double* cdf, const int32_t* guide, int64_t N, const double* L,
                     const int32_t* kind, const double* params, uint64_t seed,
                     uint32_t gen, int64_t idx0, int64_t B, int max_attempts,
                     double* theta, double* lp, int64_t* anc, int32_t* att) {
 #define ABC_PROPOSE_CASE(DD)                                                     \
   case DD:                                                                       \
     hipLaunchKernelGGL((propose_kernel<DD, PPL>), grid, dim3(256), 0, s, X, cdf, \
-                       N, d, L, kind, params, seed, gen, idx0, B, max_attempts,  \
-                       theta, lp, anc, att);                                     \
+                       guide, N, d, L, kind, params, seed, gen, idx0, B,         \
+                       max_attempts, theta, lp, anc, att);                       \
     break;
   switch (d) {
     ABC_PROPOSE_CASE(1) ABC_PROPOSE_CASE(2) ABC_PROPOSE_CASE(3)
@@ -373,7 +404,18 @@ __global__ __launch_bounds__(CT_T) void accept_write_kernel(
 
 using namespace abc;
 
-extern "C" int abc_propose(const double* X, const double* cdf, int64_t N,
+extern "C" int abc_cdf_guide(const double* cdf, int64_t N, int32_t* guide,
+                             void* stream) {
+  ABC_CHECK_ARG(N >= 1 && N < (1ll << 31), "cdf_guide: bad N");
+  ABC_CHECK_ARG(cdf && guide, "cdf_guide: null pointer");
+  hipLaunchKernelGGL(cdf_guide_kernel, dim3((unsigned)ceil_div(N, 256)), dim3(256), 0,
+                     as_stream(stream), cdf, N, guide);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
+extern "C" int abc_propose(const double* X, const double* cdf,
+                           const int32_t* guide, int64_t N,
                            int d, const double* L, const int32_t* prior_kind,
                            const double* prior_params, uint64_t seed,
                            uint32_t generation, int64_t idx0, int64_t B,
@@ -386,13 +428,14 @@ extern "C" int abc_propose(const double* X, const double* cdf, int64_t N,
   ABC_CHECK_ARG(theta && prior_logpdf && prior_kind && prior_params, "propose: null pointer");
   ABC_CHECK_ARG(X == nullptr || (cdf && L && N >= 1), "propose: population needs cdf, L, N");
   launch_propose<false>(d, dim3((unsigned)ceil_div(B, 256)), as_stream(stream), X, cdf,
-                        N, L, prior_kind, prior_params, seed, generation, idx0, B,
+                        guide, N, L, prior_kind, prior_params, seed, generation, idx0, B,
                         max_attempts, theta, prior_logpdf, ancestor, attempts);
   ABC_LAUNCHED();
   return ABC_OK;
 }
 
-extern "C" int abc_local_propose(const double* X, const double* cdf, int64_t N,
+extern "C" int abc_local_propose(const double* X, const double* cdf,
+                                 const int32_t* guide, int64_t N,
                                  int d, const double* chol,
                                  const int32_t* prior_kind,
                                  const double* prior_params, uint64_t seed,
@@ -406,7 +449,7 @@ extern "C" int abc_local_propose(const double* X, const double* cdf, int64_t N,
   ABC_CHECK_ARG(X && cdf && chol && N >= 1 && theta && prior_logpdf && prior_kind &&
                 prior_params, "local_propose: null pointer");
   launch_propose<true>(d, dim3((unsigned)ceil_div(B, 256)), as_stream(stream), X, cdf,
-                       N, chol, prior_kind, prior_params, seed, generation, idx0, B,
+                       guide, N, chol, prior_kind, prior_params, seed, generation, idx0, B,
                        max_attempts, theta, prior_logpdf, ancestor, attempts);
   ABC_LAUNCHED();
   return ABC_OK;

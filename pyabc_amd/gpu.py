@@ -199,8 +199,16 @@ def mvn_logpdf_direct(x, X, w, U, V, support_tol, log_const, out=None):
 
 # ---- proposal / prior / simulator / distance / acceptance ----------------
 
+def cdf_guide(cdf):
+    """int32 guide table of an inclusive weight scan (abc_cdf_guide)."""
+    N = cdf.numel()
+    guide = torch.empty(N, dtype=torch.int32, device=cdf.device)
+    nat.call("abc_cdf_guide", p(cdf), N, p(guide), stream_ptr())
+    return guide
+
+
 def propose(X, cdf, L, prior_kind, prior_params, seed, generation, idx0, B,
-            max_attempts, d, per_particle_L=False):
+            max_attempts, d, per_particle_L=False, guide=None):
     dev = prior_params.device
     theta = torch.empty((B, d), dtype=F64, device=dev)
     lp = torch.empty(B, dtype=F64, device=dev)
@@ -208,7 +216,7 @@ def propose(X, cdf, L, prior_kind, prior_params, seed, generation, idx0, B,
     att = torch.empty(B, dtype=torch.int32, device=dev)
     N = 0 if X is None else X.shape[0]
     fn = "abc_local_propose" if per_particle_L else "abc_propose"
-    nat.call(fn, p(X), p(cdf), N, d, p(L), p(prior_kind), p(prior_params),
+    nat.call(fn, p(X), p(cdf), p(guide), N, d, p(L), p(prior_kind), p(prior_params),
              int(seed) & (2 ** 64 - 1), int(generation) & 0xFFFFFFFF, int(idx0),
              int(B), int(max_attempts), p(theta), p(lp), p(anc), p(att),
              stream_ptr())

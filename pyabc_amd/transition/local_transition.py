@@ -77,6 +77,7 @@ class LocalTransition(Transition):
         self._dev_covs, self._dev_inv, self._dev_dets = covs, inv, dets
         self._dev_chol, self._dev_lnorm = chol, lnorm
         self._dev_cdf = gpu.inclusive_scan(wd)
+        self._dev_guide = gpu.cdf_guide(self._dev_cdf)
         self._dev_flat_kind, self._dev_flat_params = gpu.flat_prior(d, Xd.device)
         self._seed = int(np.random.randint(0, 2 ** 62))
         self._counter = 0
@@ -130,7 +131,8 @@ class LocalTransition(Transition):
         return gpu.propose(self._dev_X, self._dev_cdf, self._dev_chol,
                            prior_kind, prior_params,
                            self._seed if seed is None else seed, generation,
-                           idx0, B, max_attempts, d, per_particle_L=True)
+                           idx0, B, max_attempts, d, per_particle_L=True,
+                           guide=self._dev_guide)
 
     def rvs_single(self):
         theta = self.propose_device(1)[0].cpu().numpy()[0]

@@ -138,6 +138,7 @@ class MultivariateNormalTransition(Transition):
         self._dev_V = views[2].view(d, d - psd["rank"]) if psd["rank"] < d else None
         self._dev_L = views[3].view(d, d)
         self._dev_cdf = gpu.inclusive_scan(wd)
+        self._dev_guide = gpu.cdf_guide(self._dev_cdf)
         self._rank = psd["rank"]
         self._support_tol = psd["tol"]
         self._log_norm = -0.5 * (psd["rank"] * gpu.LOG_2PI + psd["log_pdet"])
@@ -218,7 +219,8 @@ class MultivariateNormalTransition(Transition):
             self._counter += B
         return gpu.propose(self._dev_X, self._dev_cdf, self._dev_L, prior_kind,
                            prior_params, self._seed if seed is None else seed,
-                           generation, idx0, B, max_attempts, d)
+                           generation, idx0, B, max_attempts, d,
+                           guide=self._dev_guide)
 
     def rvs(self, size: int = None) -> Union[pd.Series, pd.DataFrame]:
         n = 1 if size is None else size

@@ -324,11 +324,18 @@ def test_propose_replay(dev):
     kinds = ["uniform", "norm", "expon"]
     params = np.array([[-1.0, 2.0, 0, 0], [0.0, 1.0, 0, 0], [-0.5, 1.0, 0, 0]])
     ref = osamp.propose_mvn(X, w, L, 123, 4, 1000, 5000, kinds, params)
+    cdf = gpu.inclusive_scan(T(w))
     th, lp, anc, att = gpu.propose(
-        T(X), gpu.inclusive_scan(T(w)), T(L),
+        T(X), cdf, T(L),
         T([osamp.KIND[k] for k in kinds], dtype=torch.int32), T(params.ravel()),
         123, 4, 1000, 5000, 1000, d)
     np.testing.assert_array_equal(anc.cpu().numpy(), ref[2])
+    # the guide-table search returns the same ancestors (bit-exact draws)
+    th_g, lp_g, anc_g, att_g = gpu.propose(
+        T(X), cdf, T(L),
+        T([osamp.KIND[k] for k in kinds], dtype=torch.int32), T(params.ravel()),
+        123, 4, 1000, 5000, 1000, d, guide=gpu.cdf_guide(cdf))
+    assert torch.equal(anc_g, anc) and torch.equal(th_g, th)
     np.testing.assert_array_equal(att.cpu().numpy(), ref[3])
     np.testing.assert_allclose(th.cpu().numpy(), ref[0], rtol=1e-12, atol=1e-13)
     np.testing.assert_allclose(lp.cpu().numpy(), ref[1], rtol=1e-12)
@@ -427,3 +434,33 @@ def test_gather_rows_batch(dev):
         for a, b in zip(got, (th, lp, x, anc)):
             assert a.dtype == b.dtype and a.shape == (n,) + tuple(b.shape[1:])
             assert torch.equal(a, b.index_select(0, idx))
+
+
+def test_cdf_guide_search_edges(dev):
+    """Guide-table ancestor search == searchsorted(side='right') clamped to
+    N-1, for weights with zeros, one dominant weight, tiny weights, N = 1."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(12)
+    cases = {"n1": np.array([1.0]),
+             "zeros": np.where(rng.uniform(size=5000) < 0.5, 0.0, rng.uniform(size=5000)),
+             "dominant": np.r_[np.full(3000, 1e-12), [1.0], np.full(3000, 1e-12)],
+             "tiny": np.exp(-40 * rng.uniform(size=20000)),
+             "uniform": np.ones(70001)}
+    d = 2
+    for name, w in cases.items():
+        N = len(w)
+        X = rng.standard_normal((N, d))
+        cdf = gpu.inclusive_scan(T(w))
+        guide = gpu.cdf_guide(cdf)
+        kinds = T([-1, -1], dtype=torch.int32)
+        params = T(np.zeros(8))
+        L = T(np.eye(d) * 0.1)
+        _, _, a0, _ = gpu.propose(T(X), cdf, L, kinds, params, 7, 1, 0, 20000, 1, d)
+        _, _, a1, _ = gpu.propose(T(X), cdf, L, kinds, params, 7, 1, 0, 20000, 1, d,
+                                  guide=guide)
+        assert torch.equal(a0, a1), name
+        g = guide.cpu().numpy()
+        c = cdf.cpu().numpy()
+        t = np.arange(N) * (c[-1] / N)
+        np.testing.assert_array_equal(
+            g, np.minimum(np.searchsorted(c, t, side="right"), N - 1), err_msg=name)
