@@ -250,6 +250,16 @@ int abc_local_propose(const double* X, const double* cdf,
                       int max_attempts, double* theta, double* prior_logpdf,
                       int64_t* ancestor, int32_t* attempts, void* stream);
 
+/* ---- bootstrapped KDE variation (pyabc/cv/bootstrap.py:86-108) ----------
+ * logdens [B x N] row-major: log densities of B bootstrapped transitions at
+ * N test points.  variation[i] = std_b(exp) / mean_b(exp) (scipy.stats
+ * .variation, ddof 0); *cv = sum_i variation[i] * scale * w[i] (device
+ * double).  Replaces the numpy/scipy tail of calc_cv. */
+size_t abc_bootstrap_cv_workspace(int64_t N);
+int abc_bootstrap_cv(const double* logdens, int64_t B, int64_t N,
+                     const double* w, double scale, double* variation,
+                     double* cv, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,5 +22,7 @@ from .distance import (pnorm, standard_deviation, median_absolute_deviation,
                        adaptive_weights)
 from .epsilon import weighted_quantile, quantile_epsilon
 from .philox import philox4x32_10, uniform01, normal_pairs
+from .cv import (bootstrap_variation, mvn_bootstrap_densities,
+                 mvn_calc_cv)
 from .generation import (effective_sample_size, normalize_weights,
                          importance_weights)

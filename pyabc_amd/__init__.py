@@ -25,7 +25,8 @@ from .model import (Model, SimpleModel, ModelResult, IntegratedModel,
 from .transition import (Transition, MultivariateNormalTransition,
                          LocalTransition, NotEnoughParticles)
 from .population import Particle, Population
-from .populationstrategy import ConstantPopulationSize, PopulationStrategy
+from .populationstrategy import (ConstantPopulationSize, PopulationStrategy,
+                                 AdaptivePopulationSize, ListPopulationSize)
 from .weighted_statistics import (weighted_quantile, weighted_median,
                                   weighted_mean, weighted_std,
                                   effective_sample_size)

@@ -64,6 +64,8 @@ SIGNATURES = {
     "abc_local_logpdf": (I32, [P, I64, P, P, I64, I32, P, P, P, P]),
     "abc_local_propose": (I32, [P, P, P, I64, I32, P, P, P, U64, U32, I64,
                                 I64, I32, P, P, P, P, P]),
+    "abc_bootstrap_cv_workspace": (SZ, [I64]),
+    "abc_bootstrap_cv": (I32, [P, I64, I64, P, D, P, P, P, SZ, P]),
 }
 
 # C error codes (include/abcgpu.h)

@@ -338,6 +338,22 @@ def column_mad(X):
     return out
 
 
+def bootstrap_cv(logdens, w, scale=1.0):
+    """logdens [B, N] (bootstrapped log densities at N test points), w [N]
+    -> (variation [N], cv [1]) on the device (abc_bootstrap_cv)."""
+    B, N = logdens.shape
+    if w.numel() != N or not logdens.is_contiguous():
+        raise ValueError(f"bootstrap_cv: {w.numel()} weights for {N} test "
+                         "points (or non-contiguous densities)")
+    var = torch.empty(N, dtype=F64, device=logdens.device)
+    cv = torch.empty(1, dtype=F64, device=logdens.device)
+    nb = nat.query("abc_bootstrap_cv_workspace", N)
+    ws = workspace(nb, "cv")
+    nat.call("abc_bootstrap_cv", p(logdens), B, N, p(w), float(scale), p(var),
+             p(cv), p(ws), ws.numel(), stream_ptr())
+    return var, cv
+
+
 # ---- LocalTransition -------------------------------------------------------
 
 def local_fit(X, w, k, scaling, eps):

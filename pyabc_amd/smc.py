@@ -553,7 +553,9 @@ class ABCSMC:
             return
         w = np.array(list(self.history.model_probabilities_dict(
             self.history.max_t).values()))
-        self.population_size.update(self.transitions, w, t)
+        # smc.py:1042-1063: the strategy works on copies (device tensors are
+        # shared by Transition.__deepcopy__, not duplicated)
+        self.population_size.update(copy.deepcopy(self.transitions), w, t)
 
     def _fit_transitions(self, t):
         """smc.py:1065-1079; device-resident populations are fitted in

@@ -45,6 +45,37 @@ class Transition(BaseEstimator, metaclass=TransitionMeta):
     def no_meaningful_particles(self) -> bool:
         return len(self.X) == 0 or self.no_parameters
 
+    def mean_cv(self, n_samples=None) -> float:
+        """transition/base.py:121-169: bootstrapped mean coefficient of
+        variation of the KDE at its own particles (device bootstraps for the
+        GPU transitions, pyabc_amd/cv/bootstrap.py)."""
+        import numpy as np
+        from ..cv.bootstrap import calc_cv
+        if self.no_meaningful_particles():
+            raise NotEnoughParticles(n_samples)
+        if n_samples is None:
+            n_samples = len(self.X)
+        self.test_points_ = self.X
+        self.test_weights_ = self.w
+        # base.py:161-163 passes the weight array itself as ``test_w`` (not
+        # a one-element list), so calc_cv's zip weights model 0's variations
+        # by the scalar w[0]; kept as the reference computes it
+        cv, variation_at_test = calc_cv(n_samples, np.array([1]),
+                                        self.NR_BOOTSTRAP, self.w, [self],
+                                        [self.X])
+        self.variation_at_test_points_ = variation_at_test[0]
+        return cv
+
+    def required_nr_samples(self, coefficient_of_variation: float) -> int:
+        """transition/base.py:171-178."""
+        from .predict_population_size import predict_population_size
+        if self.no_meaningful_particles():
+            raise NotEnoughParticles
+        res = predict_population_size(len(self.X), coefficient_of_variation,
+                                      self.mean_cv)
+        self.cv_estimate_ = res
+        return res.n_estimated
+
     # device tensors are immutable after fit(): share them on deepcopy
     # (ABCSMC deep-copies transitions every generation, smc.py:979).
     _SHARED = ()

@@ -278,7 +278,59 @@ def gen_e2e10(seeds=(0, 1, 2, 3), pop=1000, gens=5):
         json.dump(out, f, indent=1)
 
 
+def gen_cv(seeds=tuple(range(24))):
+    """Bootstrapped KDE CV (pyabc/cv/bootstrap.py:44-110) and the population
+    size predicted from it (transition/predict_population_size.py).
+    Deterministic part: fixed bootstrap samples (drawn once with the
+    reference's own rvs) -> fit + pdf + scipy.stats.variation + weighted
+    sum.  Statistical part: the reference's calc_cv / required_nr_samples
+    over seeds (their RNG is numpy's, so the GPU matches in distribution)."""
+    from pyabc.cv.bootstrap import calc_cv
+    import scipy.stats as st
+    rng = np.random.default_rng(777)
+    N, d = 400, 2
+    X = rng.normal(size=(N, d)) @ np.array([[1.0, 0.4], [0.0, 0.7]])
+    w = np.exp(0.4 * rng.standard_normal(N))
+    w /= w.sum()
+    cols = names(d)
+    Xdf = pd.DataFrame(X, columns=cols)
+    t = MultivariateNormalTransition()
+    t.fit(Xdf, w.copy())
+    np.random.seed(4242)
+    B, n = 6, 300
+    samples = np.stack([t.rvs(size=n).values for _ in range(B)])
+    dens = []
+    for b in range(B):
+        tt = MultivariateNormalTransition()
+        tt.fit(pd.DataFrame(samples[b], columns=cols), np.ones(n) / n)
+        dens.append(tt.pdf(Xdf))
+    dens = np.array(dens)
+    variation = st.variation(dens, axis=0)
+    cv_fixed = float((variation * w).sum())
+    stat_n = [100, 400]
+    cvs = np.zeros((len(stat_n), len(seeds)))
+    for i, nn in enumerate(stat_n):
+        for j, s in enumerate(seeds):
+            np.random.seed(s)
+            cvs[i, j] = calc_cv(nn, np.array([1.0]), 10, [t.w], [t],
+                                [t.X])[0]
+    n_est = np.zeros(8)
+    for j in range(len(n_est)):
+        np.random.seed(100 + j)
+        tr = MultivariateNormalTransition()
+        tr.fit(Xdf, w.copy())
+        n_est[j] = tr.required_nr_samples(0.1)
+    np.savez_compressed(os.path.join(HERE, "cv.npz"), X=X, w=w,
+                        samples=samples, dens=dens, variation=variation,
+                        cv_fixed=cv_fixed, stat_n=np.array(stat_n), cvs=cvs,
+                        n_est=n_est, n_est_target=0.1)
+    print("cv", cv_fixed, cvs.mean(axis=1), cvs.std(axis=1), n_est)
+
+
 if __name__ == "__main__":
+    if "--cv" in sys.argv:
+        gen_cv()
+        sys.exit(0)
     if "--e2e10" in sys.argv:
         gen_e2e10()
         sys.exit(0)

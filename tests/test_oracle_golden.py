@@ -135,3 +135,28 @@ def test_philox_known_answer():
     r = oracle.philox4x32_10(np.zeros(1, np.uint64), 0, 0, 0)[0]
     assert [int(v) for v in r] == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c,
                                    0x9b00dbd8]
+
+
+# ---- bootstrapped KDE CV (cv/bootstrap.py, golden from the reference) -----
+
+def test_cv_fixed_samples_golden():
+    g = load("cv.npz")
+    dens = oracle.mvn_bootstrap_densities(g["samples"], g["X"])
+    np.testing.assert_allclose(dens, g["dens"], rtol=1e-11)
+    var, cv = oracle.bootstrap_variation(dens, g["w"])
+    np.testing.assert_allclose(var, g["variation"], rtol=1e-9)
+    assert cv == pytest.approx(float(g["cv_fixed"]), rel=1e-10)
+
+
+def test_cv_statistics_match_reference():
+    # the reference's calc_cv over 24 seeds at n = 100, 400 (numpy RNG);
+    # the restatement with an independent RNG must agree in distribution
+    g = load("cv.npz")
+    rng = np.random.default_rng(5)
+    for i, n in enumerate(g["stat_n"]):
+        ref = g["cvs"][i]
+        ours = np.array([oracle.mvn_calc_cv(int(n), g["X"], g["w"], 10, rng)
+                         for _ in range(12)])
+        se = np.hypot(ref.std() / np.sqrt(len(ref)),
+                      ours.std() / np.sqrt(len(ours)))
+        assert abs(ours.mean() - ref.mean()) < 4 * se, (n, ours.mean(), ref.mean())

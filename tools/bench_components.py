@@ -15,6 +15,7 @@ peak.  Inputs are synthetic, generated on the device or from seeded numpy.
   c5        LocalTransition d = 5, N = 1e5: k-NN covariance fit (k = 50 and
             the default k = N/4 = 25000), density of 1e5 candidates
   sampler   propose + simulate + pnorm + accept at the c3 batch (4.6e6)
+  cv        AdaptivePopulationSize.update on the c2 population (wall time)
 """
 import argparse
 import json
@@ -162,9 +163,45 @@ def sampler(reps):
     emit("accept + compaction", "c3 batch", ms, bytes_=B * 8 * 2)
 
 
+def cv(reps):
+    """AdaptivePopulationSize.update at c2 size (N = 1e5, d = 10): the
+    bootstrapped KDE CV on range(N/3, 2N, N/10) x 10 bootstraps, each an
+    rvs + fit + N x n transition-density launch."""
+    import time
+    import pandas as pd
+    import torch
+    import pyabc_amd as pa
+    from pyabc_amd import gpu
+    N, d = 100_000, 10
+    rng = np.random.default_rng(8)
+    X = rng.normal(0.8, 0.45, size=(N, d))
+    w = np.exp(0.3 * rng.standard_normal(N))
+    w /= w.sum()
+    tr = pa.MultivariateNormalTransition()
+    tr.fit(pd.DataFrame(X, columns=[f"p{k}" for k in range(d)]), w)
+    ns = list(range(N // 3, 2 * N, N // 10))
+    pairs = 10 * N * sum(ns)
+    for r in range(max(1, reps // 2) + 1):
+        ps = pa.AdaptivePopulationSize(N, mean_cv=0.02, n_bootstrap=10,
+                                       max_population_size=10 ** 6)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ps.update([tr], np.array([1.0]), t=1)
+        torch.cuda.synchronize()
+        sec = time.perf_counter() - t0
+    # reference: 7.8e6 transition-density pair-evals/s per core (BASELINE.md,
+    # multivariatenormal.py:99-113 at N = 1e6)
+    emit("AdaptivePopulationSize.update (bootstrapped KDE CV)",
+         "c2 population: N=1e5, d=10, 17 sizes x 10 bootstraps",
+         sec * 1e3, extra=dict(pair_evals=pairs,
+                               pair_evals_per_s=round(pairs / sec, 1),
+                               new_size=ps.nr_particles,
+                               reference_core_s_extrapolated=round(pairs / 7.8e6)))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="c4,quantile,c5,sampler")
+    ap.add_argument("--only", default="c4,quantile,c5,sampler,cv")
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
     for name in a.only.split(","):
