@@ -195,9 +195,12 @@ int abc_gather_rows_batch(int n_arrays, const double* const* ins,
                           int64_t n, void* stream);
 
 /* ---- importance weight (smc.py:768-811, single model) --------------------
- * w[i] = exp(prior_logpdf[i] - trans_logpdf[i]) * scale  (t > 0). */
+ * w[i] = exp(prior_logpdf[i] - trans_logpdf[i]) * scale * acc_weights[i]
+ * (t > 0; acc_weights = the StochasticAcceptor's acceptance weights, NULL
+ * for the uniform acceptor). */
 int abc_importance_weights(const double* prior_logpdf,
-                           const double* trans_logpdf, int64_t A, double scale,
+                           const double* trans_logpdf,
+                           const double* acc_weights, int64_t A, double scale,
                            double* w, void* stream);
 
 /* ---- QuantileEpsilon (epsilon.py:202-228 -> weighted_statistics.py:27-43)
@@ -259,6 +262,44 @@ size_t abc_bootstrap_cv_workspace(int64_t N);
 int abc_bootstrap_cv(const double* logdens, int64_t B, int64_t N,
                      const double* w, double scale, double* variation,
                      double* cv, void* ws, size_t ws_bytes, void* stream);
+
+/* ---- Stochastic acceptance (acceptor/acceptor.py:309-476,
+ * distance/kernel.py:18-592, epsilon/temperature.py:276-742) ---------------
+ * abc_kernel_logpdf: log pdf(x_0 | x) of a StochasticKernel per row of the
+ *   sum-stat matrix x [B x S]; cols[K] = column of each kernel element (the
+ *   kernel's sorted key order), x0k[K] the observed values.  kind:
+ *   0 IndependentNormalKernel (par = var[K], c = sum log(2 pi var)),
+ *   1 IndependentLaplaceKernel (par = scale[K], c = sum log(2 scale)),
+ *   2 NormalKernel (U [K x r] with U U^T = pinv(cov), c = r log 2pi + log pdet),
+ *   3 PoissonKernel, 4 BinomialKernel (par[0] = p), 5 NegativeBinomialKernel
+ *   (par[0] = p).  ret_lin: write exp(log pdf) (SCALE_LIN).
+ *   Replaces StochasticKernel.__call__ (kernel.py:207-226, 285-303, 361-378,
+ *   426-445, 478-495, 533-552).
+ * abc_stochastic_accept: StochasticAcceptor.__call__ (acceptor.py:434-476)
+ *   for B candidates with global indices idx0.. : key[b] = u - acc (accepted
+ *   iff key <= 0, feed to abc_accept_compact with eps 0), accw[b] = the
+ *   acceptance weight.  u comes from the counter-based stream (seed,
+ *   generation, index).
+ * abc_temper_sums: one objective evaluation of AcceptanceRateScheme (mode 0,
+ *   temperature.py:322-352) or EssScheme (mode 1, temperature.py:710-742) at
+ *   beta, over R records with densities dens and log importance weights
+ *   lr - lr_sub (log t_pd - log t_pd_prev; lr_sub may be NULL) shifted by
+ *   `shift`; for mode 1, lr holds the linear population weights; mode 2
+ *   writes max(lr - lr_sub); mode 3 = mode 0 with linear record weights in
+ *   lr.  out[2] device doubles. */
+int abc_kernel_logpdf(const double* x, int64_t B, int S, const int32_t* cols,
+                      int K, const double* x0k, int kind, const double* par,
+                      const double* U, int r, double c, int ret_lin,
+                      double* out, void* stream);
+int abc_stochastic_accept(const double* dens, int64_t B, double pdf_norm,
+                          double temperature, int scale_log, int apply_iw,
+                          uint64_t seed, uint32_t generation, int64_t idx0,
+                          double* key, double* accw, void* stream);
+size_t abc_temper_workspace(void);
+int abc_temper_sums(const double* dens, const double* lr,
+                    const double* lr_sub, int64_t R, double pdf_norm, int scale_log, int mode, double beta,
+                    double shift, double* out, void* ws, size_t ws_bytes,
+                    void* stream);
 
 #ifdef __cplusplus
 }

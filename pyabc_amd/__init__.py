@@ -13,13 +13,24 @@ from .random_variables import (Distribution, ModelPerturbationKernel, RV,
                                RVBase, RVDecorator, LowerBoundDecorator)
 from .distance import (Distance, NoDistance, IdentityFakeDistance,
                        AcceptAllDistance, SimpleFunctionDistance,
-                       PNormDistance, AdaptivePNormDistance, to_distance)
+                       PNormDistance, AdaptivePNormDistance, to_distance,
+                       StochasticKernel, SimpleFunctionKernel, NormalKernel,
+                       IndependentNormalKernel, IndependentLaplaceKernel,
+                       BinomialKernel, PoissonKernel, NegativeBinomialKernel)
 from .epsilon import (Epsilon, NoEpsilon, ConstantEpsilon, QuantileEpsilon,
-                      MedianEpsilon, ListEpsilon)
+                      MedianEpsilon, ListEpsilon, TemperatureBase,
+                      ListTemperature, Temperature, TemperatureScheme,
+                      AcceptanceRateScheme, ExpDecayFixedIterScheme,
+                      ExpDecayFixedRatioScheme,
+                      PolynomialDecayFixedIterScheme, DalyScheme,
+                      FrielPettittScheme, EssScheme)
 from .sampler import (Sampler, Sample, SingleCoreSampler, BatchedGPUSampler)
 from .smc import ABCSMC, GenerationSpec
 from .storage import History, create_sqlite_db_id
-from .acceptor import (Acceptor, SimpleFunctionAcceptor, UniformAcceptor)
+from .acceptor import (Acceptor, SimpleFunctionAcceptor, UniformAcceptor,
+                       StochasticAcceptor, pdf_norm_from_kernel,
+                       pdf_norm_max_found, ScaledPDFNorm)
+from . import distance, epsilon, acceptor, storage
 from .model import (Model, SimpleModel, ModelResult, IntegratedModel,
                     VectorizedModel, LinearGaussianModel)
 from .transition import (Transition, MultivariateNormalTransition,

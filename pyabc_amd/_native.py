@@ -50,7 +50,7 @@ SIGNATURES = {
     "abc_accept_compact": (I32, [P, I64, D, P, P, P, SZ, P]),
     "abc_gather_rows": (I32, [P, P, I64, I32, P, P]),
     "abc_gather_rows_batch": (I32, [I32, P, P, P, P, P, I64, P]),
-    "abc_importance_weights": (I32, [P, P, I64, D, P, P]),
+    "abc_importance_weights": (I32, [P, P, P, I64, D, P, P]),
     "abc_sort_pairs_workspace": (SZ, [I64]),
     "abc_sort_pairs_f64": (I32, [P, P, I64, P, P, P, SZ, P]),
     "abc_weighted_quantile_workspace": (SZ, [I64]),
@@ -66,6 +66,12 @@ SIGNATURES = {
                                 I64, I32, P, P, P, P, P]),
     "abc_bootstrap_cv_workspace": (SZ, [I64]),
     "abc_bootstrap_cv": (I32, [P, I64, I64, P, D, P, P, P, SZ, P]),
+    "abc_kernel_logpdf": (I32, [P, I64, I32, P, I32, P, I32, P, P, I32, D,
+                                I32, P, P]),
+    "abc_stochastic_accept": (I32, [P, I64, D, D, I32, I32, U64, U32, I64,
+                                    P, P, P]),
+    "abc_temper_workspace": (SZ, []),
+    "abc_temper_sums": (I32, [P, P, P, I64, D, I32, I32, D, D, P, P, SZ, P]),
 }
 
 # C error codes (include/abcgpu.h)

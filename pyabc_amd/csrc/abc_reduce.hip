@@ -368,10 +368,15 @@ __global__ void gather_batch_kernel(GatherBatch g, const int64_t* __restrict__ i
 
 __global__ void importance_weights_kernel(const double* __restrict__ lp,
                                           const double* __restrict__ lt,
+                                          const double* __restrict__ accw,
                                           int64_t A, double scale,
                                           double* __restrict__ w) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < A) w[i] = exp(lp[i] - lt[i]) * scale;
+  if (i < A) {
+    // prior_pd * acceptance_weight * fraction / transition_pd (smc.py:803-809)
+    double v = exp(lp[i] - lt[i]) * scale;
+    w[i] = accw ? v * accw[i] : v;
+  }
 }
 
 
@@ -523,13 +528,15 @@ extern "C" int abc_gather_rows_batch(int n_arrays, const double* const* ins,
 }
 
 extern "C" int abc_importance_weights(const double* prior_logpdf,
-                                      const double* trans_logpdf, int64_t A,
+                                      const double* trans_logpdf,
+                                      const double* acc_weights, int64_t A,
                                       double scale, double* w, void* stream) {
   ABC_CHECK_ARG(A >= 0, "weights: A < 0");
   if (A == 0) return ABC_OK;
   ABC_CHECK_ARG(prior_logpdf && trans_logpdf && w, "weights: null pointer");
   hipLaunchKernelGGL(importance_weights_kernel, dim3((unsigned)ceil_div(A, 256)), dim3(256),
-                     0, as_stream(stream), prior_logpdf, trans_logpdf, A, scale, w);
+                     0, as_stream(stream), prior_logpdf, trans_logpdf, acc_weights, A,
+                     scale, w);
   ABC_LAUNCHED();
   return ABC_OK;
 }

@@ -9,3 +9,8 @@ from .scale import (median_absolute_deviation, mean_absolute_deviation,
                     combined_median_absolute_deviation,
                     combined_mean_absolute_deviation,
                     standard_deviation_to_observation, span, mean, median)
+from .kernel import (SCALE_LIN, SCALE_LOG, SCALES, StochasticKernel,
+                     SimpleFunctionKernel, NormalKernel,
+                     IndependentNormalKernel, IndependentLaplaceKernel,
+                     BinomialKernel, PoissonKernel, NegativeBinomialKernel,
+                     binomial_pdf_max)

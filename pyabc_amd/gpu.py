@@ -289,10 +289,10 @@ def gather_rows_batch(arrays, idx, n=None):
     return outs
 
 
-def importance_weights(prior_lp, trans_lp, scale=1.0):
+def importance_weights(prior_lp, trans_lp, scale=1.0, acc_w=None):
     A = prior_lp.numel()
     w = torch.empty(A, dtype=F64, device=prior_lp.device)
-    nat.call("abc_importance_weights", p(prior_lp), p(trans_lp), A,
+    nat.call("abc_importance_weights", p(prior_lp), p(trans_lp), p(acc_w), A,
              float(scale), p(w), stream_ptr())
     return w
 
@@ -384,3 +384,58 @@ def local_logpdf(x, X, w, inv, lnorm, out=None):
 
 
 LOG_2PI = math.log(2 * math.pi)
+
+
+# ---- stochastic acceptance -------------------------------------------------
+
+KERNEL_KINDS = {"independent_normal": 0, "independent_laplace": 1,
+                "normal": 2, "poisson": 3, "binomial": 4,
+                "negative_binomial": 5}
+
+
+def kernel_logpdf(x, cols, x0k, kind, par, c, U=None, ret_lin=False,
+                  out=None):
+    """StochasticKernel values pdf(x_0 | x) for every row of x [B, S]
+    (abc_kernel_logpdf); cols / x0k / par / U are device tensors in the
+    kernel's key order."""
+    B, S = x.shape
+    K = int(cols.numel())
+    r = 0 if U is None else int(U.shape[1])
+    out = torch.empty(B, dtype=F64, device=x.device) if out is None else out
+    nat.call("abc_kernel_logpdf", p(x), B, S, p(cols), K, p(x0k),
+             KERNEL_KINDS[kind], p(par), p(U), r, float(c), int(bool(ret_lin)),
+             p(out), stream_ptr())
+    return out
+
+
+def stochastic_accept(dens, pdf_norm, temperature, scale_log, apply_iw, seed,
+                      generation, idx0):
+    """(key, acceptance weight) per candidate (abc_stochastic_accept):
+    accepted iff key <= 0."""
+    B = dens.numel()
+    key = torch.empty(B, dtype=F64, device=dens.device)
+    accw = torch.empty(B, dtype=F64, device=dens.device)
+    nat.call("abc_stochastic_accept", p(dens), B, float(pdf_norm),
+             float(temperature), int(bool(scale_log)), int(bool(apply_iw)),
+             int(seed) & (2 ** 64 - 1), int(generation) & 0xFFFFFFFF,
+             int(idx0), p(key), p(accw), stream_ptr())
+    return key, accw
+
+
+TEMPER_ACCEPTANCE, TEMPER_ESS, TEMPER_MAX, TEMPER_ACCEPTANCE_LIN = 0, 1, 2, 3
+
+
+def temper_sums(dens, lr, pdf_norm, scale_log, mode, beta=0.0, shift=0.0,
+                lr_sub=None):
+    """Two device reductions over R records (abc_temper_sums); returns the
+    host pair (a, b), see include/abcgpu.h."""
+    R = lr.numel()
+    if lr_sub is not None and lr_sub.numel() != R:
+        raise ValueError("temper_sums: lr / lr_sub sizes differ")
+    out = torch.empty(2, dtype=F64, device=lr.device)
+    ws = workspace(nat.query("abc_temper_workspace"), "temper")
+    nat.call("abc_temper_sums", p(dens), p(lr), p(lr_sub), R, float(pdf_norm),
+             int(bool(scale_log)), int(mode), float(beta), float(shift),
+             p(out), p(ws), ws.numel(), stream_ptr())
+    a, b = out.cpu().numpy()
+    return float(a), float(b)

@@ -39,8 +39,9 @@ class ColumnarSample:
     """Sample of the batched sampler (device columns, see Sample)."""
 
     def __init__(self, columns, recorded, recorded_keys, record_rejected, ok,
-                 accepted_flags=None):
+                 accepted_flags=None, records=None):
         self._cols = columns
+        self._records = records              # (theta, dens, key, anc) or None
         self._recorded = recorded            # [R, S] device or None
         self._recorded_keys = recorded_keys
         self._accepted_flags = accepted_flags
@@ -61,6 +62,21 @@ class ColumnarSample:
         if m is not None and np.isfinite(m) and m < rec.shape[0]:
             rec = rec[: int(m)].contiguous()
         return SumStatMatrix(rec, self._recorded_keys)
+
+    def device_records(self, m=None):
+        """(theta [R, d], density [R], acceptance key [R], ancestor [R] or
+        None) of the first m recorded candidates (all evaluated candidates
+        up to the cutoff, accepted and rejected, in index order); None if
+        the generation did not record them (StochasticAcceptor runs with
+        record_rejected only)."""
+        if self._records is None:
+            return None
+        th, dn, key, anc = self._records
+        if m is not None and np.isfinite(m) and m < th.shape[0]:
+            m = int(m)
+            th, dn, key = th[:m], dn[:m], key[:m]
+            anc = None if anc is None else anc[:m]
+        return th, dn, key, anc
 
     @property
     def all_sum_stats(self):
@@ -134,8 +150,12 @@ class BatchedGPUSampler(Sampler):
         record = self.sample_factory.record_rejected
         d = len(spec.param_names)
 
-        acc_theta, acc_lp, acc_d, acc_x, acc_anc = [], [], [], [], []
+        acc_theta, acc_lp, acc_d, acc_x, acc_anc, acc_w = [], [], [], [], [], []
         rec_x = []
+        stochastic = getattr(spec, "stochastic", None) is not None and not all_accepted
+        # StochasticAcceptor + record_rejected: keep every evaluated
+        # candidate's (theta, density, key, ancestor) for the temperature
+        rec_extra = [] if (stochastic and record) else None
         keeps = []          # per round: accepted rows kept by each rank
         rec_keeps = []      # per round: recorded rows of each rank
         n_acc = 0
@@ -158,7 +178,12 @@ class BatchedGPUSampler(Sampler):
             else:
                 dist = spec.distance.device_call(x, spec.x0vec, spec.t,
                                                  spec.sum_stat_keys)
-                idx, cnt = gpu.accept_compact(dist, spec.eps)
+                if stochastic:
+                    key, accw = gpu.stochastic_accept(dist, *spec.stochastic,
+                                                      seed, gen, lo)
+                    idx, cnt = gpu.accept_compact(key, 0.0)
+                else:
+                    idx, cnt = gpu.accept_compact(dist, spec.eps)
                 if ws == 1:
                     # one read: the count and the index of the n-th accepted
                     # (meaningful only when this round completes the sample)
@@ -191,7 +216,8 @@ class BatchedGPUSampler(Sampler):
             rec_rows = int(rec_all[rank])
             if k_mine:
                 sel = idx[:k_mine]
-                cols = [theta, lp, dist, x] + ([anc] if anc is not None else [])
+                cols = [theta, lp, dist, x] + ([anc] if anc is not None else []) \
+                    + ([accw] if stochastic else [])
                 got = gpu.gather_rows_batch(cols, sel)   # one launch
                 acc_theta.append(got[0])
                 acc_lp.append(got[1])
@@ -199,9 +225,15 @@ class BatchedGPUSampler(Sampler):
                 acc_x.append(got[3])
                 if anc is not None:
                     acc_anc.append(got[4])
+                if stochastic:
+                    acc_w.append(got[-1])
             if record:
                 rec_x.append(x[:rec_rows])
                 rec_keeps.append(rec_all)
+                if rec_extra is not None:
+                    rec_extra.append((theta[:rec_rows], dist[:rec_rows],
+                                      key[:rec_rows],
+                                      None if anc is None else anc[:rec_rows]))
             keeps.append(keep)
             n_acc += total_keep
             n_eval += evaluated
@@ -215,17 +247,32 @@ class BatchedGPUSampler(Sampler):
         if n_acc < n:
             ok = False
         cols = self._assemble(spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
-                              all_accepted, keeps, acc_anc)
+                              all_accepted, keeps, acc_anc, acc_w)
         recorded = None
+        records = None
         if record:
-            recorded = gpu.torch.cat(rec_x, 0) if rec_x else None
-            if ws > 1 and recorded is not None:
-                recorded = dd.allgather_rows(recorded, dev)
-                recorded = self.reorder(recorded, self.global_pieces(rec_keeps))
+            recorded = self._gather_recorded(rec_x, rec_keeps, dev, ws)
+            if rec_extra:
+                parts = list(zip(*rec_extra))
+                records = tuple(
+                    None if any(a is None for a in col)
+                    else self._gather_recorded(list(col), rec_keeps, dev, ws)
+                    for col in parts)
         elif cols is not None:
             recorded = cols.sum_stats
         return ColumnarSample(cols, recorded, spec.sum_stat_keys,
-                              record, ok and n_acc == n)
+                              record, ok and n_acc == n, records=records)
+
+    def _gather_recorded(self, pieces, rec_keeps, dev, ws):
+        """Concatenate this rank's recorded rows and, over several ranks,
+        all-gather them back into global candidate-index order."""
+        if not pieces:
+            return None
+        out = gpu.torch.cat(pieces, 0) if len(pieces) > 1 else pieces[0]
+        if ws > 1:
+            out = dd.allgather_rows(out.contiguous(), dev)
+            out = self.reorder(out, self.global_pieces(rec_keeps))
+        return out.contiguous()
 
     @staticmethod
     def _local_cutoff_pos(idx, k):
@@ -283,7 +330,7 @@ class BatchedGPUSampler(Sampler):
         return gpu.torch.cat([t[a:a + n] for a, n in pieces], 0)
 
     def _assemble(self, spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
-                  all_accepted, keeps, acc_anc=()):
+                  all_accepted, keeps, acc_anc=(), acc_w=()):
         rank, ws = dd.world()
         torch = gpu.torch
         def cat(lst):
@@ -296,16 +343,23 @@ class BatchedGPUSampler(Sampler):
             lp = torch.empty(0, dtype=gpu.F64, device=dev)
             dist = torch.empty(0, dtype=gpu.F64, device=dev)
             x = torch.empty((0, S), dtype=gpu.F64, device=dev)
-        # importance weights for this rank's accepted rows (smc.py:768-811)
-        if spec.transition is None or all_accepted:
+        # importance weights for this rank's accepted rows (smc.py:768-811);
+        # a StochasticAcceptor's acceptance weights multiply in
+        accw = cat(acc_w) if acc_w and len(acc_w) == len(acc_theta) else None
+        if all_accepted:
             w = torch.ones(theta.shape[0], dtype=gpu.F64, device=dev)
+        elif spec.transition is None:
+            # t = 0: w = n_acc / n_per_param * prod(acceptance weights)
+            w = (accw.contiguous() if accw is not None else
+                 torch.ones(theta.shape[0], dtype=gpu.F64, device=dev))
         else:
             # ancestors of the accepted rows: population rows near them,
             # used by the x3 density kernel as exponent offsets
             anc = (cat(acc_anc) if acc_anc and
                    len(acc_anc) == len(acc_theta) else None)
             lt = spec.transition.logpdf_device(theta, hint=anc)
-            w = gpu.importance_weights(lp, lt, spec.weight_scale)
+            w = gpu.importance_weights(lp, lt, spec.weight_scale,
+                                       acc_w=None if accw is None else accw.contiguous())
         if ws > 1:
             theta = dd.allgather_rows(theta, dev)
             w = dd.allgather_rows(w, dev)

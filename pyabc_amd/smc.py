@@ -19,9 +19,10 @@ import numpy as np
 import pandas as pd
 
 from . import gpu
-from .acceptor import Acceptor, SimpleFunctionAcceptor, UniformAcceptor
-from .distance import Distance, PNormDistance, to_distance
-from .epsilon import Epsilon, MedianEpsilon
+from .acceptor import (Acceptor, SimpleFunctionAcceptor, StochasticAcceptor,
+                       UniformAcceptor)
+from .distance import Distance, PNormDistance, StochasticKernel, to_distance
+from .epsilon import DeviceRecords, Epsilon, MedianEpsilon, TemperatureBase
 from .model import Model, SimpleModel, VectorizedModel
 from .parameters import Parameter
 from .population import Particle, Population
@@ -59,6 +60,11 @@ class GenerationSpec:
         self.distance = None if all_accepted else abc.distance_function
         self.eps = None if all_accepted else abc.eps(t)
         self.sum_stat_keys = list(abc.x_0.keys())
+        # StochasticAcceptor: (pdf_norm, temperature, log scale, importance
+        # weighting) of this generation for abc_stochastic_accept
+        self.stochastic = None
+        if isinstance(abc.acceptor, StochasticAcceptor) and not all_accepted:
+            self.stochastic = abc.acceptor.device_config(t, self.eps)
         self._closure = None
         self._init_device(abc)
 
@@ -74,10 +80,17 @@ class GenerationSpec:
             why.append("custom summary_statistics function")
         if self.nr_samples_per_parameter != 1:
             why.append("nr_samples_per_parameter != 1")
-        if not isinstance(abc.acceptor, UniformAcceptor) or \
+        if isinstance(abc.acceptor, StochasticAcceptor):
+            if not getattr(abc.distance_function, "batched_capable", False):
+                why.append("StochasticAcceptor without a batched noise-model "
+                           "kernel")
+        elif not isinstance(abc.acceptor, UniformAcceptor) or \
                 abc.acceptor.use_complete_history:
-            why.append("acceptor is not UniformAcceptor(current time)")
-        if self.distance is not None and not hasattr(self.distance, "device_call"):
+            why.append("acceptor is not UniformAcceptor(current time) or "
+                       "StochasticAcceptor")
+        if self.distance is not None and (
+                not hasattr(self.distance, "device_call")
+                or not getattr(self.distance, "batched_capable", True)):
             why.append("distance has no device kernel")
         if self.transition is not None and not hasattr(self.transition,
                                                        "propose_device"):
@@ -176,6 +189,18 @@ class ABCSMC:
         # optional callable(t) run after each completed generation (timing
         # hooks; not part of the reference API)
         self.generation_callback = None
+        self._sanity_check()
+
+    def _sanity_check(self):
+        """smc.py:238-248: the stochastic components go together."""
+        stochastics = [isinstance(self.acceptor, StochasticAcceptor),
+                       isinstance(self.eps, TemperatureBase),
+                       isinstance(self.distance_function, StochasticKernel)]
+        if not all(stochastics) and any(stochastics):
+            raise ValueError(
+                "Please only use acceptor.StochasticAcceptor, "
+                "epsilon.TemperatureBase and distance.StochasticKernel "
+                "together.")
 
     def __getstate__(self):
         state = self.__dict__.copy()
@@ -233,6 +258,11 @@ class ABCSMC:
 
         def get_initial_records():
             population = _get_initial_population_with_distances()
+            if population.columns is not None:
+                # calibration sample on the device: transition densities 1
+                d = population.columns.distances
+                one = gpu.torch.zeros_like(d)
+                return DeviceRecords(d, one, one, gpu.torch.full_like(d, -1.0))
             records = []
             for particle in population.get_list():
                 for d in particle.accepted_distances:
@@ -432,7 +462,9 @@ class ABCSMC:
             max_nr_populations: int = np.inf,
             min_acceptance_rate: float = 0.) -> History:
         if minimum_epsilon is None:
-            minimum_epsilon = 0.0
+            # smc.py:860-864: a temperature schedule ends at T = 1
+            minimum_epsilon = 1.0 if isinstance(self.eps, TemperatureBase) \
+                else 0.0
         self.minimum_epsilon = minimum_epsilon
         self.max_nr_populations = max_nr_populations
         self.min_acceptance_rate = min_acceptance_rate
@@ -528,6 +560,9 @@ class ABCSMC:
                              acceptance_rate)
 
         def get_all_records():
+            dev = self._device_records(t, sample, prev_transitions)
+            if dev is not None:
+                return dev
             recorded_particles = sample.first_m_particles(
                 self.max_nr_recorded_particles)
             records = []
@@ -547,6 +582,34 @@ class ABCSMC:
 
         self.eps.update(t, get_weighted_distances, get_all_records,
                         acceptance_rate, self.acceptor.get_epsilon_config(t))
+
+    def _device_records(self, t, sample, prev_transitions):
+        """Records of the batched sampler (smc.py:1008-1035) with the two
+        transition densities evaluated for all of them on the device: log
+        t_pd_prev under the transition that proposed them (the prior for
+        t - 1 == 0), log t_pd under the freshly fitted one."""
+        recs = getattr(sample, "device_records", None)
+        if recs is None or len(self.models) != 1:
+            return None
+        rec = recs(self.max_nr_recorded_particles)
+        if rec is None:
+            return None
+        theta, dist, key, anc = rec
+        if t - 1 == 0:
+            spec = self.parameter_priors[0].device_spec()
+            kinds = gpu.as_dev(spec[0], dtype=gpu.torch.int32, device=theta.device)
+            lp_prev = gpu.prior_logpdf(theta, kinds,
+                                       gpu.as_dev(spec[1], device=theta.device))
+        else:
+            tr_prev = prev_transitions[0]
+            if not hasattr(tr_prev, "logpdf_device"):
+                return None
+            lp_prev = tr_prev.logpdf_device(theta, hint=anc)
+        tr = self.transitions[0]
+        if not hasattr(tr, "logpdf_device"):
+            return None
+        lp = tr.logpdf_device(theta)
+        return DeviceRecords(dist, lp_prev, lp, key)
 
     def _adapt_population_size(self, t):
         if t == 0:

@@ -327,7 +327,149 @@ def gen_cv(seeds=tuple(range(24))):
     print("cv", cv_fixed, cvs.mean(axis=1), cvs.std(axis=1), n_est)
 
 
+def gen_stochastic():
+    """StochasticKernel values, StochasticAcceptor decisions, pdf norms and
+    temperature schemes (kernel.py, acceptor.py, pdf_norm.py,
+    temperature.py)."""
+    from pyabc.distance import (NormalKernel, IndependentNormalKernel,
+                                IndependentLaplaceKernel, BinomialKernel,
+                                PoissonKernel, NegativeBinomialKernel,
+                                SCALE_LIN, SCALE_LOG)
+    from pyabc.epsilon.temperature import (
+        match_acceptance_rate, EssScheme, AcceptanceRateScheme,
+        ExpDecayFixedIterScheme, ExpDecayFixedRatioScheme,
+        PolynomialDecayFixedIterScheme, DalyScheme, FrielPettittScheme,
+        Temperature)
+    from pyabc.acceptor import (StochasticAcceptor, pdf_norm_max_found,
+                                pdf_norm_from_kernel, ScaledPDFNorm)
+    rng = np.random.default_rng(2024)
+    keys = ["s0", "s1", "s2", "s3"]
+    B = 64
+    out = {}
+
+    def run(kern, X, x0):
+        x0d = dict(zip(keys, x0))
+        kern.initialize(0, None, x0d)
+        v = np.array([kern(dict(zip(keys, row)), x0d) for row in X],
+                     dtype=float)
+        pm = np.nan if kern.pdf_max is None else float(kern.pdf_max)
+        return v, pm
+
+    x0 = rng.normal(size=4)
+    X = x0 + 1.5 * rng.normal(size=(B, 4))
+    var = np.array([0.5, 1.0, 2.0, 0.7])
+    A = rng.normal(size=(4, 4))
+    cov = A @ A.T + np.eye(4)
+    out.update(cont_x=X, cont_x0=x0, var=var, cov=cov)
+    for tag, kern in [
+            ("inorm", IndependentNormalKernel(var=var)),
+            ("inorm1", IndependentNormalKernel()),
+            ("ilap", IndependentLaplaceKernel(scale=var)),
+            ("normal", NormalKernel(cov=cov)),
+            ("normal_lin", NormalKernel(cov=cov, ret_scale=SCALE_LIN))]:
+        out[tag], out[tag + "_pdfmax"] = run(kern, X, x0)
+    k0 = rng.integers(0, 12, size=4).astype(float)
+    Xc = rng.integers(0, 20, size=(B, 4)) + 0.6 * (rng.random((B, 4)) < 0.3)
+    out.update(count_x=Xc, count_x0=k0, p_binom=0.7, p_nbinom=0.4)
+    for tag, kern in [
+            ("poisson", PoissonKernel()),
+            ("poisson_lin", PoissonKernel(ret_scale=SCALE_LIN)),
+            ("binom", BinomialKernel(p=0.7)),
+            ("binom_lin", BinomialKernel(p=0.7, ret_scale=SCALE_LIN)),
+            ("nbinom", NegativeBinomialKernel(p=0.4))]:
+        with np.errstate(all="ignore"):
+            out[tag], out[tag + "_pdfmax"] = run(kern, Xc, k0)
+
+    # accept decisions: the reference draws u with np.random.uniform
+    kern = IndependentNormalKernel(var=var)
+    x0d = dict(zip(keys, x0))
+    kern.initialize(0, None, x0d)
+    for tag, scale in (("acc_log", SCALE_LOG), ("acc_lin", SCALE_LIN)):
+        acc = StochasticAcceptor()
+        acc.pdf_norms = {0: -3.0 if scale == SCALE_LOG else 0.01}
+        kk = kern if scale == SCALE_LOG else NormalKernel(
+            cov=np.diag(var), ret_scale=SCALE_LIN)
+        kk.initialize(0, None, x0d)
+        us, ds, accs, ws = [], [], [], []
+        for i in range(B):
+            np.random.seed(1000 + i)
+            us.append(np.random.uniform(low=0, high=1))
+            np.random.seed(1000 + i)
+            r = acc(kk, lambda t: 2.5, dict(zip(keys, X[i])), x0d, 0, None)
+            ds.append(r.distance)
+            accs.append(r.accept)
+            ws.append(r.weight)
+        out[tag + "_u"] = np.array(us)
+        out[tag + "_dens"] = np.array(ds)
+        out[tag + "_accept"] = np.array(accs)
+        out[tag + "_weight"] = np.array(ws)
+        out[tag + "_pdf_norm"] = acc.pdf_norms[0]
+
+    # match_acceptance_rate: log and linear scale, and the corner cases
+    R = 500
+    pds = rng.normal(-3.0, 2.0, R)
+    wts = np.exp(0.5 * rng.standard_normal(R))
+    out.update(mar_pds=pds, mar_w=wts)
+    out["mar_log"] = match_acceptance_rate(wts / wts.sum(), pds, pds.max(),
+                                           SCALE_LOG, 0.3)
+    out["mar_log_low"] = match_acceptance_rate(wts / wts.sum(), pds,
+                                               pds.max() + 1.0, SCALE_LOG, 0.05)
+    out["mar_log_one"] = match_acceptance_rate(wts / wts.sum(), pds, pds.min(),
+                                               SCALE_LOG, 0.3)
+    lpds = np.exp(pds)
+    out["mar_lin"] = match_acceptance_rate(wts / wts.sum(), lpds, lpds.max(),
+                                           SCALE_LIN, 0.3)
+    # EssScheme
+    N = 400
+    ep = rng.normal(-2.0, 1.5, N)
+    ew = np.exp(0.3 * rng.standard_normal(N))
+    out.update(ess_pds=ep, ess_w=ew)
+
+    def wd():
+        return pd.DataFrame({"distance": ep, "w": ew})
+    for tag, prev in (("ess_prev", 7.53), ("ess_none", None)):
+        out[tag] = float(np.ravel(EssScheme()(
+            t=1, get_weighted_distances=wd, get_all_records=None,
+            max_nr_populations=5, pdf_norm=ep.max(), kernel_scale=SCALE_LOG,
+            prev_temperature=prev, acceptance_rate=0.3))[0])
+    # deterministic schemes at a few (t, prev_temperature, acceptance rate)
+    sch = []
+    for t, prev, ar in ((1, 7.53, 0.4), (2, 3.0, 0.6), (3, 12.0, 5e-5)):
+        args = dict(t=t, get_weighted_distances=wd, get_all_records=None,
+                    max_nr_populations=5, pdf_norm=0.0,
+                    kernel_scale=SCALE_LOG, prev_temperature=prev,
+                    acceptance_rate=ar)
+        row = [ExpDecayFixedIterScheme()(**args),
+               ExpDecayFixedRatioScheme()(**args),
+               PolynomialDecayFixedIterScheme()(**args),
+               DalyScheme()(**args), FrielPettittScheme()(**args)]
+        sch.append([t, prev, ar] + row)
+    out["schemes"] = np.array(sch)
+    # Temperature orchestration with list records
+    recs = [dict(distance=pds[i], transition_pd_prev=1.0,
+                 transition_pd=wts[i], accepted=bool(i % 3 == 0))
+            for i in range(R)]
+    temp = Temperature()
+    cfg = dict(pdf_norm=pds.max(), kernel_scale=SCALE_LOG)
+    temp.initialize(0, wd, lambda: recs, 4, cfg)
+    for t in (1, 2, 3):
+        temp.update(t, wd, lambda: recs, 0.2, cfg)
+    out["temp_seq"] = np.array([temp(t) for t in range(4)])
+    # pdf norms
+    pn = dict(kernel_val=42, prev_pdf_norm=3.5, get_weighted_distances=wd,
+              prev_temp=10.3, acceptance_rate=0.05)
+    out["pdfnorm"] = np.array([pdf_norm_max_found(**pn),
+                               pdf_norm_from_kernel(**pn),
+                               ScaledPDFNorm()(**pn)])
+    np.savez_compressed(os.path.join(HERE, "stochastic.npz"), **out)
+    print("stochastic", out["mar_log"], out["mar_lin"], out["ess_prev"],
+          out["temp_seq"], out["pdfnorm"])
+
+
 if __name__ == "__main__":
+    if "--stochastic" in sys.argv:
+        gen_stochastic()
+        sys.exit(0)
     if "--cv" in sys.argv:
         gen_cv()
         sys.exit(0)

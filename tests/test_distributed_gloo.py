@@ -108,8 +108,9 @@ def _install_cpu_doubles(monkeypatch_like):
     def gather_rows_batch(arrays, idx, n=None):
         return [a.index_select(0, idx) for a in arrays]
 
-    def importance_weights(lp, lt, scale=1.0):
-        return torch.exp(lp - lt) * scale
+    def importance_weights(lp, lt, scale=1.0, acc_w=None):
+        w = torch.exp(lp - lt) * scale
+        return w if acc_w is None else w * acc_w
 
     monkeypatch_like(g, "require_device", lambda: torch.device("cpu"))
     monkeypatch_like(g, "accept_compact", accept_compact)
