@@ -16,6 +16,11 @@ peak.  Inputs are synthetic, generated on the device or from seeded numpy.
             the default k = N/4 = 25000), density of 1e5 candidates
   sampler   propose + simulate + pnorm + accept at the c3 batch (4.6e6)
   cv        AdaptivePopulationSize.update on the c2 population (wall time)
+  stochastic StochasticAcceptor stack at the c3 batch (4.6e6 candidates):
+            IndependentNormalKernel values (S = 10), tempered accept step,
+            one AcceptanceRateScheme objective over 4.6e6 records, the full
+            bisection; plus wall time per generation of a c2-size
+            (N = 1e5, d = 10) stochastic ABCSMC run
 """
 import argparse
 import json
@@ -197,6 +202,61 @@ def cv(reps):
                                pair_evals_per_s=round(pairs / sec, 1),
                                new_size=ps.nr_particles,
                                reference_core_s_extrapolated=round(pairs / 7.8e6)))
+
+
+def stochastic(reps):
+    import time
+    import torch
+    import pyabc_amd as pa
+    from pyabc_amd import gpu
+    from pyabc_amd.epsilon.temperature import match_acceptance_rate
+    B, S = 4_600_000, 10
+    x = torch.randn(B, S, dtype=torch.float64, device="cuda")
+    keys = [f"y{k}" for k in range(S)]
+    x0 = {k: 0.5 for k in keys}
+    kern = pa.IndependentNormalKernel(var=np.full(S, 0.3))
+    kern.initialize(0, None, x0)
+    x0v = gpu.as_dev(np.full(S, 0.5))
+    out = torch.empty(B, dtype=torch.float64, device="cuda")
+    ms = timed(lambda: kern.device_call(x, x0v, 0, keys, out=out), reps)
+    emit("kernel values (IndependentNormalKernel, S=10)", "c3 batch: 4.6e6",
+         ms, bytes_=B * (8 * S + 8))
+    res = {}
+    ms = timed(lambda: res.__setitem__("a", gpu.stochastic_accept(
+        out, float(out.max()), 3.0, True, True, 7, 2, 0)), reps)
+    emit("stochastic accept (u, acc, weight)", "c3 batch", ms,
+         bytes_=B * (8 + 16))
+    lr = torch.randn(B, dtype=torch.float64, device="cuda").mul_(0.3)
+    lp = torch.zeros(B, dtype=torch.float64, device="cuda")
+    c = float(out.max())
+    ms = timed(lambda: gpu.temper_sums(out, lr, c, True, gpu.TEMPER_ACCEPTANCE,
+                                       0.3, 0.0, lr_sub=lp), reps)
+    emit("AcceptanceRateScheme objective (one bisection step)",
+         "c3 records: 4.6e6", ms, bytes_=B * 24,
+         extra={"note": "includes the 16-byte host read of the two sums"})
+    t0 = time.perf_counter()
+    T = match_acceptance_rate(out, lr, c, pa.distance.SCALE_LOG, 0.3, lp)
+    emit("match_acceptance_rate (full bisection)", "c3 records: 4.6e6",
+         (time.perf_counter() - t0) * 1e3, extra={"temperature": T})
+    # end to end: c2-size noise-model ABC (y = theta, IndependentNormal
+    # noise), StochasticAcceptor + Temperature(), batched sampler
+    d = 10
+    names = [f"p{k}" for k in range(d)]
+    model = pa.LinearGaussianModel(names, keys, src=list(range(d)),
+                                   sigma=[0.0] * d)
+    prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.IndependentNormalKernel(var=np.full(S, 0.25)),
+                    population_size=100_000, eps=pa.Temperature(),
+                    acceptor=pa.StochasticAcceptor(),
+                    sampler=pa.BatchedGPUSampler(seed=5))
+    abc.new("sqlite://", {k: 1.0 for k in keys})
+    abc.run(max_nr_populations=6)
+    log = abc.generation_log
+    emit("stochastic ABCSMC generation (c2 size)",
+         "N=1e5, d=S=10, IndependentNormalKernel(var .25), Temperature()",
+         1e3 * float(np.median([g["seconds"] for g in log[1:]])),
+         extra={"temperatures": [round(abc.eps(g["t"]), 3) for g in log],
+                "n_sim": [g["n_sim"] for g in log]})
 
 
 def main():
