@@ -16,6 +16,9 @@ CSRC = os.path.join(HERE, "csrc")
 ROOT = os.path.dirname(HERE)
 OBJ = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libabcgpu.so")
+# host-only bulk SQLite writer (History file store), built with g++
+STORE_SRC = os.path.join(HERE, "hostsrc", "abc_store.cpp")
+STORE_LIB = os.path.join(HERE, "libabcstore.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}",
@@ -54,6 +57,25 @@ def _compile(src):
     return obj, True
 
 
+def build_store(force=False, verbose=True):
+    """libabcstore.so: g++ against the system libsqlite3.so.0."""
+    deps = [STORE_SRC, os.path.join(ROOT, "include", "abcstore.h")]
+    if (not force and os.path.exists(STORE_LIB) and
+            os.path.getmtime(STORE_LIB) >= max(os.path.getmtime(f) for f in deps)):
+        changed = False
+    else:
+        cmd = ["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-Wall",
+               "-I", os.path.join(ROOT, "include"), STORE_SRC, "-o", STORE_LIB,
+               "-l:libsqlite3.so.0"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"g++ failed for {STORE_SRC}:\n{r.stderr}")
+        changed = True
+    if verbose:
+        print(f"libabcstore: {STORE_LIB} ({'rebuilt' if changed else 'up to date'})")
+    return STORE_LIB
+
+
 def build(force=False, verbose=True):
     os.makedirs(OBJ, exist_ok=True)
     if force:
@@ -71,6 +93,7 @@ def build(force=False, verbose=True):
             raise RuntimeError(f"link failed:\n{r.stderr}")
     if verbose:
         print(f"libabcgpu: {LIB} ({'rebuilt' if changed else 'up to date'})")
+    build_store(force=force, verbose=verbose)
     return LIB
 
 

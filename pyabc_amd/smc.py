@@ -226,14 +226,14 @@ class ABCSMC:
         return self.history
 
     def load(self, db: str, abc_id: int = 1, observed_sum_stat: dict = None):
-        """smc.py:355-389 for an in-process History object or db string."""
+        """smc.py:355-389: resume from an in-process History object or a
+        ``sqlite:///path`` file (written by this engine or by pyABC)."""
         if isinstance(db, History):
             self.history = db
+            self.history.id = abc_id
         else:
-            raise NotImplementedError(
-                "resuming from a database file is not supported; pass the "
-                "History object of the earlier run")
-        self.history.id = abc_id
+            self.history = History(db)
+            self.history.load_run(abc_id)
         if observed_sum_stat is None:
             observed_sum_stat = self.history.observed_sum_stat()
         self.x_0 = observed_sum_stat

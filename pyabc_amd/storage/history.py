@@ -9,13 +9,13 @@ exceeds ``History.DEVICE_BUDGET``; older ones then move to host numpy.  Host
 copies are made on first query only.
 The query methods ABCSMC and users need (get_distribution,
 get_model_probabilities, get_population, get_all_populations, max_t,
-total_nr_simulations, ...) return the reference's pandas shapes.  The
-``db`` string is kept for API compatibility; an optional ``sqlite:///path``
-is written with a bulk (executemany) writer in ``done()``.
+total_nr_simulations, ...) return the reference's pandas shapes.
+``sqlite://`` (in memory) keeps everything in HBM / host memory; a file
+``sqlite:///path`` is also written in pyABC's schema by the bulk writer of
+``sqlite_store`` (libabcstore.so, in the background) and can be resumed with
+``ABCSMC.load`` -- including files written by pyABC itself.
 """
 import datetime
-import json
-import sqlite3
 
 import numpy as np
 import pandas as pd
@@ -38,6 +38,32 @@ class _Gen:
         self.model_names = model_names
         self.end_time = datetime.datetime.now()
         self.host = None
+
+    @classmethod
+    def from_host(cls, t, h, model_names):
+        """A generation read back from a database file (host only)."""
+        g = cls(t, h["epsilon"], h["samples"], None, model_names)
+        g.host = h
+        g.end_time = h.get("end_time", g.end_time)
+        return g
+
+    def host_future(self):
+        """Callable returning the host dict; for device populations the
+        copies are enqueued now (pinned, async) and waited for on call."""
+        pop = self.population
+        if pop is None or pop.columns is None:
+            return self.to_host
+        from .. import gpu
+        c = pop.columns
+        futs = [gpu.HostFuture(a) for a in (c.theta, c.weights, c.distances,
+                                             c.sum_stats)]
+        names, keys = list(c.param_names), list(c.sum_stat_keys)
+
+        def get():
+            th, w, d, ss = (f.get() for f in futs)
+            return dict(theta=th, w=w, distance=d, sum_stats=ss, names=names,
+                        keys=keys)
+        return get
 
     def to_host(self):
         if self.host is not None:
@@ -87,6 +113,23 @@ class _Gen:
         self.population = None
 
 
+def _population_from_host(h):
+    """A particle-list Population of a host-only generation (one accepted
+    sample per particle, as History stores it)."""
+    from ..parameters import Parameter
+    from ..population import Particle, Population
+    parts = []
+    for i in range(len(h["w"])):
+        ss = dict(zip(h["keys"], map(float, h["sum_stats"][i]))) \
+            if len(h["keys"]) else {}
+        parts.append(Particle(
+            m=int(h["m"][i]) if "m" in h else 0,
+            parameter=Parameter(dict(zip(h["names"], map(float, h["theta"][i])))),
+            weight=float(h["w"][i]), accepted_sum_stats=[ss],
+            accepted_distances=[float(h["distance"][i])]))
+    return Population(parts)
+
+
 class History:
     PRE_TIME = -1
 
@@ -103,6 +146,34 @@ class History:
         self.start_time = None
         self.end_time = None
         self._meta = {}
+        self._store = None
+        path = db[len("sqlite:///"):] if db.startswith("sqlite:///") else ""
+        if path:
+            from .sqlite_store import SQLiteStore
+            self._store = SQLiteStore(path)
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state["_store"] = None          # thread + native handle stay local
+        return state
+
+    @property
+    def db_file(self):
+        return self._store.path if self._store is not None else None
+
+    def load_run(self, abc_id=None):
+        """Read a run back from the database file (history.py readers)."""
+        from .sqlite_store import read_run
+        if self._store is None:
+            raise ValueError("load_run needs a sqlite:///path database")
+        self._store.flush()
+        self.id, gens, meta = read_run(self._store.path, abc_id)
+        names = meta.get("model_names", [])
+        self._gens = {t: _Gen.from_host(t, h, names) for t, h in gens.items()}
+        self._pre_samples = meta["pre_samples"]
+        self._meta.update(x_0=meta["x_0"], gt_par=meta["gt_par"],
+                          model_names=names)
+        return self
 
     # -- writing ----------------------------------------------------------
     def store_initial_data(self, ground_truth_model, options, observed_summary_statistics,
@@ -116,15 +187,36 @@ class History:
                           distance=distance_function_json_str,
                           epsilon=eps_function_json_str,
                           population_strategy=population_strategy_json_str)
+        if self._store is not None:
+            self.id = self._store.new_run(options, distance_function_json_str,
+                                          eps_function_json_str,
+                                          population_strategy_json_str)
+            self._store.store_pre_population(
+                self.id, ground_truth_model, observed_summary_statistics,
+                ground_truth_parameter, model_names)
 
     def update_nr_samples(self, t, nr_samples):
         if t == History.PRE_TIME:
             self._pre_samples = int(nr_samples)
+        elif t in self._gens:
+            self._gens[t].samples = int(nr_samples)
+        if self._store is not None:
+            self._store.update_nr_samples(self.id, t, nr_samples)
 
     def append_population(self, t, current_epsilon, population, nr_simulations,
                           model_names):
-        self._gens[t] = _Gen(t, current_epsilon, nr_simulations, population,
-                             model_names)
+        g = _Gen(t, current_epsilon, nr_simulations, population, model_names)
+        self._gens[t] = g
+        if self._store is not None:
+            mp = g.model_probabilities()
+            if len(mp) > 1:
+                raise NotImplementedError(
+                    "the file store writes single-model populations")
+            m = next(iter(mp)) if mp else 0
+            self._store.submit(self.id, t, current_epsilon, nr_simulations,
+                               g.host_future(), model_names[m] if model_names
+                               else "model", float(mp.get(m, 1.0)), m,
+                               self.stores_sum_stats)
         # keep generations device-resident (no host round trip inside the
         # generation loop); offload the oldest beyond the HBM budget
         resident = sorted(tt for tt, g in self._gens.items()
@@ -138,27 +230,13 @@ class History:
 
     def done(self):
         self.end_time = datetime.datetime.now()
-        if self.db.startswith("sqlite:///"):
-            self._write_sqlite(self.db[len("sqlite:///"):])
+        if self._store is not None:
+            self._store.done(self.id)
 
-    def _write_sqlite(self, path):
-        con = sqlite3.connect(path)
-        cur = con.cursor()
-        cur.execute("CREATE TABLE IF NOT EXISTS populations (abc_id INTEGER, t "
-                    "INTEGER, epsilon REAL, nr_samples INTEGER)")
-        cur.execute("CREATE TABLE IF NOT EXISTS particles (abc_id INTEGER, t "
-                    "INTEGER, m INTEGER, w REAL, distance REAL, params TEXT)")
-        for t, g in sorted(self._gens.items()):
-            cur.execute("INSERT INTO populations VALUES (?,?,?,?)",
-                        (self.id, t, g.epsilon, g.samples))
-            h = g.to_host()
-            rows = [(self.id, t, int(h["m"][i]), float(h["w"][i]),
-                     float(h["distance"][i]),
-                     json.dumps(dict(zip(h["names"], map(float, h["theta"][i])))))
-                    for i in range(len(h["w"]))]
-            cur.executemany("INSERT INTO particles VALUES (?,?,?,?,?,?)", rows)
-        con.commit()
-        con.close()
+    def flush(self):
+        """Wait until every population is in the database file."""
+        if self._store is not None:
+            self._store.flush()
 
     # -- reading ----------------------------------------------------------
     @property
@@ -171,7 +249,9 @@ class History:
 
     @property
     def total_nr_simulations(self):
-        return sum(g.samples for g in self._gens.values())
+        # history.py:556-568 sums nr_samples over all populations, the
+        # calibration (t = PRE_TIME) included
+        return self._pre_samples + sum(g.samples for g in self._gens.values())
 
     def observed_sum_stat(self):
         return self._meta.get("x_0", {})
@@ -181,7 +261,7 @@ class History:
         g = self._gens[t]
         if g.population is not None:
             return g.population
-        raise KeyError(f"population {t} is no longer device resident")
+        return _population_from_host(g.to_host())
 
     def get_population_device(self, t=None):
         t = self.max_t if t is None else t
@@ -224,7 +304,7 @@ class History:
     def get_all_populations(self):
         rows = [dict(t=History.PRE_TIME, population_end_time=self.start_time,
                      samples=self._pre_samples, epsilon=np.inf,
-                     particles=0)]
+                     particles=1)]       # the ground-truth particle
         for t, g in sorted(self._gens.items()):
             rows.append(dict(t=t, population_end_time=g.end_time,
                              samples=g.samples, epsilon=g.epsilon,

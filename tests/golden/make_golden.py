@@ -466,7 +466,76 @@ def gen_stochastic():
           out["temp_seq"], out["pdfnorm"])
 
 
+def gen_history():
+    """A small run stored by pyABC's own History (read back by our
+    read_run), and a file written by our bulk writer read by pyABC's
+    History (history.py readers over db_model.py)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from pyabc_amd.storage.sqlite_store import SQLiteStore
+    ref_db = os.path.join(HERE, "ref_history.db")
+    if os.path.exists(ref_db):
+        os.remove(ref_db)
+    np.random.seed(0)
+
+    def model(p):
+        return {"y": p["x"] + 0.5 * np.random.randn(), "z": 2 * p["x"]}
+    prior = pyabc.Distribution(x=pyabc.RV("norm", 0, 1))
+    abc = pyabc.ABCSMC(model, prior, pyabc.PNormDistance(), population_size=40,
+                       sampler=pyabc.sampler.SingleCoreSampler())
+    abc.new("sqlite:///" + ref_db, {"y": 2.0, "z": 4.0},
+            gt_par={"x": 1.5})
+    h = abc.run(max_nr_populations=2)
+    out = {}
+    for t in range(h.max_t + 1):
+        df, w = h.get_distribution(0, t)
+        out[f"theta_{t}"] = df["x"].values
+        out[f"w_{t}"] = w
+        wd = h.get_weighted_distances(t)
+        out[f"dist_{t}"] = wd["distance"].values
+    pops = h.get_all_populations()
+    out["pops"] = pops[["t", "samples", "epsilon", "particles"]].values.astype(float)
+    # our writer -> pyABC's reader
+    ours_db = "/tmp/ours_history_golden.db"
+    if os.path.exists(ours_db):
+        os.remove(ours_db)
+    rng = np.random.default_rng(3)
+    n, d, S = 50, 3, 2
+    th = rng.normal(size=(n, d))
+    w = rng.random(n)
+    w /= w.sum()
+    dist = rng.random(n)
+    ss = rng.normal(size=(n, S))
+    st = SQLiteStore(ours_db)
+    abc_id = st.new_run({}, "{}", "{}", "{}")
+    st.store_pre_population(abc_id, 0, {"s0": 1.0, "s1": 2.0}, {"a": 0.5},
+                            ["m0"])
+    st.submit(abc_id, 0, 0.7, 123, lambda: dict(
+        theta=th, w=w, distance=dist, sum_stats=ss, names=["a", "b", "c"],
+        keys=["s0", "s1"]), "m0")
+    st.update_nr_samples(abc_id, -1, 77)
+    st.done(abc_id)
+    st.close()
+    hr = pyabc.History("sqlite:///" + ours_db)
+    hr.id = abc_id
+    df, wr = hr.get_distribution(0, 0)
+    ws, sss = hr.get_weighted_sum_stats(0)
+    out.update(ours_theta=th, ours_w=w, ours_dist=dist, ours_ss=ss,
+               ours_ref_theta=df[["a", "b", "c"]].values, ours_ref_w=wr,
+               ours_ref_ss=np.array([[s["s0"], s["s1"]] for s in sss]),
+               ours_ref_dist=hr.get_weighted_distances(0)["distance"].values,
+               ours_ref_x0=np.array([hr.observed_sum_stat()["s0"],
+                                     hr.observed_sum_stat()["s1"]]),
+               ours_ref_pops=hr.get_all_populations()[
+                   ["t", "samples", "epsilon", "particles"]].values.astype(float),
+               ours_ref_nsim=hr.total_nr_simulations)
+    np.savez_compressed(os.path.join(HERE, "history.npz"), **out)
+    print("history", out["pops"], out["ours_ref_pops"])
+
+
 if __name__ == "__main__":
+    if "--history" in sys.argv:
+        gen_history()
+        sys.exit(0)
     if "--stochastic" in sys.argv:
         gen_stochastic()
         sys.exit(0)

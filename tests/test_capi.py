@@ -41,3 +41,21 @@ def test_invalid_arguments_raise_without_device():
     with pytest.raises(ValueError):
         nat.call("abc_pnorm", None, 10, 0, None, None, 2.0, None, None)
     assert "pnorm" in nat.load().abc_last_error().decode()
+
+
+def test_store_library_exports_abcstore_h():
+    """libabcstore.so (host code) exports every symbol include/abcstore.h
+    declares, and reports errors through abc_store_last_error."""
+    from pyabc_amd import build
+    from pyabc_amd.storage import sqlite_store
+    build.build_store(verbose=False)
+    src = open(os.path.join(ROOT, "include", "abcstore.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = sorted(set(re.findall(r"\b(abc_store_[a-z0-9_]+)\s*\(", src)))
+    assert len(names) == 5
+    lib = sqlite_store.load()
+    for name in names:
+        assert hasattr(lib, name), name
+    h = ctypes.c_void_p()
+    assert lib.abc_store_open(b"/nonexistent-dir/x.db", ctypes.byref(h)) != 0
+    assert b"open" in lib.abc_store_last_error()
