@@ -239,10 +239,14 @@ int abc_local_fit(const double* X, const double* w, int64_t N, int d,
                   double* inv_covs, double* dets, double* chol,
                   double* log_norm, void* ws, size_t ws_bytes, void* stream);
 /* pdf: out[i] = log( sum_j w_j exp(-d_ij^T inv_j d_ij / 2 - log_norm_j)
- * / sum_j w_j ), d_ij = X_j - x_i. */
+ * / sum_j w_j ), d_ij = X_j - x_i.  The quadratic form is a GEMM over the
+ * candidates' quadratic features on fp64 MFMA (workspace: packed population
+ * coefficients + per-chunk partial sums). */
+size_t abc_local_logpdf_workspace(int64_t M, int64_t N, int d);
 int abc_local_logpdf(const double* x, int64_t M, const double* X,
                      const double* w, int64_t N, int d, const double* inv_covs,
-                     const double* log_norm, double* out, void* stream);
+                     const double* log_norm, double* out, void* ws,
+                     size_t ws_bytes, void* stream);
 /* rvs: ancestor j ~ Cat(w) (cdf), theta = X_j + chol_j n; same Philox keying
  * and prior re-draw loop as abc_propose. */
 int abc_local_propose(const double* X, const double* cdf,

@@ -61,7 +61,8 @@ SIGNATURES = {
     "abc_local_fit_workspace": (SZ, [I64, I32]),
     "abc_local_fit": (I32, [P, P, I64, I32, I64, D, D, P, P, P, P, P, P, SZ,
                             P]),
-    "abc_local_logpdf": (I32, [P, I64, P, P, I64, I32, P, P, P, P]),
+    "abc_local_logpdf_workspace": (SZ, [I64, I64, I32]),
+    "abc_local_logpdf": (I32, [P, I64, P, P, I64, I32, P, P, P, P, SZ, P]),
     "abc_local_propose": (I32, [P, P, P, I64, I32, P, P, P, U64, U32, I64,
                                 I64, I32, P, P, P, P, P]),
     "abc_bootstrap_cv_workspace": (SZ, [I64]),

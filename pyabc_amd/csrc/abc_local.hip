@@ -361,67 +361,6 @@ __global__ __launch_bounds__(256) void local_fit_kernel(
   lnorm[n] = 0.5 * (D * LOG_2PI + log(det));
 }
 
-// density: block of 256 candidates, population staged through LDS in tiles;
-// exponents in fp64, the online log-sum-exp in log2 units with f32 exp2
-// (~1e-7 relative, the north star's fp32 bar is 1e-5)
-template <int D>
-__global__ __launch_bounds__(256) void local_pdf_kernel(
-    const double* __restrict__ x, int64_t M, const double* __restrict__ X,
-    const double* __restrict__ w, int64_t N, const double* __restrict__ invs,
-    const double* __restrict__ lnorm, double* __restrict__ out) {
-  constexpr int TJ = 32;
-  constexpr int REC = D + D * D + 1;  // X_j, inv_j, log w_j - lnorm_j
-  __shared__ double tile[TJ * REC];
-  __shared__ double wsum_sh[4];
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  double xi[D];
-#pragma unroll
-  for (int q = 0; q < D; ++q) xi[q] = (i < M) ? x[i * D + q] : 0.0;
-  double m = -INFINITY, l = 0.0, wsum = 0.0;
-  for (int64_t j0 = 0; j0 < N; j0 += TJ) {
-    const int nj = (int)((N - j0) < TJ ? (N - j0) : TJ);
-    __syncthreads();
-    for (int e = threadIdx.x; e < nj * REC; e += 256) {
-      const int jj = e / REC, f = e % REC;
-      const int64_t j = j0 + jj;
-      double v;
-      // log2 units: the exponent sums run on the f32 exp2 unit
-      if (f < D) v = X[j * D + f];
-      else if (f < D + D * D) v = invs[j * D * D + (f - D)] * (0.5 * LOG2E_L);
-      else { const double wj = w[j]; v = (wj > 0.0) ? (log(wj) - lnorm[j]) * LOG2E_L : -INFINITY; }
-      tile[jj * REC + f] = v;
-    }
-    __syncthreads();
-    for (int jj = 0; jj < nj; ++jj) {
-      const double* r = tile + jj * REC;
-      double dv[D];
-#pragma unroll
-      for (int q = 0; q < D; ++q) dv[q] = r[q] - xi[q];
-      double md = 0.0;
-#pragma unroll
-      for (int a = 0; a < D; ++a) {
-        double t = 0.0;
-#pragma unroll
-        for (int b = 0; b < D; ++b) t += r[D + a * D + b] * dv[b];
-        md += dv[a] * t;
-      }
-      // s in fp64 (log2 units); 2^(s - m) on v_exp_f32 (1e-7 per term)
-      const double s = r[D + D * D] - md;
-      const double dl = s - m;
-      if (dl > 0.0) { l = l * (double)__builtin_amdgcn_exp2f((float)-dl) + 1.0; m = s; }
-      else if (s > -INFINITY) l += (double)__builtin_amdgcn_exp2f((float)dl);
-    }
-  }
-  // sum of weights (np.average denominator), same for every candidate
-  double ws = 0.0;
-  for (int64_t j = threadIdx.x; j < N; j += 256) ws += w[j];
-  ws = wave_sum(ws);
-  if ((threadIdx.x & 63) == 0) wsum_sh[threadIdx.x >> 6] = ws;
-  __syncthreads();
-  wsum = ((wsum_sh[0] + wsum_sh[1]) + wsum_sh[2]) + wsum_sh[3];
-  if (i < M) out[i] = (l > 0.0) ? LN2_L * (m + log2(l)) - log(wsum) : -INFINITY;
-}
-
 constexpr int SEL_PB = 8;  // particles per selection block (in registers)
 
 template <int D>
@@ -448,12 +387,251 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   return ABC_OK;
 }
 
+
+// ---- density on fp64 MFMA ----------------------------------------------------
+// s_ij = log2 of w_j N(x_i; X_j, cov_j) = log2e (c_j - q_ij / 2), c_j =
+// log w_j - lnorm_j, q_ij = (X_j - x_i)^T A_j (X_j - x_i), A_j = inv_j.  In
+// coordinates centred at X_0 (y = x - X_0, Y_j = X_j - X_0), q is linear in the
+// quadratic features of the candidate,
+//   phi(y) = [y_a y_b (a <= b), y_a, 1, 0-padding]        (K = 4 * KB)
+// with population coefficients
+//   psi_j  = log2e * [-(A_ab + A_ba)/2 (a < b) | -A_aa/2,
+//                     ((A + A^T) Y_j)_a / 2, c_j - Y_j^T A Y_j / 2]
+// so s = psi_j . phi(y_i): a [N x K] x [K x M] GEMM on v_mfma_f64_16x16x4_f64
+// (population rows = A operand, candidate columns = B operand), followed by
+// the running max / exp2 / sum over j of each candidate column (exp2 on the
+// f32 unit, 1e-7 per term).
+template <int D>
+struct LocalFeat {
+  static constexpr int K0 = D * (D + 1) / 2 + D + 1;
+  static constexpr int KB = (K0 + 3) / 4;          // MFMA k-blocks of 4
+  static constexpr int NT = KB <= 6 ? 4 : 2;       // candidate tiles per wave
+};
+
+// feature k of centred candidate y (order: a <= b pairs, linear, constant)
+template <int D>
+__device__ __forceinline__ double local_phi(const double (&y)[D], int k) {
+  int q = 0;
+#pragma unroll
+  for (int a = 0; a < D; ++a)
+#pragma unroll
+    for (int b = a; b < D; ++b, ++q)
+      if (k == q) return y[a] * y[b];
+#pragma unroll
+  for (int a = 0; a < D; ++a, ++q)
+    if (k == q) return y[a];
+  return (k == q) ? 1.0 : 0.0;
+}
+
+// psi in fragment order [N/16 tiles][KB][64 lanes]: lane l of k-block kb
+// holds psi[tile*16 + (l & 15)][4 kb + (l >> 4)] (the A operand of one MFMA).
+// Rows j >= N get -inf in the constant slot (they add nothing).
+template <int D>
+__global__ __launch_bounds__(256) void local_pack_kernel(
+    const double* __restrict__ X, const double* __restrict__ w,
+    const double* __restrict__ invs, const double* __restrict__ lnorm,
+    int64_t N, int64_t ntiles, double* __restrict__ psi) {
+  constexpr int KB = LocalFeat<D>::KB;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= ntiles * KB * 64) return;
+  const int lane = (int)(e & 63);
+  const int kb = (int)((e >> 6) % KB);
+  const int64_t tile = (e >> 6) / KB;
+  const int64_t j = tile * 16 + (lane & 15);
+  const int k = 4 * kb + (lane >> 4);
+  double v = 0.0;
+  const int K0 = LocalFeat<D>::K0;
+  if (j >= N) {
+    v = (k == K0 - 1) ? -INFINITY : 0.0;
+  } else if (k < K0) {
+    const double* A = invs + j * D * D;
+    double y[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) y[a] = X[j * D + a] - X[a];
+    int q = 0;
+    bool done = false;
+#pragma unroll
+    for (int a = 0; a < D; ++a)
+#pragma unroll
+      for (int b = a; b < D; ++b, ++q)
+        if (k == q) {
+          v = (a == b) ? -0.5 * A[a * D + a] : -0.5 * (A[a * D + b] + A[b * D + a]);
+          done = true;
+        }
+    if (!done) {
+#pragma unroll
+      for (int a = 0; a < D; ++a, ++q)
+        if (k == q) {
+          double t = 0.0;
+#pragma unroll
+          for (int b = 0; b < D; ++b) t += (A[a * D + b] + A[b * D + a]) * y[b];
+          v = 0.5 * t;
+          done = true;
+        }
+    }
+    if (!done) {                      // constant slot
+      double qf = 0.0;
+#pragma unroll
+      for (int a = 0; a < D; ++a) {
+        double t = 0.0;
+#pragma unroll
+        for (int b = 0; b < D; ++b) t += A[a * D + b] * y[b];
+        qf += y[a] * t;
+      }
+      const double wj = w[j];
+      const double c = (wj > 0.0) ? log(wj) - lnorm[j] : -INFINITY;
+      v = c - 0.5 * qf;
+    }
+    v *= LOG2E_L;
+  }
+  psi[e] = v;
+}
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+// grid (candidate blocks of 4 waves x NT x 16, population chunks); each wave
+// keeps NT candidate tiles' features in registers and streams its chunk of
+// population tiles; writes the (max, sum) partial of each candidate.
+template <int D>
+__global__ __launch_bounds__(256) void local_mfma_kernel(
+    const double* __restrict__ x, int64_t M, const double* __restrict__ X,
+    const double* __restrict__ psi, int64_t ntiles, int64_t tiles_per_chunk,
+    double2* __restrict__ part) {
+  constexpr int KB = LocalFeat<D>::KB, NT = LocalFeat<D>::NT;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c0 = ((int64_t)blockIdx.x * 4 + wv) * (NT * 16);
+  double phi[NT][KB];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int64_t i = c0 + t * 16 + (lane & 15);
+    double y[D];
+#pragma unroll
+    for (int a = 0; a < D; ++a) y[a] = (i < M) ? x[i * D + a] - X[a] : 0.0;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) phi[t][kb] = local_phi<D>(y, 4 * kb + (lane >> 4));
+  }
+  double m[NT], l[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) { m[t] = -INFINITY; l[t] = 0.0; }
+  const int64_t p0 = (int64_t)blockIdx.y * tiles_per_chunk;
+  const int64_t p1 = (p0 + tiles_per_chunk < ntiles) ? p0 + tiles_per_chunk : ntiles;
+  for (int64_t pt = p0; pt < p1; ++pt) {
+    double a[KB];
+    const double* src = psi + pt * (KB * 64) + lane;
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb) a[kb] = src[kb * 64];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[kb], phi[t][kb], acc, 0, 0, 0);
+      const double mx = fmax(fmax(acc[0], acc[1]), fmax(acc[2], acc[3]));
+      if (mx > m[t]) {
+        l[t] *= (double)__builtin_amdgcn_exp2f((float)(m[t] - mx));
+        m[t] = mx;
+      }
+      if (m[t] > -INFINITY) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          l[t] += (double)__builtin_amdgcn_exp2f((float)(acc[r] - m[t]));
+      }
+    }
+  }
+  // merge the 4 row groups (lanes l, l^16, l^32, l^48 share a candidate)
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      const double mo = __shfl_xor(m[t], o, 64), lo = __shfl_xor(l[t], o, 64);
+      const double mn = fmax(m[t], mo);
+      if (mn > -INFINITY) {
+        l[t] = l[t] * (double)__builtin_amdgcn_exp2f((float)(m[t] - mn)) +
+               lo * (double)__builtin_amdgcn_exp2f((float)(mo - mn));
+        m[t] = mn;
+      }
+    }
+    const int64_t i = c0 + t * 16 + (lane & 15);
+    if (lane < 16 && i < M) part[(int64_t)blockIdx.y * M + i] = make_double2(m[t], l[t]);
+  }
+}
+
+// sum of the weights (np.average's denominator) in a fixed order
+__global__ __launch_bounds__(1024) void local_wsum_kernel(
+    const double* __restrict__ w, int64_t N, double* __restrict__ out) {
+  __shared__ double sh[16];
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < N; j += 1024) s += w[j];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < 16; ++k) t += sh[k];
+    out[0] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void local_combine_kernel(
+    const double2* __restrict__ part, int64_t M, int nchunks,
+    const double* __restrict__ wsum, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= M) return;
+  double m = -INFINITY;
+  for (int c = 0; c < nchunks; ++c) m = fmax(m, part[(int64_t)c * M + i].x);
+  double l = 0.0;
+  if (m > -INFINITY)
+    for (int c = 0; c < nchunks; ++c) {
+      const double2 p = part[(int64_t)c * M + i];
+      if (p.x > -INFINITY) l += p.y * exp2(p.x - m);
+    }
+  out[i] = (l > 0.0) ? LN2_L * (m + log2(l)) - log(wsum[0]) : -INFINITY;
+}
+
+template <int D>
+size_t pdf_workspace(int64_t M, int64_t N, int* nchunks_out) {
+  const int64_t ntiles = ceil_div(N, 16);
+  const int64_t cblocks = ceil_div(M > 0 ? M : 1, 4 * LocalFeat<D>::NT * 16);
+  // enough workgroups for 256 CUs x several waves, chunks of >= 64 tiles
+  int64_t nch = ceil_div(2048, cblocks);
+  nch = nch < 1 ? 1 : nch;
+  const int64_t maxch = ceil_div(ntiles, 64);
+  nch = nch > maxch ? maxch : nch;
+  nch = nch > 64 ? 64 : nch;
+  if (nchunks_out) *nchunks_out = (int)nch;
+  size_t off = 0;
+  size_only<double>(off, (size_t)ntiles * LocalFeat<D>::KB * 64);
+  size_only<double2>(off, (size_t)nch * (M > 0 ? M : 1));
+  size_only<double>(off, 1);
+  return off + 256;
+}
+
 template <int D>
 int launch_pdf(const double* x, int64_t M, const double* X, const double* w,
                int64_t N, const double* inv, const double* lnorm, double* out,
-               hipStream_t s) {
-  hipLaunchKernelGGL(local_pdf_kernel<D>, dim3((unsigned)ceil_div(M, 256)), dim3(256), 0, s,
-                     x, M, X, w, N, inv, lnorm, out);
+               void* ws, size_t ws_bytes, hipStream_t s) {
+  int nch = 1;
+  if (ws_bytes < pdf_workspace<D>(M, N, &nch))
+    return set_error(ABC_ERR_WORKSPACE, "local_logpdf: workspace too small");
+  const int64_t ntiles = ceil_div(N, 16);
+  constexpr int KB = LocalFeat<D>::KB, NT = LocalFeat<D>::NT;
+  Carver c(ws, ws_bytes);
+  double* psi = c.take<double>((size_t)ntiles * KB * 64);
+  double2* part = c.take<double2>((size_t)nch * M);
+  double* wsum = c.take<double>(1);
+  const int64_t npack = ntiles * KB * 64;
+  hipLaunchKernelGGL(local_pack_kernel<D>, dim3((unsigned)ceil_div(npack, 256)), dim3(256), 0,
+                     s, X, w, inv, lnorm, N, ntiles, psi);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(local_wsum_kernel, dim3(1), dim3(1024), 0, s, w, N, wsum);
+  ABC_LAUNCHED();
+  const int64_t tpc = ceil_div(ntiles, nch);
+  const int64_t cblocks = ceil_div(M, 4 * NT * 16);
+  hipLaunchKernelGGL(local_mfma_kernel<D>, dim3((unsigned)cblocks, (unsigned)nch), dim3(256),
+                     0, s, x, M, X, psi, ntiles, tpc, part);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(local_combine_kernel, dim3((unsigned)ceil_div(M, 256)), dim3(256), 0, s,
+                     part, M, nch, wsum, out);
   ABC_LAUNCHED();
   return ABC_OK;
 }
@@ -488,17 +666,26 @@ extern "C" int abc_local_fit(const double* X, const double* w, int64_t N,
   return set_error(ABC_ERR_UNSUPPORTED, "local_fit: d=%d", d);
 }
 
+extern "C" size_t abc_local_logpdf_workspace(int64_t M, int64_t N, int d) {
+  switch (d) {
+#define ABC_D(n) case n: return pdf_workspace<n>(M, N, nullptr);
+    ABC_D(1) ABC_D(2) ABC_D(3) ABC_D(4) ABC_D(5) ABC_D(6) ABC_D(7) ABC_D(8)
+#undef ABC_D
+  }
+  return 256;
+}
+
 extern "C" int abc_local_logpdf(const double* x, int64_t M, const double* X,
                                 const double* w, int64_t N, int d,
                                 const double* inv_covs,
                                 const double* log_norm, double* out,
-                                void* stream) {
+                                void* ws, size_t ws_bytes, void* stream) {
   ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= 8, "local_logpdf: bad M/N/d");
   if (M == 0) return ABC_OK;
-  ABC_CHECK_ARG(x && X && w && inv_covs && log_norm && out, "local_logpdf: null pointer");
+  ABC_CHECK_ARG(x && X && w && inv_covs && log_norm && out && ws, "local_logpdf: null pointer");
   hipStream_t s = as_stream(stream);
   switch (d) {
-#define ABC_D(n) case n: return launch_pdf<n>(x, M, X, w, N, inv_covs, log_norm, out, s);
+#define ABC_D(n) case n: return launch_pdf<n>(x, M, X, w, N, inv_covs, log_norm, out, ws, ws_bytes, s);
     ABC_D(1) ABC_D(2) ABC_D(3) ABC_D(4) ABC_D(5) ABC_D(6) ABC_D(7) ABC_D(8)
 #undef ABC_D
   }

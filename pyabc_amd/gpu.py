@@ -378,8 +378,9 @@ def local_logpdf(x, X, w, inv, lnorm, out=None):
     out = torch.empty(M, dtype=F64, device=x.device) if out is None else out
     if M == 0:
         return out
+    ws = workspace(nat.query("abc_local_logpdf_workspace", M, N, d), "local_pdf")
     nat.call("abc_local_logpdf", p(x), M, p(X), p(w), N, d, p(inv), p(lnorm),
-             p(out), stream_ptr())
+             p(out), p(ws), ws.numel(), stream_ptr())
     return out
 
 

@@ -196,6 +196,38 @@ def test_local_golden(dev, tag, kw):
     np.testing.assert_allclose(pdf, gg["pdf"], rtol=1e-6)
 
 
+@pytest.mark.parametrize("d,N,M,offset", [(5, 3001, 777, 0.0), (2, 17, 5, 40.0),
+                                            (8, 1000, 130, 5.0), (1, 64, 64, 0.0)])
+def test_local_logpdf_mfma_vs_oracle(dev, d, N, M, offset):
+    """fp64-MFMA quadratic-feature GEMM vs the fp64 oracle: ragged N / M
+    (tiles of 16 rows, 64-candidate waves), a population far from the origin
+    (centring), zero weights, a far-away candidate (pdf underflows to 0)."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(d * 1000 + N)
+    X = offset + rng.normal(size=(N, d)) * (1 + np.arange(d))
+    w = rng.random(N)
+    w[::7] = 0.0
+    w /= w.sum()
+    A = rng.normal(size=(N, d, d)) * 0.3
+    covs = np.einsum("nij,nkj->nik", A, A) + 0.2 * np.eye(d)
+    inv = np.linalg.inv(covs)
+    norm = np.sqrt((2 * np.pi) ** d * np.linalg.det(covs))
+    x = X[rng.integers(0, N, M)] + 0.5 * rng.normal(size=(M, d))
+    x[0] += 1e4
+    fit = dict(w=w, inv_covs=inv, normalization=norm)
+    ref = oracle.local_logpdf(x, X, fit)
+    got = gpu.local_logpdf(gpu.as_dev(x), gpu.as_dev(X), gpu.as_dev(w),
+                           gpu.as_dev(inv), gpu.as_dev(np.log(norm))).cpu().numpy()
+    # far candidate: the reference's pdf underflows to 0 (log -inf); the
+    # log-space sum keeps the exact log, whose exp is the same 0
+    assert ref[0] == -np.inf and got[0] < -1e5 and np.exp(got[0]) == 0.0
+    got, ref = got[1:], ref[1:]
+    fin = np.isfinite(ref)
+    assert np.array_equal(np.isfinite(got), fin)
+    # log density: absolute 1e-6 ~ relative 1e-6 of the density
+    np.testing.assert_allclose(got[fin], ref[fin], rtol=0, atol=2e-6)
+
+
 def test_pnorm_golden(dev):
     from pyabc_amd import gpu
     gg = g("pnorm.npz")

@@ -33,7 +33,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 HBM_PEAK = 8.0e12          # B/s (MI355X_MICROARCH.md)
-F64_VALU_PEAK = 78.6e12    # FLOP/s fp64 vector (spec)
+F64_VALU_PEAK = 78.6e12    # FLOP/s fp64 vector = fp64 matrix on MI355X (spec)
 
 
 def timed(fn, reps):
@@ -125,8 +125,17 @@ def c5(reps):
              extra={"note": "per (n, j) pair: 3d distance + masked moments"})
     x = t.propose_device(N)[0]
     ms = timed(lambda: t.logpdf_device(x), reps)
+    # the pair term as a GEMM over K0 = d(d+1)/2 + d + 1 quadratic features
+    # (abc_local.hip), priced against the fp64 MFMA peak
+    k0 = d * (d + 1) // 2 + d + 1
+    fl = N * N * 2 * k0
     emit("LocalTransition.pdf", "c5: 1e5 candidates x 1e5 particles", ms,
-         flop=N * N * (d * d + 2 * d + 4))
+         extra=dict(algorithmic_flop=fl, flop_per_pair=2 * k0,
+                    achieved_TFLOPs=round(fl / (ms * 1e-3) / 1e12, 3),
+                    bound="fp64 mfma", peak_TFLOPs=78.6,
+                    frac=round(fl / (ms * 1e-3) / F64_VALU_PEAK, 4),
+                    note="quadratic-feature GEMM on v_mfma_f64_16x16x4_f64 + "
+                         "exp2/sum; per-pair VALU form is d^2+2d+4 FLOP"))
 
 
 def sampler(reps):
