@@ -16,6 +16,7 @@ peak.  Inputs are synthetic, generated on the device or from seeded numpy.
             the default k = N/4 = 25000), density of 1e5 candidates
   sampler   propose + simulate + pnorm + accept at the c3 batch (4.6e6)
   cv        AdaptivePopulationSize.update on the c2 population (wall time)
+  e2e       whole-run generation times of c1, c4 (MAD / std), c5
   history   History file store: a c2 population written in pyABC's schema
   stochastic StochasticAcceptor stack at the c3 batch (4.6e6 candidates):
             IndependentNormalKernel values (S = 10), tempered accept step,
@@ -294,6 +295,92 @@ def history(reps):
          sec * 1e3, extra=dict(us_per_particle=round(sec / n * 1e6, 2),
                                reference_ms_per_particle=2.9,
                                file_MB=round(os.path.getsize(path) / 1e6, 1)))
+
+
+def e2e(reps):
+    """Whole runs of the BASELINE.json configs on one GPU (wall time per
+    generation from ABCSMC.generation_log; History in HBM):
+      c1  d=1, N=1000, 8 generations, MVN + PNorm + MedianEpsilon
+      c4  S=256 heterogeneous-scale model, N=2e5, AdaptivePNormDistance with
+          the MAD scale (and the default std scale), record_rejected on
+      c5  LocalTransition (k=50) as the transition of a 5-D run, N=1e5"""
+    import time
+    import torch
+    import pyabc_amd as pa
+    # c1
+    np.random.seed(0)
+    abc = pa.ABCSMC(pa.LinearGaussianModel(["x"], ["y"], src=[0], sigma=[0.5]),
+                    pa.Distribution(x=pa.RV("norm", 0, 1)), pa.PNormDistance(),
+                    population_size=1000, sampler=pa.BatchedGPUSampler(seed=1))
+    abc.new("sqlite://", {"y": 2.0})
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    abc.run(max_nr_populations=8)
+    torch.cuda.synchronize()
+    sec = time.perf_counter() - t0
+    emit("c1 end to end (8 generations)", "d=1, N=1000, MVN + PNorm + MedianEpsilon",
+         sec * 1e3, extra=dict(accepted_per_s=round(8000 / sec, 1),
+                               reference_accepted_per_s={"SingleCore": 229,
+                                                         "MulticoreEval(8)": 912}))
+    # c4
+    rng = np.random.default_rng(1234)
+    S = 256
+    a = rng.uniform(0.5, 2.0, S)
+    sig = 10.0 ** rng.uniform(-2, 2, S)
+    names = [f"th{k}" for k in range(4)]
+    keys = [f"s{k:03d}" for k in range(S)]
+    model = pa.LinearGaussianModel(names, keys, src=np.arange(S) % 4, a=a,
+                                   sigma=sig)
+    x0 = {k: float(a[i] * 0.5) for i, k in enumerate(keys)}
+    prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
+    for tag, scale in (("MAD", pa.distance.median_absolute_deviation),
+                       ("std", None)):
+        dist = (pa.AdaptivePNormDistance(scale_function=scale) if scale
+                else pa.AdaptivePNormDistance())
+        abc = pa.ABCSMC(model, prior, dist, population_size=200_000,
+                        sampler=pa.BatchedGPUSampler(seed=2))
+        abc.new("sqlite://", x0)
+        abc.run(max_nr_populations=5)
+        log = abc.generation_log
+        emit(f"c4 generation (AdaptivePNormDistance, {tag} scale)",
+             "S=256, N=2e5, record_rejected, MedianEpsilon",
+             1e3 * float(np.median([g["seconds"] for g in log[1:]])),
+             extra=dict(n_sim=[g["n_sim"] for g in log],
+                        accepted_per_s=round(2e5 / float(np.median(
+                            [g["seconds"] for g in log[1:]])), 1)))
+    # c5: LocalTransition in a 5-D run
+    d = 5
+    names = [f"p{k}" for k in range(d)]
+    keys = [f"y{k}" for k in range(d)]
+    abc = pa.ABCSMC(pa.LinearGaussianModel(names, keys, src=list(range(d)),
+                                           sigma=[0.5] * d),
+                    pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names}),
+                    pa.PNormDistance(), population_size=100_000,
+                    transitions=pa.LocalTransition(k=50, k_fraction=None),
+                    eps=pa.QuantileEpsilon(alpha=0.5),
+                    sampler=pa.BatchedGPUSampler(seed=3))
+    abc.new("sqlite://", {k: 1.0 for k in keys})
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    abc.run(max_nr_populations=4)
+    torch.cuda.synchronize()
+    sec = time.perf_counter() - t0
+    log = abc.generation_log
+    emit("c5 generation (LocalTransition k=50)", "d=5, N=1e5, PNorm, QuantileEpsilon(.5)",
+         1e3 * float(np.median([g["seconds"] for g in log[1:]])),
+         extra=dict(n_sim=[g["n_sim"] for g in log],
+                    run_total_ms=round(sec * 1e3, 1),
+                    note="run_total: calibration + 4 generations + 4 fits, synchronized"))
+    # the fit alone on this run's last population
+    cols = abc.history.get_population_device()
+    tr = pa.LocalTransition(k=50, k_fraction=None)
+    tr.fit_device(cols.theta, cols.weights, cols.param_names)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr.fit_device(cols.theta, cols.weights, cols.param_names)
+    torch.cuda.synchronize()
+    emit("c5 LocalTransition fit on the run's population", "N=1e5, d=5, k=50",
+         (time.perf_counter() - t0) * 1e3)
 
 
 def main():
