@@ -119,8 +119,11 @@ __device__ void cholesky(const double (&a)[D][D], double (&L)[D][D]) {
       for (int j = 0; j < D; ++j) L[i][j] = (i == j) ? sqrt(fabs(a[i][i])) : 0.0;
 }
 
+constexpr int SEL_CAP = 256;  // LDS list of the rank bucket
+
 // k-NN selection for PB particles per block: MSD radix select (8 passes of
-// 8 bits) of the rank nq-1 squared distance, every streamed row X[j] shared by
+// 8 bits; usually 2 passes + one collecting sweep) of the rank nq-1 squared
+// distance, every streamed row X[j] shared by
 // the block's PB particles (PB x less L2 traffic than one particle per block).
 // Writes, per particle, the key v* of rank nq-1, how many keys equal to v*
 // are inside the k+1 nearest (ties taken by index), and the rank-0 index (the
@@ -136,6 +139,9 @@ __global__ __launch_bounds__(256) void local_select_kernel(
   __shared__ double xn[PB][D];
   __shared__ unsigned long long s_prefix[PB], s_rank0[PB];
   __shared__ long long s_rank[PB];
+  __shared__ unsigned long long s_lkey[PB][SEL_CAP];
+  __shared__ long long s_lidx[PB][SEL_CAP];
+  __shared__ int s_lcnt[PB];
   const int tid = threadIdx.x;
   const int64_t n0 = (int64_t)blockIdx.x * PB;
   for (int e = tid; e < PB * D; e += 256) {
@@ -183,6 +189,54 @@ __global__ __launch_bounds__(256) void local_select_kernel(
       s_tot[tid] = hist[tid][b];  // last pass: number of keys equal to v*
     }
     __syncthreads();
+    if (pass >= 1 && pass < 7) {
+      // Once the bucket holding rank nq-1 is small (its size is s_tot; after
+      // 16 bits for small k, 24 bits for k = N/4), collect its (key, j) pairs
+      // in one more sweep and select the rank by (key, index) order in LDS:
+      // 3-4 sweeps instead of 8.  Larger buckets take another radix pass.
+      bool fits = true;
+#pragma unroll
+      for (int q = 0; q < PB; ++q) fits = fits && (s_tot[q] <= SEL_CAP);
+      if (fits) {
+        if (tid < PB) s_lcnt[tid] = 0;
+        __syncthreads();
+        for (int64_t j = tid; j < N; j += 256) {
+          double xj[D];
+#pragma unroll
+          for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
+#pragma unroll
+          for (int q = 0; q < PB; ++q) {
+            const unsigned long long key =
+                (unsigned long long)__double_as_longlong(dist2v<D>(xj, xr[q]));
+            if ((key >> (shift)) == s_prefix[q]) {
+              const int slot = atomicAdd(&s_lcnt[q], 1);
+              s_lkey[q][slot] = key;
+              s_lidx[q][slot] = j;
+            }
+          }
+        }
+        __syncthreads();
+        for (int q = 0; q < PB; ++q) {
+          const int cnt = s_lcnt[q];
+          const long long r = s_rank[q];
+          for (int e = tid; e < cnt; e += 256) {
+            const unsigned long long ke = s_lkey[q][e];
+            const long long je = s_lidx[q][e];
+            int less = 0;
+            for (int f = 0; f < cnt; ++f) {
+              const unsigned long long kf = s_lkey[q][f];
+              less += (kf < ke) || (kf == ke && s_lidx[q][f] < je);
+            }
+            if (less == r && n0 + q < N) {
+              sel_v[n0 + q] = ke;
+              sel_jcut[n0 + q] = je + 1;      // (key, j) <= (v*, j*) are in
+              sel_rank0[n0 + q] = (long long)s_rank0[q];
+            }
+          }
+        }
+        return;
+      }
+    }
   }
   // keys equal to v* enter in index order: ties_in = s_rank + 1 of s_tot.  If
   // not all of them do, find the index cutoff with an ordered sweep (rare:

@@ -196,6 +196,28 @@ def test_local_golden(dev, tag, kw):
     np.testing.assert_allclose(pdf, gg["pdf"], rtol=1e-6)
 
 
+@pytest.mark.parametrize("grid,N,d,k", [(None, 3000, 5, 50), (None, 3000, 5, 700),
+                                         (7, 2000, 3, 50), (2, 1500, 3, 40)])
+def test_local_fit_selection_paths_vs_oracle(dev, grid, N, d, k):
+    """k-NN selection: the LDS bucket path (small and large k) and the
+    radix-pass fallback (a {0,1}^3 grid: buckets of hundreds of exact ties,
+    taken by index) against the oracle's (distance, index) order."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(N + k)
+    if grid is None:
+        X = rng.normal(size=(N, d))
+    else:
+        X = rng.integers(0, grid, size=(N, d)).astype(float)
+    w = np.exp(0.3 * rng.standard_normal(N))
+    w /= w.sum()
+    ref = oracle.local_fit(X, w, k=k, k_fraction=None)
+    covs, inv, dets, chol, lnorm = gpu.local_fit(gpu.as_dev(X), gpu.as_dev(w), k,
+                                                 1.0, 1e-3)
+    np.testing.assert_allclose(covs.cpu().numpy(), ref["covs"], rtol=1e-9,
+                               atol=1e-12)
+    np.testing.assert_allclose(dets.cpu().numpy(), ref["dets"], rtol=1e-8)
+
+
 @pytest.mark.parametrize("d,N,M,offset", [(5, 3001, 777, 0.0), (2, 17, 5, 40.0),
                                             (8, 1000, 130, 5.0), (1, 64, 64, 0.0)])
 def test_local_logpdf_mfma_vs_oracle(dev, d, N, M, offset):
