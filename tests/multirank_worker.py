@@ -1,6 +1,7 @@
 """Worker for tests/test_gpu_multirank.py (not a test module).
 
-Runs a small c2-shaped ABC-SMC (d = 4, QuantileEpsilon, PNorm, MVN x3) with
+Runs a small c2-shaped ABC-SMC (d = 4, QuantileEpsilon, PNorm, MVN x3; or
+with MODE=stochastic the StochasticAcceptor / Temperature stack) with
 the batched GPU sampler and writes rank 0's final population, weights,
 epsilons and evaluation counts to ``$OUT``.  Started either as a single
 process or under torch.distributed.run (gloo backend, every rank on cuda:0:
@@ -30,10 +31,19 @@ def main():
     model = pa.LinearGaussianModel(names, keys, src=list(range(d)),
                                    sigma=[0.5] * d)
     prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
-    abc = pa.ABCSMC(model, prior, pa.PNormDistance(p=2),
+    if os.environ.get("MODE") == "stochastic":
+        # noise-model ABC: kernel values, stochastic accept, records of all
+        # candidates with both transition densities, temperature bisection
+        dist = pa.IndependentNormalKernel(var=[0.3] * d)
+        eps = pa.Temperature()
+        acceptor = pa.StochasticAcceptor()
+    else:
+        dist, eps, acceptor = (pa.PNormDistance(p=2),
+                               pa.QuantileEpsilon(alpha=0.5), None)
+    abc = pa.ABCSMC(model, prior, dist,
                     population_size=int(os.environ.get("POP", "20000")),
                     transitions=pa.MultivariateNormalTransition(),
-                    eps=pa.QuantileEpsilon(alpha=0.5),
+                    eps=eps, acceptor=acceptor,
                     sampler=pa.BatchedGPUSampler(seed=77, batch_size=None))
     abc.new("sqlite://", {k: 1.0 for k in keys})
     h = abc.run(max_nr_populations=int(os.environ.get("GENS", "4")))

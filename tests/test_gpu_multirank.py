@@ -28,9 +28,9 @@ def _port():
     return p
 
 
-def _run(tmp_path, nproc):
-    out = str(tmp_path / f"pop_{nproc}.npz")
-    env = dict(os.environ, OUT=out, POP="20000", GENS="4")
+def _run(tmp_path, nproc, mode="uniform"):
+    out = str(tmp_path / f"pop_{mode}_{nproc}.npz")
+    env = dict(os.environ, OUT=out, POP="20000", GENS="4", MODE=mode)
     if nproc == 1:
         cmd = [sys.executable, WORKER]
     else:
@@ -49,3 +49,13 @@ def test_sharded_generations_bit_identical(tmp_path):
         got = _run(tmp_path, nproc)
         for k in ("theta", "w", "eps", "samples"):
             np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{k} @ {nproc} ranks")
+
+
+def test_sharded_stochastic_generations_bit_identical(tmp_path):
+    """The StochasticAcceptor path on 1 vs 2 ranks: accept uniforms keyed by
+    the global index, records all-gathered back into global order, the
+    temperature objective reduced over identical records."""
+    ref = _run(tmp_path, 1, "stochastic")
+    got = _run(tmp_path, 2, "stochastic")
+    for k in ("theta", "w", "eps", "samples"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{k} @ 2 ranks")
