@@ -109,11 +109,15 @@ class BatchedGPUSampler(Sampler):
         RNG on rank 0 and broadcast).
     max_attempts: prior re-draws per candidate before giving up
         (the reference loops forever and warns at 1000, smc.py:658-662).
+    check_max_eval: stop a generation once ``max_eval`` candidates are
+        evaluated (sample not ok), like the reference samplers' flag of the
+        same name (singlecore.py:14-26); off by default, as there.
     """
 
     def __init__(self, batch_size=None, max_batch_size=1 << 22, seed=None,
-                 max_attempts=10000):
+                 max_attempts=10000, check_max_eval=False):
         super().__init__()
+        self.check_max_eval = check_max_eval
         self.batch_size = batch_size
         self.max_batch_size = max_batch_size
         self.seed = seed
@@ -164,7 +168,7 @@ class BatchedGPUSampler(Sampler):
         ok = True
         rounds = 0
         while n_acc < n:
-            if n_eval >= max_eval:
+            if self.check_max_eval and n_eval >= max_eval:
                 ok = False
                 break
             B = self._round_size(n - n_acc, ws)
