@@ -191,3 +191,33 @@ def test_wrong_output_sampler():
                            accepted=True)
     with pytest.raises(AssertionError):
         WrongOutputSampler().sample_until_n_accepted(5, simulate_one)
+
+
+# ---- two competing models (test_samplers.py:128-209) ----------------------------
+
+@pytest.mark.parametrize("n_sim", [1, 2])
+def test_two_competing_gaussians_multiple_population(n_sim):
+    """Model selection through the per-particle sampler (PNormDistance in
+    place of the reference's PercentileDistance): the run completes, model
+    probabilities are numbers, calibration used exactly nr_particles
+    evaluations."""
+    import pyabc_amd as pa
+    np.random.seed(3)
+    sigma = .5
+
+    def model(args):
+        return {"y": st.norm(args['x'], sigma).rvs()}
+    models = list(map(pa.SimpleModel, [model, model]))
+    priors = [pa.Distribution(x=pa.RV("norm", 0, sigma)),
+              pa.Distribution(x=pa.RV("norm", 1, sigma))]
+    pop_size = pa.ConstantPopulationSize(23, nr_samples_per_parameter=n_sim)
+    abc = pa.ABCSMC(models, priors, pa.PNormDistance(), pop_size,
+                    eps=pa.MedianEpsilon())
+    abc.new("sqlite://", {"y": 1})
+    history = abc.run(.05, max_nr_populations=2)
+    assert history.max_t == 1
+    mp = history.get_model_probabilities(history.max_t)
+    assert abs(float(mp.p.sum()) - 1.0) < 1e-12
+    pops = history.get_all_populations()
+    pre_evals = pops[pops['t'] == pa.History.PRE_TIME]['samples'].values
+    assert pre_evals == pop_size.nr_particles
