@@ -197,7 +197,7 @@ class BatchedGPUSampler(Sampler):
                     cnt_local = int(both[0])
                     pos_hint = int(both[1])
                 else:
-                    cnt_local = int(cnt.item())
+                    cnt_local = cnt        # gathered on the device, one host read
             counts = dd.allgather_counts(cnt_local, dev)
             keep = dd.cutoff(counts, n - n_acc)
             total_keep = int(keep.sum())
@@ -274,8 +274,7 @@ class BatchedGPUSampler(Sampler):
             return None
         out = gpu.torch.cat(pieces, 0) if len(pieces) > 1 else pieces[0]
         if ws > 1:
-            out = dd.allgather_rows(out.contiguous(), dev)
-            out = self.reorder(out, self.global_pieces(rec_keeps))
+            out = dd.allgather_rows_ordered([out.contiguous()], rec_keeps, dev)[0]
         return out.contiguous()
 
     @staticmethod
@@ -365,15 +364,15 @@ class BatchedGPUSampler(Sampler):
             w = gpu.importance_weights(lp, lt, spec.weight_scale,
                                        acc_w=None if accw is None else accw.contiguous())
         if ws > 1:
-            theta = dd.allgather_rows(theta, dev)
-            w = dd.allgather_rows(w, dev)
-            dist = dd.allgather_rows(dist, dev)
-            x = dd.allgather_rows(x, dev)
-            # rows arrive rank-major; restore global candidate-index order so
-            # the population (and every later draw keyed on it) is the same
-            # for any number of ranks
-            pieces = self.global_pieces(keeps)
-            theta, w, dist, x = (self.reorder(a, pieces) for a in (theta, w, dist, x))
+            # one packed all-gather; the rows come back in global
+            # candidate-index order so the population (and every later draw
+            # keyed on it) is the same for any number of ranks
+            parts = [theta, w, dist, x]
+            if len({a.dtype for a in parts}) == 1:
+                theta, w, dist, x = dd.allgather_rows_ordered(parts, keeps, dev)
+            else:
+                theta, w, dist, x = (dd.allgather_rows_ordered([a], keeps, dev)[0]
+                                     for a in parts)
         if theta.shape[0] == 0:
             return None
         return ColumnarParticles(theta.contiguous(), w.contiguous(),

@@ -9,9 +9,11 @@ is identical for 1, 2, 4 or 8 ranks.
 
 Collectives per generation (all RCCL over xGMI on the GPU box):
   * all_gather of per-round accept counts (R int64) -> global cutoff,
-  * all_gather of the accepted rows (theta, weight, distance, sum stats) ->
-    the next population, replicated on every rank,
-  * all_gather of the recorded sum stats when the distance adapts.
+  * ONE all_gather of the accepted rows (theta, weight, distance, sum stats
+    packed column-wise) -> the next population, replicated on every rank;
+    row counts come from the cutoff every rank already holds,
+  * one all_gather of the recorded rows when the distance adapts (or the
+    temperature needs every record).
 """
 import numpy as np
 
@@ -36,11 +38,17 @@ def rank_range(base, B, rank):
 
 
 def allgather_counts(count, device):
-    """int count per rank -> numpy array [world] (rank order)."""
+    """int count (or a 1-element device tensor, read by no one but the
+    collective) per rank -> numpy array [world] (rank order)."""
     rank, ws = world()
-    if ws == 1:
-        return np.array([int(count)])
-    t = torch.tensor([int(count)], dtype=torch.int64, device=device)
+    if isinstance(count, torch.Tensor):
+        t = count.reshape(1).to(torch.int64)
+        if ws == 1:
+            return t.cpu().numpy()
+    else:
+        if ws == 1:
+            return np.array([int(count)])
+        t = torch.tensor([int(count)], dtype=torch.int64, device=device)
     out = [torch.empty_like(t) for _ in range(ws)]
     dist.all_gather(out, t)
     return torch.cat(out).cpu().numpy()      # one host read
@@ -74,6 +82,64 @@ def allgather_rows(t, device):
     out = [torch.empty_like(pad) for _ in range(ws)]
     dist.all_gather(out, pad)
     return torch.cat([o[: int(k)] for o, k in zip(out, n)], dim=0)
+
+
+def allgather_rows_ordered(tensors, keeps, device):
+    """All-gather several per-rank row blocks in ONE collective and return
+    them in global candidate-index order.
+
+    tensors: list of same-dtype tensors [n_mine, c_i] or [n_mine] with the
+    same leading size (this rank's rows, round after round); keeps: [rounds x
+    ranks] rows each rank contributed per round -- known identically on every
+    rank from the cutoff, so no count exchange (and no host read) is needed.
+    The columns are packed into one [nmax x sum(c_i)] buffer (padded to the
+    largest rank), gathered with one all_gather, and the pieces (round-major,
+    then rank) are cut straight from the padded result: one collective and
+    one concatenation instead of a count gather + row gather + trim + reorder
+    per tensor.
+    """
+    rank, ws = world()
+    k = np.asarray(keeps, dtype=np.int64).reshape(len(keeps), -1)
+    if ws == 1:
+        return list(tensors)
+    per_rank = k.sum(0)
+    nmax = int(per_rank.max()) if per_rank.size else 0
+    if len({t.dtype for t in tensors}) != 1:
+        raise TypeError("allgather_rows_ordered packs one dtype per call")
+    cols = [t.reshape(t.shape[0], int(np.prod(t.shape[1:], dtype=np.int64)))
+            for t in tensors]
+    widths = [c.shape[1] for c in cols]
+    C = int(sum(widths))
+    n_mine = cols[0].shape[0]
+    if n_mine != int(per_rank[rank]):
+        raise AssertionError(
+            f"rank {rank}: {n_mine} rows, cutoff says {int(per_rank[rank])}")
+    pad = torch.zeros((max(nmax, 1), C), dtype=cols[0].dtype, device=cols[0].device)
+    c0 = 0
+    for c, wdt in zip(cols, widths):
+        if n_mine:
+            pad[:n_mine, c0:c0 + wdt] = c
+        c0 += wdt
+    out = torch.empty((ws * pad.shape[0], C), dtype=pad.dtype, device=pad.device)
+    if pad.is_cuda and dist.get_backend() == "gloo":
+        # gloo's flat all-gather is CPU-only; multi-rank tests on one GPU
+        dist.all_gather(list(out.chunk(ws)), pad)
+    else:
+        dist.all_gather_into_tensor(out, pad)
+    # piece (round r, rank q) starts at q * nmax + rows q kept in rounds < r
+    round_off = np.cumsum(k, axis=0) - k
+    pieces = [(int(q * pad.shape[0] + round_off[r, q]), int(k[r, q]))
+              for r in range(k.shape[0]) for q in range(ws) if k[r, q] > 0]
+    if not pieces:
+        full = out[:0]
+    else:
+        full = torch.cat([out[a:a + n] for a, n in pieces], 0)
+    res, c0 = [], 0
+    for t, wdt in zip(tensors, widths):
+        piece = full[:, c0:c0 + wdt]
+        res.append(piece.reshape((full.shape[0],) + tuple(t.shape[1:])).contiguous())
+        c0 += wdt
+    return res
 
 
 def broadcast_int(v, device):

@@ -177,9 +177,27 @@ def _collective_worker(rank, ws, port, out_dir):
         gathered = dd.allgather_rows(rows, dev)
         empty = dd.allgather_rows(torch.zeros((0, 2), dtype=torch.float64), dev)
         b = dd.broadcast_int(99 if rank == 0 else -1, dev)
+        # packed ordered gather: 3 rounds, rank 1 keeps nothing in round 1,
+        # rank 0 nothing in round 2; rows carry their global order number
+        keeps = np.array([[2, 1], [3, 0], [0, 2]])
+        order = np.arange(keeps.sum()).reshape(-1)
+        mine, o = [], 0
+        for r in range(keeps.shape[0]):
+            for q in range(ws):
+                if q == rank:
+                    mine.extend(order[o:o + keeps[r, q]])
+                o += keeps[r, q]
+        g = torch.tensor(mine, dtype=torch.float64)
+        th = torch.stack([g, -g], 1)
+        t2, w2, x2 = dd.allgather_rows_ordered(
+            [th, g + 0.5, torch.stack([g, g, g], 1).reshape(-1, 3, 1)], keeps, dev)
+        e1, e2 = dd.allgather_rows_ordered(
+            [torch.zeros((0, 2), dtype=torch.float64),
+             torch.zeros(0, dtype=torch.float64)], np.zeros((1, ws)), dev)
         np.savez(os.path.join(out_dir, f"c{rank}.npz"), counts=counts,
                  gathered=gathered.numpy(), empty=np.array(empty.shape),
-                 b=np.array(b))
+                 b=np.array(b), t2=t2.numpy(), w2=w2.numpy(), x2=x2.numpy(),
+                 e=np.array(list(e1.shape) + list(e2.shape)))
     finally:
         dist.destroy_process_group()
 
@@ -195,6 +213,12 @@ def test_collectives_two_ranks():
                                           [[0, 0], [1, 1], [1, 1]])
             np.testing.assert_array_equal(r["empty"], [0, 2])
             assert int(r["b"]) == 99
+            g = np.arange(8, dtype=np.float64)
+            np.testing.assert_array_equal(r["t2"], np.stack([g, -g], 1))
+            np.testing.assert_array_equal(r["w2"], g + 0.5)
+            assert r["x2"].shape == (8, 3, 1)
+            np.testing.assert_array_equal(r["x2"][:, :, 0], np.stack([g] * 3, 1))
+            np.testing.assert_array_equal(r["e"], [0, 2, 0])
 
 
 def test_cutoff_prefix():
