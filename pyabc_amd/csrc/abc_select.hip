@@ -15,8 +15,10 @@
 //   level l: one pass over the surviving set that compacts the keys of the
 //            picked bin into scratch (in place from level 2 on, chunk-wise
 //            behind a barrier) and histograms their next digit.
-// The surviving set shrinks by ~the bin count per level, so a column costs ~2
-// full reads per select.  For even R the (k+1)-th statistic is tracked along:
+// The surviving set shrinks by ~the bin count per level.  Long columns are
+// first bracketed by a sorted sample (see BR_MARG): one streaming pass keeps
+// the ~12% of keys around the wanted rank, so a select costs ~1 full read of
+// the column instead of ~2.  For even R the (k+1)-th statistic is tracked along:
 // while it falls in the same bin it survives with rank k; once it falls in
 // the next non-empty bin it is the minimum of that bin, taken in the next
 // pass (LDS 64-bit atomic min).  Results are exact and bitwise deterministic
@@ -60,14 +62,44 @@ __global__ __launch_bounds__(256) void transpose_keys_kernel(
   }
 }
 
+// sample bracketing: columns with R >= BR_MIN first take SMP evenly spaced
+// keys, sort them in LDS and keep only the keys between the sample order
+// statistics BR_MARG places either side of the wanted rank(s) (5.7 sigma of
+// the sample rank at the median).  One streaming pass counts the keys below
+// the window and compacts the window into scratch; the radix levels then run
+// on ~12% of the column.  When the rank is not inside the window (a sample
+// that misrepresents the column) the full radix select runs instead.
+constexpr int SMP = 2 * SEL_T;
+constexpr int BR_MARG = 128;
+constexpr int64_t BR_MIN = 4 * SMP;
+constexpr int BR_U = 8;  // keys in flight per thread in the bracket pass
+
 struct SelShared {
   uint32_t hist[SEL_BINS];
+  uint64_t smp[SMP];
   uint32_t wsum[SEL_T / 64];
   unsigned long long vmin;
+  unsigned long long below;
+  uint64_t lo, hi;
   uint32_t cnt;
   int b1, b2;
   int64_t below1;
 };
+
+// ascending bitonic sort of sh.smp (SMP = 2 x blockDim keys)
+__device__ void sort_sample(SelShared& sh) {
+  const int t = threadIdx.x;
+  for (int size = 2; size <= SMP; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int i = 2 * t - (t & (stride - 1));
+      const int j = i + stride;
+      const bool asc = (i & size) == 0;
+      const uint64_t a = sh.smp[i], b = sh.smp[j];
+      if ((a > b) == asc) { sh.smp[i] = b; sh.smp[j] = a; }
+      __syncthreads();
+    }
+  }
+}
 
 // exclusive-prefix search over the histogram: bin holding rank k (and k+1)
 __device__ void find_bins(SelShared& sh, int64_t k, bool want2) {
@@ -118,17 +150,90 @@ __global__ __launch_bounds__(SEL_T) void col_select_kernel(
   bool want2 = (R & 1) == 0;     // still tracking rank k+1 inside the set
   bool have2 = false;            // rank k+1 resolved as a bin minimum
   uint64_t v2 = 0;
-  // ---- level 0: histogram of the top digit over the whole column
+  int64_t n = R;
+  bool in_scratch = false;
+  const int lane = t & 63;
+  if (R >= BR_MIN) {
+    // ---- sample bracketing (see BR_MARG): one pass instead of two
+    for (int q = t; q < SMP; q += SEL_T)
+      sh.smp[q] = keyof(col[((2 * (int64_t)q + 1) * R) / (2 * SMP)]);
+    if (t == 0) { sh.cnt = 0; sh.below = 0; }
+    __syncthreads();
+    sort_sample(sh);
+    if (t == 0) {
+      const int64_t j1 = (k * SMP) / R - BR_MARG;
+      const int64_t j2 = ((k + (want2 ? 1 : 0)) * SMP) / R + BR_MARG;
+      sh.lo = j1 < 0 ? 0ull : sh.smp[j1];
+      sh.hi = j2 >= SMP ? ~0ull : sh.smp[j2];
+    }
+    __syncthreads();
+    const uint64_t lo = sh.lo, hi = sh.hi;
+    uint64_t below = 0;
+    for (int64_t base = 0; base < R; base += (int64_t)SEL_T * BR_U) {
+      uint64_t kv[BR_U];
+      bool keep[BR_U];
+      uint64_t bal[BR_U];
+#pragma unroll
+      for (int u = 0; u < BR_U; ++u) {
+        const int64_t i = base + (int64_t)u * SEL_T + t;
+        kv[u] = i < R ? col[i] : 0;
+      }
+      uint32_t tot = 0;
+#pragma unroll
+      for (int u = 0; u < BR_U; ++u) {
+        const int64_t i = base + (int64_t)u * SEL_T + t;
+        const uint64_t key = keyof(kv[u]);
+        kv[u] = key;
+        below += (i < R && key < lo) ? 1 : 0;
+        keep[u] = i < R && key >= lo && key <= hi;
+        bal[u] = __ballot(keep[u]);
+        tot += (uint32_t)__popcll(bal[u]);
+      }
+      uint32_t wpos = 0;
+      if (lane == 0 && tot) wpos = atomicAdd(&sh.cnt, tot);
+      wpos = __shfl(wpos, 0, 64);
+      const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+      for (int u = 0; u < BR_U; ++u) {
+        if (keep[u]) sc[wpos + __popcll(bal[u] & lt)] = kv[u];
+        wpos += (uint32_t)__popcll(bal[u]);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) below += __shfl_down(below, o, 64);
+    if (lane == 0 && below) atomicAdd(&sh.below, (unsigned long long)below);
+    __syncthreads();
+    const int64_t nin = sh.cnt, bel = (int64_t)sh.below;
+    if (bel <= k && k + (want2 ? 1 : 0) < bel + nin) {  // uniform
+      k -= bel;
+      n = nin;
+      in_scratch = true;
+    }
+    // else: the full select below, from the column
+  }
+  // ---- level 0: histogram of the top digit over the (bracketed) set
   for (int i = t; i < SEL_BINS; i += SEL_T) sh.hist[i] = 0;
   if (t == 0) sh.b2 = -1;
   __syncthreads();
   int shift = 64 - SEL_BITS;
-  for (int64_t i = t; i < R; i += SEL_T)
-    atomicAdd(&sh.hist[(keyof(col[i]) >> shift) & (SEL_BINS - 1)], 1u);
+  for (int64_t base = 0; base < n; base += (int64_t)SEL_T * BR_U) {
+    uint64_t kv[BR_U];
+#pragma unroll
+    for (int u = 0; u < BR_U; ++u) {
+      const int64_t i = base + (int64_t)u * SEL_T + t;
+      kv[u] = i < n ? (in_scratch ? sc[i] : col[i]) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < BR_U; ++u) {
+      const int64_t i = base + (int64_t)u * SEL_T + t;
+      if (i < n) {
+        const uint64_t key = in_scratch ? kv[u] : keyof(kv[u]);
+        atomicAdd(&sh.hist[(key >> shift) & (SEL_BINS - 1)], 1u);
+      }
+    }
+  }
   __syncthreads();
   find_bins(sh, k, want2);
-  int64_t n = R;
-  bool in_scratch = false;
   uint64_t prefix = 0, pmask = 0;
   while (true) {
     const int b1 = sh.b1, b2 = sh.b2;

@@ -329,6 +329,11 @@ def test_column_mad_select_edges(dev):
         X[:, 6] = np.exp(rng.standard_normal(R) * 20)    # many exponents
         X[:, 7] = 1.0 + rng.integers(0, 3, R) * 2.0 ** -52  # last-bit ties
         X[:, 8] = -np.abs(rng.standard_normal(R))
+        if R >= 8192:
+            # sample-bracket misses: huge values exactly at the kernel's
+            # sample rows ((2q+1)R / 4096, q < 2048) -> full radix fallback
+            X = np.concatenate([X, rng.standard_normal((R, 1))], 1)
+            X[(2 * np.arange(2048) + 1) * R // 4096, 9] = 1e9
         mad = gpu.column_mad(T(X)).cpu().numpy()
         np.testing.assert_array_equal(mad, oracle.median_absolute_deviation(X),
                                       err_msg=f"R={R}")
