@@ -120,6 +120,63 @@ __device__ void cholesky(const double (&a)[D][D], double (&L)[D][D]) {
 }
 
 constexpr int SEL_CAP = 256;  // LDS list of the rank bucket
+constexpr int BR_SK = 512;    // k-NN sample rows per block (sample bracketing)
+constexpr int BR_NB = 520;    // window histogram bins (offsets 0..512 used)
+constexpr int BR_PER = (BR_NB + 31) / 32;
+
+// Collect the (key, index) pairs of each particle's rank bucket -- keys with
+// (key >> s_sh[p]) == s_prefix[p] -- into LDS in one sweep and select rank
+// s_rank[p] by (key, index) order.  Writes v*, the index cutoff of the ties
+// and the rank-0 index.
+template <int D, int PB>
+__device__ __forceinline__ void collect_select(
+    const double* __restrict__ X, int64_t N, int64_t n0, const double (&xr)[PB][D],
+    const int* s_sh, const unsigned long long* s_prefix, const long long* s_rank,
+    const unsigned long long* s_rank0, unsigned long long (*s_lkey)[2 * SEL_CAP],
+    int* s_lcnt, unsigned long long* __restrict__ sel_v,
+    long long* __restrict__ sel_jcut, long long* __restrict__ sel_rank0) {
+  const int tid = threadIdx.x;
+  if (tid < PB) s_lcnt[tid] = 0;
+  __syncthreads();
+  int sh[PB];
+  unsigned long long pre[PB];
+#pragma unroll
+  for (int q = 0; q < PB; ++q) { sh[q] = s_sh[q]; pre[q] = s_prefix[q]; }
+  for (int64_t j = tid; j < N; j += 256) {
+    double xj[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const unsigned long long key =
+          (unsigned long long)__double_as_longlong(dist2v<D>(xj, xr[q]));
+      if ((key >> sh[q]) == pre[q]) {
+        const int slot = atomicAdd(&s_lcnt[q], 1);
+        s_lkey[q][slot] = key;
+        s_lkey[q][SEL_CAP + slot] = (unsigned long long)j;
+      }
+    }
+  }
+  __syncthreads();
+  for (int q = 0; q < PB; ++q) {
+    const int cnt = s_lcnt[q];
+    const long long r = s_rank[q];
+    for (int e = tid; e < cnt; e += 256) {
+      const unsigned long long ke = s_lkey[q][e];
+      const long long je = (long long)s_lkey[q][SEL_CAP + e];
+      int less = 0;
+      for (int f = 0; f < cnt; ++f) {
+        const unsigned long long kf = s_lkey[q][f];
+        less += (kf < ke) || (kf == ke && (long long)s_lkey[q][SEL_CAP + f] < je);
+      }
+      if (less == r && n0 + q < N) {
+        sel_v[n0 + q] = ke;
+        sel_jcut[n0 + q] = je + 1;      // (key, j) <= (v*, j*) are in
+        sel_rank0[n0 + q] = (long long)s_rank0[q];
+      }
+    }
+  }
+}
 
 // k-NN selection for PB particles per block: MSD radix select (8 passes of
 // 8 bits; usually 2 passes + one collecting sweep) of the rank nq-1 squared
@@ -133,15 +190,20 @@ __global__ __launch_bounds__(256) void local_select_kernel(
     const double* __restrict__ X, int64_t N, int64_t nq,
     unsigned long long* __restrict__ sel_v, long long* __restrict__ sel_jcut,
     long long* __restrict__ sel_rank0) {
-  __shared__ unsigned hist[PB][256];
+  __shared__ unsigned hist[PB][BR_NB];
   __shared__ long long s_tot[PB];
   __shared__ int s_cnt[4];
   __shared__ double xn[PB][D];
   __shared__ unsigned long long s_prefix[PB], s_rank0[PB];
   __shared__ long long s_rank[PB];
-  __shared__ unsigned long long s_lkey[PB][SEL_CAP];
-  __shared__ long long s_lidx[PB][SEL_CAP];
+  // the rank bucket's (key, index) list; before the passes the same LDS holds
+  // the sorted distance sample of each particle
+  __shared__ unsigned long long s_buf[PB][2 * SEL_CAP];
   __shared__ int s_lcnt[PB];
+  __shared__ int s_sh[PB];
+  __shared__ unsigned long long s_below[PB];
+  __shared__ int s_fail;
+  unsigned long long (*s_lkey)[2 * SEL_CAP] = s_buf;
   const int tid = threadIdx.x;
   const int64_t n0 = (int64_t)blockIdx.x * PB;
   for (int e = tid; e < PB * D; e += 256) {
@@ -149,16 +211,137 @@ __global__ __launch_bounds__(256) void local_select_kernel(
     const int64_t n = n0 + p < N ? n0 + p : N - 1;  // pad: duplicate, not written
     xn[p][q] = X[n * D + q];
   }
-  if (tid < PB) { s_prefix[tid] = 0ull; s_rank[tid] = nq - 1; s_rank0[tid] = (unsigned long long)N; }
+  if (tid < PB) { s_rank0[tid] = (unsigned long long)N; }
+  if (tid == 0) s_fail = 0;
   __syncthreads();
   double xr[PB][D];  // the block's particles in registers (no LDS reads per pair)
 #pragma unroll
   for (int p = 0; p < PB; ++p)
 #pragma unroll
     for (int q = 0; q < D; ++q) xr[p][q] = xn[p][q];
+  if (N >= 4 * BR_SK) {
+    // ---- sample bracketing: BR_SK evenly spaced rows give each particle a
+    // sorted distance sample; the sample order statistics BR_M places either
+    // side of the rank bound a key window [lo, hi].  ONE sweep then counts the
+    // keys below the window and histograms the window on the ~9 bits below
+    // the top bit of hi - lo (BR_NB bins, offsets from lo); the bin holding
+    // the rank is collected in a second sweep and selected in LDS.  Two
+    // sweeps instead of 3-4 radix sweeps; the histogram atomics see only the
+    // window.  If the rank is outside the window or its bin overflows the
+    // LDS list, the full radix select below runs instead.
+    for (int q = tid; q < BR_SK; q += 256) {
+      const int64_t j = ((2 * (int64_t)q + 1) * N) / (2 * BR_SK);
+      double xj[D];
+#pragma unroll
+      for (int c = 0; c < D; ++c) xj[c] = X[j * D + c];
+#pragma unroll
+      for (int p = 0; p < PB; ++p)
+        s_buf[p][q] = (unsigned long long)__double_as_longlong(dist2v<D>(xj, xr[p]));
+    }
+    __syncthreads();
+    for (int size = 2; size <= BR_SK; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int e = tid; e < PB * (BR_SK / 2); e += 256) {
+          const int p = e / (BR_SK / 2), t = e % (BR_SK / 2);
+          const int i = 2 * t - (t & (stride - 1)), j = i + stride;
+          const bool asc = (i & size) == 0;
+          const unsigned long long a = s_buf[p][i], b = s_buf[p][j];
+          if ((a > b) == asc) { s_buf[p][i] = b; s_buf[p][j] = a; }
+        }
+        __syncthreads();
+      }
+    const double pf = (double)(nq - 1) / (double)N;
+    const int64_t mrg = 8 + (int64_t)(5.0 * sqrt(BR_SK * pf * (1.0 - pf)));
+    const int64_t jk = ((nq - 1) * BR_SK) / N;
+    unsigned long long lo_r[PB];
+    int sh_r[PB];
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      // a rank below the sample's reach (small k): the window starts 2^-12 x
+      // the smallest sampled distance (squared distances are >= 0, so key
+      // minus 12 << 52 divides by 4096), not at 0 -- starting at 0 would
+      // bin the window by exponent only and overflow the bucket list
+      const unsigned long long s0 = s_buf[p][0];
+      const unsigned long long lo =
+          jk - mrg >= 0 ? s_buf[p][jk - mrg]
+                        : (s0 > (12ull << 52) ? s0 - (12ull << 52) : 0ull);
+      const unsigned long long hi = jk + mrg >= BR_SK ? ~0ull : s_buf[p][jk + mrg];
+      const int L = hi > lo ? 64 - __builtin_clzll(hi - lo) : 0;
+      sh_r[p] = L > 9 ? L - 9 : 0;   // (hi >> sh) - (lo >> sh) <= 512 < BR_NB
+      lo_r[p] = lo >> sh_r[p];
+    }
+    __syncthreads();  // sample reads done; s_buf becomes the bucket list
+    for (int e = tid; e < PB * BR_NB; e += 256) (&hist[0][0])[e] = 0u;
+    if (tid < PB) { s_below[tid] = 0ull; s_sh[tid] = sh_r[tid]; }
+    __syncthreads();
+    unsigned below[PB];
+#pragma unroll
+    for (int p = 0; p < PB; ++p) below[p] = 0u;
+    for (int64_t j = tid; j < N; j += 256) {
+      double xj[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
+#pragma unroll
+      for (int p = 0; p < PB; ++p) {
+        const unsigned long long key =
+            (unsigned long long)__double_as_longlong(dist2v<D>(xj, xr[p]));
+        const unsigned long long top = key >> sh_r[p];
+        if (top < lo_r[p]) ++below[p];
+        else if (top - lo_r[p] < (unsigned long long)BR_NB)
+          atomicAdd(&hist[p][top - lo_r[p]], 1u);
+        if (key == 0ull) atomicMin(&s_rank0[p], (unsigned long long)j);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      unsigned v = below[p];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+      if ((tid & 63) == 0 && v) atomicAdd(&s_below[p], (unsigned long long)v);
+    }
+    __syncthreads();
+    {
+      // bin holding the rank: 32 lanes per particle, BR_PER bins per lane
+      const int p = tid >> 5, l = tid & 31;
+      if (p < PB) {
+        const long long r = nq - 1 - (long long)s_below[p];
+        long long v = 0;
+        for (int b = l * BR_PER; b < (l + 1) * BR_PER && b < BR_NB; ++b) v += hist[p][b];
+        long long inc = v;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          const long long u = __shfl_up(inc, o, 32);
+          if (l >= o) inc += u;
+        }
+        const long long tot = __shfl(inc, 31, 32);
+        if (r < 0 || r >= tot) {
+          if (l == 0) s_fail = 1;
+        } else if (r >= inc - v && r < inc) {
+          long long run = inc - v;
+          int b = l * BR_PER;
+          for (; b < BR_NB; ++b) {
+            if (r < run + (long long)hist[p][b]) break;
+            run += hist[p][b];
+          }
+          if (hist[p][b] > (unsigned)SEL_CAP) s_fail = 1;
+          s_prefix[p] = lo_r[p] + (unsigned long long)b;
+          s_rank[p] = r - run;
+        }
+      }
+    }
+    __syncthreads();
+    if (!s_fail) {
+      collect_select<D, PB>(X, N, n0, xr, s_sh, s_prefix, s_rank, s_rank0, s_lkey,
+                            s_lcnt, sel_v, sel_jcut, sel_rank0);
+      return;
+    }
+    __syncthreads();
+  }
+  if (tid < PB) { s_prefix[tid] = 0ull; s_rank[tid] = nq - 1; s_rank0[tid] = (unsigned long long)N; }
+  __syncthreads();
   for (int pass = 0; pass < 8; ++pass) {
     const int shift = 56 - 8 * pass;
-    for (int e = tid; e < PB * 256; e += 256) (&hist[0][0])[e] = 0u;
+    for (int e = tid; e < PB * BR_NB; e += 256) (&hist[0][0])[e] = 0u;
     unsigned long long pre[PB];
 #pragma unroll
     for (int p = 0; p < PB; ++p) pre[p] = s_prefix[p];
@@ -198,42 +381,10 @@ __global__ __launch_bounds__(256) void local_select_kernel(
 #pragma unroll
       for (int q = 0; q < PB; ++q) fits = fits && (s_tot[q] <= SEL_CAP);
       if (fits) {
-        if (tid < PB) s_lcnt[tid] = 0;
+        if (tid < PB) s_sh[tid] = shift;
         __syncthreads();
-        for (int64_t j = tid; j < N; j += 256) {
-          double xj[D];
-#pragma unroll
-          for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
-#pragma unroll
-          for (int q = 0; q < PB; ++q) {
-            const unsigned long long key =
-                (unsigned long long)__double_as_longlong(dist2v<D>(xj, xr[q]));
-            if ((key >> (shift)) == s_prefix[q]) {
-              const int slot = atomicAdd(&s_lcnt[q], 1);
-              s_lkey[q][slot] = key;
-              s_lidx[q][slot] = j;
-            }
-          }
-        }
-        __syncthreads();
-        for (int q = 0; q < PB; ++q) {
-          const int cnt = s_lcnt[q];
-          const long long r = s_rank[q];
-          for (int e = tid; e < cnt; e += 256) {
-            const unsigned long long ke = s_lkey[q][e];
-            const long long je = s_lidx[q][e];
-            int less = 0;
-            for (int f = 0; f < cnt; ++f) {
-              const unsigned long long kf = s_lkey[q][f];
-              less += (kf < ke) || (kf == ke && s_lidx[q][f] < je);
-            }
-            if (less == r && n0 + q < N) {
-              sel_v[n0 + q] = ke;
-              sel_jcut[n0 + q] = je + 1;      // (key, j) <= (v*, j*) are in
-              sel_rank0[n0 + q] = (long long)s_rank0[q];
-            }
-          }
-        }
+        collect_select<D, PB>(X, N, n0, xr, s_sh, s_prefix, s_rank, s_rank0, s_lkey,
+                              s_lcnt, sel_v, sel_jcut, sel_rank0);
         return;
       }
     }

@@ -197,10 +197,12 @@ def test_local_golden(dev, tag, kw):
 
 
 @pytest.mark.parametrize("grid,N,d,k", [(None, 3000, 5, 50), (None, 3000, 5, 700),
-                                         (7, 2000, 3, 50), (2, 1500, 3, 40)])
+                                         (7, 2000, 3, 50), (2, 1500, 3, 40),
+                                         (None, 12000, 5, 3000), (None, 4096, 2, 10),
+                                         (3, 5000, 4, 200)])
 def test_local_fit_selection_paths_vs_oracle(dev, grid, N, d, k):
-    """k-NN selection: the LDS bucket path (small and large k) and the
-    radix-pass fallback (a {0,1}^3 grid: buckets of hundreds of exact ties,
+    """k-NN selection: the sample-bracketed path (N >= 2048), the LDS bucket
+    path (small and large k) and the radix-pass fallback (a {0,1}^3 grid: buckets of hundreds of exact ties,
     taken by index) against the oracle's (distance, index) order."""
     from pyabc_amd import gpu
     rng = np.random.default_rng(N + k)
