@@ -7,15 +7,16 @@
 //   rvs   :141-145 j ~ Cat(w); theta ~ N(X_j, cov_j)  (abc_local_propose in
 //                  abc_sampler.hip uses the Cholesky factors written here)
 //
-// fit: one 256-thread workgroup per particle n.  The k+1 nearest particles in
-// (squared distance, index) order are found by an exact MSD radix select on
-// the fp64 bits of the squared distances (8 passes of 8 bits, LDS
-// histograms); a final ordered pass accumulates the weighted moments of the
-// neighbour offsets (ties at the k-th distance taken by index, rank 0
-// dropped like the reference's indices[n, 1:]).  Thread 0 then applies the
-// reference's fix-ups (diag(|X[0]|) for an all-zero covariance, scaling,
-// "while det <= 0: cov += EPS I") and writes cov, inverse (Gauss-Jordan with
-// partial pivoting), det (LU), Cholesky and log normalisation.
+// fit: workgroups of 8 particles find the k+1 nearest particles in
+// (squared distance, index) order by an exact select on the fp64 bits of the
+// squared distances (sample-bracketed window, MSD radix passes as fallback,
+// the rank's bucket selected in LDS); then one particle per lane accumulates
+// the weighted moments of the neighbour offsets over wave-uniform rows (ties
+// at the k-th distance taken by index, rank 0 dropped like the reference's
+// indices[n, 1:]), and a finishing kernel applies the reference's fix-ups
+// (diag(|X[0]|) for an all-zero covariance, scaling, "while det <= 0: cov +=
+// EPS I") and writes cov, inverse (Gauss-Jordan with partial pivoting), det
+// (LU), Cholesky and log normalisation.
 #include "abc_common.h"
 
 namespace abc {
@@ -428,87 +429,87 @@ __global__ __launch_bounds__(256) void local_select_kernel(
   }
 }
 
-// Covariance of the selected neighbours of PB particles per block: the rows
-// are streamed once per block, neighbour membership is order free
-// (key < v*, or key == v* and j < jcut; the rank-0 index excluded), the
-// moments (sum a, sum a^2, sum a d, upper triangle of sum a d d^T with a the
-// neighbour's weight) sit in registers, blocks reduce in a fixed order.  Thread
-// p < PB then applies the reference's fix-ups and factorisations.
-template <int D, int PB>
-__global__ __launch_bounds__(256) void local_fit_kernel(
+// Covariance of the selected neighbours, one particle per lane: every row
+// X[j] is wave-uniform (scalar loads, shared by the wave's 64 particles), the
+// per-pair work is the distance, the membership test (key < v*, or key == v*
+// and j < jcut; the rank-0 index excluded) and, for members, the moments
+// (sum a, sum a^2, sum a d, upper triangle of sum a d d^T with a the
+// neighbour's weight) in the lane's registers.  The rows are split into RS
+// chunks (grid.y) for occupancy; the partial moments go to part[RS][NM][N]
+// and local_finish_kernel adds them in chunk order (deterministic).
+template <int D>
+__global__ __launch_bounds__(256) void local_moments_kernel(
     const double* __restrict__ X, const double* __restrict__ w, int64_t N,
-    int64_t nq, double scaling, double eps,
     const unsigned long long* __restrict__ sel_v,
     const long long* __restrict__ sel_jcut,
-    const long long* __restrict__ sel_rank0, double* __restrict__ covs,
+    const long long* __restrict__ sel_rank0, double* __restrict__ part) {
+  constexpr int NM = 2 + D + D * (D + 1) / 2;
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t ne = n < N ? n : N - 1;
+  const int RS = gridDim.y;
+  const int64_t j0 = (N * (int64_t)blockIdx.y) / RS, j1 = (N * ((int64_t)blockIdx.y + 1)) / RS;
+  double xp[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) xp[q] = X[ne * D + q];
+  const unsigned long long vs = sel_v[ne];
+  const long long jcut = sel_jcut[ne], r0 = sel_rank0[ne];
+  double m[NM];
+#pragma unroll
+  for (int t = 0; t < NM; ++t) m[t] = 0.0;
+  auto row = [&](int64_t j, const double (&xj)[D]) {
+    const unsigned long long key = (unsigned long long)__double_as_longlong(dist2v<D>(xj, xp));
+    if ((key < vs || (key == vs && j < jcut)) && j != r0) {
+      const double lw = w[j];
+      double dj[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) dj[q] = xj[q] - xp[q];
+      m[0] += lw;
+      m[1] += lw * lw;
+      int c = 2 + D;
+#pragma unroll
+      for (int a = 0; a < D; ++a) {
+        m[2 + a] += lw * dj[a];
+#pragma unroll
+        for (int b = a; b < D; ++b) m[c++] += lw * dj[a] * dj[b];
+      }
+    }
+  };
+  // 8 rows per step: their (scalar) loads issue together, then the pairs
+  constexpr int RU = 8;
+  int64_t j = j0;
+  for (; j + RU <= j1; j += RU) {
+    double xa[RU][D];
+#pragma unroll
+    for (int u = 0; u < RU; ++u)
+#pragma unroll
+      for (int q = 0; q < D; ++q) xa[u][q] = X[(j + u) * D + q];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) row(j + u, xa[u]);
+  }
+  for (; j < j1; ++j) {
+    double xj[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
+    row(j, xj);
+  }
+  if (n < N) {
+#pragma unroll
+    for (int t = 0; t < NM; ++t) part[((int64_t)blockIdx.y * NM + t) * N + n] = m[t];
+  }
+}
+
+// Per particle: the moments (partials added in chunk order), then the
+// reference's fix-ups and factorisations (local_transition.py:112-139).
+template <int D>
+__global__ __launch_bounds__(256) void local_finish_kernel(
+    const double* __restrict__ X, int64_t N, int64_t nq, double scaling, double eps,
+    const double* __restrict__ part, int RS, double* __restrict__ covs,
     double* __restrict__ invs, double* __restrict__ dets,
     double* __restrict__ chol, double* __restrict__ lnorm) {
   constexpr int NT = D * (D + 1) / 2;
   constexpr int NM = 2 + D + NT;
-  __shared__ double red[PB][NM][4];
-  __shared__ double xn[PB][D];
-  const int tid = threadIdx.x;
-  const int64_t n0 = (int64_t)blockIdx.x * PB;
-  for (int e = tid; e < PB * D; e += 256) {
-    const int p = e / D, q = e % D;
-    const int64_t n = n0 + p < N ? n0 + p : N - 1;
-    xn[p][q] = X[n * D + q];
-  }
-  __syncthreads();
-  unsigned long long vs[PB];
-  long long jcut[PB], r0[PB];
-#pragma unroll
-  for (int p = 0; p < PB; ++p) {
-    const int64_t n = n0 + p < N ? n0 + p : N - 1;
-    vs[p] = N > 1 ? sel_v[n] : 0ull;
-    jcut[p] = N > 1 ? sel_jcut[n] : 0;
-    r0[p] = N > 1 ? sel_rank0[n] : -1;
-  }
-  double m[PB][NM];
-#pragma unroll
-  for (int p = 0; p < PB; ++p)
-#pragma unroll
-    for (int t = 0; t < NM; ++t) m[p][t] = 0.0;
-  if (N > 1) {
-    for (int64_t j = tid; j < N; j += 256) {
-      double xj[D];
-#pragma unroll
-      for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
-      const double lw = w[j];
-#pragma unroll
-      for (int p = 0; p < PB; ++p) {
-        const unsigned long long key =
-            (unsigned long long)__double_as_longlong(dist2v<D>(xj, xn[p]));
-        const bool inc = (key < vs[p] || (key == vs[p] && j < jcut[p])) && j != r0[p];
-        if (inc) {
-          double dj[D];
-#pragma unroll
-          for (int q = 0; q < D; ++q) dj[q] = xj[q] - xn[p][q];
-          m[p][0] += lw;
-          m[p][1] += lw * lw;
-          int c = 2 + D;
-#pragma unroll
-          for (int a = 0; a < D; ++a) {
-            m[p][2 + a] += lw * dj[a];
-#pragma unroll
-            for (int b = a; b < D; ++b) m[p][c++] += lw * dj[a] * dj[b];
-          }
-        }
-      }
-    }
-  }
-  // deterministic block reduction: wave shuffle, then the 4 waves in order
-#pragma unroll
-  for (int p = 0; p < PB; ++p)
-#pragma unroll
-    for (int t = 0; t < NM; ++t) {
-      const double v = wave_sum(m[p][t]);
-      if ((tid & 63) == 0) red[p][t][tid >> 6] = v;
-    }
-  __syncthreads();
-  if (tid >= PB || n0 + tid >= N) return;
-  const int p = tid;
-  const int64_t n = n0 + p;
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
   double cov[D][D];
   if (N == 1) {
     // indices is 1-D -> deltas = |X|, one sample -> diag(|X[0]|)
@@ -516,8 +517,11 @@ __global__ __launch_bounds__(256) void local_fit_kernel(
       for (int b = 0; b < D; ++b) cov[a][b] = (a == b) ? fabs(X[a]) : 0.0;
   } else {
     double M[NM];
-    for (int t = 0; t < NM; ++t)
-      M[t] = ((red[p][t][0] + red[p][t][1]) + red[p][t][2]) + red[p][t][3];
+    for (int t = 0; t < NM; ++t) {
+      double v = 0.0;
+      for (int y = 0; y < RS; ++y) v += part[((int64_t)y * NM + t) * N + n];
+      M[t] = v;
+    }
     double S2[D][D];
     {
       int c = 2 + D;
@@ -566,6 +570,16 @@ __global__ __launch_bounds__(256) void local_fit_kernel(
   lnorm[n] = 0.5 * (D * LOG_2PI + log(det));
 }
 
+// row chunks of the moments kernel: ~8 waves per SIMD, >= 64 rows a chunk
+inline int moments_chunks(int64_t N) {
+  const int64_t waves = (N + 63) / 64;
+  int64_t rs = (8192 + waves - 1) / waves;
+  const int64_t cap = N / 64 > 1 ? N / 64 : 1;
+  if (rs > cap) rs = cap;
+  if (rs > 32) rs = 32;
+  return (int)(rs < 1 ? 1 : rs);
+}
+
 constexpr int SEL_PB = 8;  // particles per selection block (in registers)
 
 template <int D>
@@ -583,10 +597,18 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
                        dim3(256), 0, s, X, N, nq, sel_v, sel_ties, sel_rank0);
     ABC_LAUNCHED();
   }
-  constexpr int FPB = D <= 5 ? 4 : 2;  // particles per accumulation block
-  hipLaunchKernelGGL((local_fit_kernel<D, FPB>), dim3((unsigned)ceil_div(N, FPB)), dim3(256),
-                     0, s, X, w, N, nq, scaling, eps, (const unsigned long long*)sel_v,
-                     (const long long*)sel_ties, (const long long*)sel_rank0, covs, inv,
+  constexpr int NM = 2 + D + D * (D + 1) / 2;
+  const int RS = N > 1 ? moments_chunks(N) : 1;
+  double* part = cv.take<double>((size_t)RS * NM * (size_t)N);
+  if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
+  if (N > 1) {
+    hipLaunchKernelGGL((local_moments_kernel<D>), dim3((unsigned)ceil_div(N, 256), (unsigned)RS),
+                       dim3(256), 0, s, X, w, N, (const unsigned long long*)sel_v,
+                       (const long long*)sel_ties, (const long long*)sel_rank0, part);
+    ABC_LAUNCHED();
+  }
+  hipLaunchKernelGGL((local_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256),
+                     0, s, X, N, nq, scaling, eps, (const double*)part, RS, covs, inv,
                      dets, chol, lnorm);
   ABC_LAUNCHED();
   return ABC_OK;
@@ -847,9 +869,11 @@ int launch_pdf(const double* x, int64_t M, const double* X, const double* w,
 using namespace abc;
 
 extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
-  (void)d;
   size_t off = 0;
   for (int i = 0; i < 3; ++i) size_only<int64_t>(off, (size_t)(N > 0 ? N : 1));
+  // partial moments of the row chunks (local_moments_kernel)
+  const size_t nm = 2 + (size_t)d + (size_t)d * (d + 1) / 2;
+  size_only<double>(off, (size_t)moments_chunks(N > 1 ? N : 1) * nm * (size_t)(N > 0 ? N : 1));
   return off + 256;
 }
 
