@@ -221,6 +221,17 @@ def test_collectives_two_ranks():
             np.testing.assert_array_equal(r["e"], [0, 2, 0])
 
 
+def test_allgather_rows_ordered_single_rank():
+    """Without a process group the packed gather is the identity (ws = 1)."""
+    from pyabc_amd.sampler import distributed as dd
+    a = torch.arange(6, dtype=torch.float64).reshape(3, 2)
+    b = torch.arange(3, dtype=torch.float64)
+    out = dd.allgather_rows_ordered([a, b], np.array([[2], [1]]), torch.device("cpu"))
+    assert out[0] is a and out[1] is b
+    t = dd.allgather_counts(torch.tensor([7]), torch.device("cpu"))
+    np.testing.assert_array_equal(t, [7])
+
+
 def test_cutoff_prefix():
     from pyabc_amd.sampler.distributed import cutoff, rank_range
     np.testing.assert_array_equal(cutoff([5, 7, 2], 9), [5, 4, 0])
