@@ -262,6 +262,20 @@ def test_pnorm_golden(dev):
         np.testing.assert_allclose(dd, gg[c + "__d"], rtol=1e-12, err_msg=c)
 
 
+@pytest.mark.parametrize("B,S", [(1, 33), (3, 256), (17, 100), (1001, 256), (64, 700)])
+def test_pnorm_wave_rows_vs_oracle(dev, B, S):
+    """Wide-row PNorm (S > 32: several rows per wave, ragged last wave)."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(B * 1000 + S)
+    x = rng.standard_normal((B, S)) * 10 ** rng.uniform(-2, 2, S)
+    x0 = rng.standard_normal(S)
+    w = rng.uniform(0.1, 2.0, S)
+    for p in (1.0, 2.0, 3.0, np.inf):
+        dd = gpu.pnorm(T(x), T(x0), T(w), p).cpu().numpy()
+        np.testing.assert_allclose(dd, oracle.pnorm(x, x0, w=w, p=p), rtol=1e-12,
+                                   err_msg=f"p={p}")
+
+
 def test_weighted_quantile_golden(dev):
     from pyabc_amd import gpu
     gg = g("quantile.npz")
