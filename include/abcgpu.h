@@ -174,6 +174,12 @@ int abc_simulate_linear_gaussian(const double* theta, int64_t B, int d, int S,
 int abc_pnorm(const double* x, int64_t B, int S, const double* x0,
               const double* wf, double p, double* d, void* stream);
 
+/* A proposal that exhausted max_attempts (attempts > max_attempts) is not a
+ * valid candidate (the reference keeps drawing, smc.py:649-662): its
+ * distance becomes +inf so that no acceptor takes it. */
+int abc_mask_gave_up(double* dist, const int32_t* attempts, int64_t B,
+                     int max_attempts, void* stream);
+
 /* ---- UniformAcceptor (acceptor.py:235-244) + order-preserving compaction -
  * accept[b] = d[b] <= eps.  Writes the positions of accepted rows in
  * increasing order to idx and their number to *count (device int64). */
@@ -181,6 +187,60 @@ size_t abc_compact_workspace(int64_t B);
 int abc_accept_compact(const double* d, int64_t B, double eps, int64_t* idx,
                        int64_t* count, void* ws, size_t ws_bytes,
                        void* stream);
+/* ---- fused candidate round: the whole per-candidate closure ---------------
+ * Replaces one sampler round of pyabc/sampler/singlecore.py:20-38 /
+ * multicore_evaluation_parallel.py:92-150 over the closure smc.py:588-724:
+ * Transition.rvs + prior re-draw (smc.py:610-662; MultivariateNormalTransition
+ * multivariatenormal.py:85-97 with L shared, LocalTransition
+ * local_transition.py:141-145 with per-particle L, or the prior itself at
+ * t = 0 when X == NULL), LinearGaussianModel (model.py:89-116), PNormDistance
+ * (distance.py:79-105) and UniformAcceptor d <= eps (acceptor.py:235-244).
+ * Candidate b of a round is global index idx0 + b, keyed exactly like
+ * abc_propose / abc_simulate_linear_gaussian, so a round accepts precisely
+ * the candidates the staged kernels (propose -> simulate -> pnorm ->
+ * accept_compact) would.  A candidate whose proposal exhausted max_attempts
+ * is rejected (the reference never accepts a zero-prior-density parameter).
+ * The spec struct is HOST memory; the arrays it points to are device memory. */
+typedef struct abc_candidate_spec {
+  int d;                       /* parameters (sorted names)                */
+  int S;                       /* summary statistics (x_0 key order)       */
+  const double* X;             /* population [N x d]; NULL: prior draw     */
+  const double* cdf;           /* inclusive scan of the weights [N]        */
+  const int32_t* guide;        /* abc_cdf_guide table [N] (nullable)        */
+  int64_t N;
+  const double* L;             /* [d x d], or [N x d x d] per particle     */
+  int per_particle_L;
+  const int32_t* prior_kind;   /* [d] ABC_PRIOR_*                          */
+  const double* prior_params;  /* [4 d]                                    */
+  int max_attempts;            /* prior re-draws per candidate             */
+  const int32_t* src;          /* simulator: x_k = a_k theta[src_k]        */
+  const double* a;             /*            + sigma_k e_k                 */
+  const double* sigma;
+  const double* x0;            /* PNorm: observed [S]                      */
+  const double* wf;            /*        weights * factors [S]             */
+  double p;                    /*        p >= 1, +inf = max norm           */
+  uint64_t seed;
+  uint32_t generation;
+} abc_candidate_spec;
+/* One round of B candidates: writes the positions b (0 <= b < B, increasing)
+ * of the first `cap` accepted candidates to idx and the number accepted in
+ * the round (uncapped) to *count (device int64).  rec_x (nullable) receives
+ * the sum stats of every candidate [B x S] (record_rejected).  filter != 0
+ * allows the exact early-rejection mode (first 4 statistics, p in {1,2,inf},
+ * no rec_x): the same accept set at lower cost when few candidates pass. */
+size_t abc_candidates_workspace(int64_t B);
+int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0,
+                         int64_t B, double eps, int filter, int64_t cap,
+                         int64_t* idx, int64_t* count, double* rec_x,
+                         void* ws, size_t ws_bytes, void* stream);
+/* Rows of the kept candidates: for i < n, candidate idx0 + idx[i] ->
+ * theta [n x d], prior log-density [n], ancestor [n] (nullable; -1 at t = 0),
+ * sum stats x [n x S], distance [n]; bit-identical to the staged kernels. */
+int abc_candidates_regen(const abc_candidate_spec* spec, int64_t idx0,
+                         const int64_t* idx, int64_t n, double* theta,
+                         double* prior_logpdf, int64_t* ancestor, double* x,
+                         double* dist, void* stream);
+
 /* Gather rows: out[i, :] = in[idx[i], :] (row width `cols` doubles). */
 int abc_gather_rows(const double* in, const int64_t* idx, int64_t n, int cols,
                     double* out, void* stream);

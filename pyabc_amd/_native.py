@@ -46,8 +46,12 @@ SIGNATURES = {
     "abc_simulate_linear_gaussian": (I32, [P, I64, I32, I32, P, P, P, U64,
                                            U32, I64, P, P]),
     "abc_pnorm": (I32, [P, I64, I32, P, P, D, P, P]),
+    "abc_mask_gave_up": (I32, [P, P, I64, I32, P]),
     "abc_compact_workspace": (SZ, [I64]),
     "abc_accept_compact": (I32, [P, I64, D, P, P, P, SZ, P]),
+    "abc_candidates_workspace": (SZ, [I64]),
+    "abc_candidates_round": (I32, [P, I64, I64, D, I32, I64, P, P, P, P, SZ, P]),
+    "abc_candidates_regen": (I32, [P, I64, P, I64, P, P, P, P, P, P]),
     "abc_gather_rows": (I32, [P, P, I64, I32, P, P]),
     "abc_gather_rows_batch": (I32, [I32, P, P, P, P, P, I64, P]),
     "abc_importance_weights": (I32, [P, P, P, I64, D, P, P]),
@@ -74,6 +78,19 @@ SIGNATURES = {
     "abc_temper_workspace": (SZ, []),
     "abc_temper_sums": (I32, [P, P, P, I64, D, I32, I32, D, D, P, P, SZ, P]),
 }
+
+
+
+class CandidateSpec(C.Structure):
+    """abc_candidate_spec (include/abcgpu.h), field for field."""
+    _fields_ = [("d", C.c_int), ("S", C.c_int),
+                ("X", P), ("cdf", P), ("guide", P), ("N", I64),
+                ("L", P), ("per_particle_L", C.c_int),
+                ("prior_kind", P), ("prior_params", P), ("max_attempts", C.c_int),
+                ("src", P), ("a", P), ("sigma", P),
+                ("x0", P), ("wf", P), ("p", D),
+                ("seed", U64), ("generation", U32)]
+
 
 # C error codes (include/abcgpu.h)
 ABC_OK = 0

@@ -1,0 +1,415 @@
+// Per-candidate device code shared by the stage kernels (abc_sampler.hip) and
+// the fused candidate round (abc_fused.hip).
+//
+// Reference per-candidate closure (pyabc/smc.py:588-724):
+//   _generate_valid_proposal (smc.py:610-662): theta = Transition.rvs()
+//     (multivariatenormal.py:85-97 / local_transition.py:141-145), re-drawn
+//     while the prior density is 0; t == 0: theta = prior.rvs()
+//   Model.accept (model.py:163-218) -> summary stats -> PNormDistance
+//     (distance/distance.py:79-105) -> UniformAcceptor d <= eps
+//     (acceptor/acceptor.py:235-244)
+// Every draw is a pure function of (seed, generation, global candidate index,
+// slot), so the stage kernels, the fused round and its regeneration of the
+// accepted rows compute the same candidate bit for bit: the functions below
+// are the single definition all of them inline, and floating-point
+// contraction is off (explicit fma() where a fused multiply-add is meant), so
+// the compiler cannot fuse differently in different kernels.
+#pragma once
+#include "abc_common.h"
+
+#pragma clang fp contract(off)
+
+namespace abc {
+
+constexpr double LOG_SQRT_2PI = 0.91893853320467274178;
+constexpr uint32_t SLOTS_PER_ATTEMPT = 65536;
+constexpr uint32_t SLOT_ANCESTOR = 0;
+constexpr uint32_t SLOT_PERTURB = 1;     // 4 normals per slot
+constexpr uint32_t SLOT_PRIOR = 32;      // + 512 k + iteration
+constexpr uint32_t SLOT_SIM = 0x40000000u;
+
+// normals q .. q+3 of one slot (Box-Muller pairs; only the first `need`
+// (1..4) are produced -- the pair the caller does not use is skipped)
+__device__ __forceinline__ void normals4(uint64_t g, uint32_t slot, uint32_t gen,
+                                         uint64_t seed, double n[4], int need = 4) {
+  u32x4 r = philox(g, slot, gen, seed);
+  box_muller(r.x, r.y, n[0], n[1]);
+  if (need > 2) box_muller(r.z, r.w, n[2], n[3]);
+}
+
+// ---- priors (scipy.stats pdf conventions, closed support [a, b]) ----------
+__device__ __noinline__ double prior_logpdf1(int kind, const double* p, double x) {
+  switch (kind) {
+    case ABC_PRIOR_FLAT:
+      return 0.0;
+    case ABC_PRIOR_NORM: {
+      double y = (x - p[0]) / p[1];
+      return -0.5 * y * y - LOG_SQRT_2PI - log(p[1]);
+    }
+    case ABC_PRIOR_UNIFORM: {
+      double y = (x - p[0]) / p[1];
+      return (y >= 0.0 && y <= 1.0) ? -log(p[1]) : -INFINITY;
+    }
+    case ABC_PRIOR_EXPON: {
+      double y = (x - p[0]) / p[1];
+      return (y >= 0.0) ? -y - log(p[1]) : -INFINITY;
+    }
+    case ABC_PRIOR_LAPLACE: {
+      double y = (x - p[0]) / p[1];
+      return -fabs(y) - log(2.0 * p[1]);
+    }
+    case ABC_PRIOR_LOGNORM: {  // s, loc, scale
+      double y = (x - p[1]) / p[2];
+      if (!(y > 0.0)) return -INFINITY;
+      double ly = log(y) / p[0];
+      return -0.5 * ly * ly - log(p[0] * y) - LOG_SQRT_2PI - log(p[2]);
+    }
+    case ABC_PRIOR_GAMMA: {  // a, loc, scale
+      double a = p[0], y = (x - p[1]) / p[2];
+      if (y < 0.0) return -INFINITY;
+      if (y == 0.0) return a < 1.0 ? INFINITY : (a == 1.0 ? -log(p[2]) : -INFINITY);
+      return (a - 1.0) * log(y) - y - lgamma(a) - log(p[2]);
+    }
+    case ABC_PRIOR_BETA: {  // a, b, loc, scale
+      double a = p[0], b = p[1], y = (x - p[2]) / p[3];
+      if (y < 0.0 || y > 1.0) return -INFINITY;
+      double lb = lgamma(a) + lgamma(b) - lgamma(a + b);
+      double t1 = (a == 1.0) ? 0.0 : (a - 1.0) * log(y);
+      double t2 = (b == 1.0) ? 0.0 : (b - 1.0) * log1p(-y);
+      return t1 + t2 - lb - log(p[3]);
+    }
+  }
+  return NAN;
+}
+
+// Prior density > 0 at x (the re-draw test of smc.py:654-656), decided on
+// the support alone: exactly the x for which prior_logpdf1 is not -inf / NaN
+// (up to overflow of a finite log density), without its transcendentals.
+__device__ __forceinline__ bool prior_in_support1(int kind, const double* p, double x) {
+  switch (kind) {
+    case ABC_PRIOR_FLAT:
+      return true;
+    case ABC_PRIOR_NORM: {
+      double y = (x - p[0]) / p[1];
+      return y * y < INFINITY;  // false for NaN
+    }
+    case ABC_PRIOR_UNIFORM: {
+      double y = (x - p[0]) / p[1];
+      return y >= 0.0 && y <= 1.0;
+    }
+    case ABC_PRIOR_EXPON: {
+      double y = (x - p[0]) / p[1];
+      return y >= 0.0 && y < INFINITY;
+    }
+    case ABC_PRIOR_LAPLACE: {
+      double y = (x - p[0]) / p[1];
+      return fabs(y) < INFINITY;
+    }
+    case ABC_PRIOR_LOGNORM: {
+      double y = (x - p[1]) / p[2];
+      return y > 0.0 && y < INFINITY;
+    }
+    case ABC_PRIOR_GAMMA: {
+      double y = (x - p[1]) / p[2];
+      return (y > 0.0 && y < INFINITY) || (y == 0.0 && p[0] <= 1.0);
+    }
+    case ABC_PRIOR_BETA: {
+      double y = (x - p[2]) / p[3];
+      if (!(y >= 0.0 && y <= 1.0)) return false;
+      if (y == 0.0 && p[0] > 1.0) return false;
+      if (y == 1.0 && p[1] > 1.0) return false;
+      return true;
+    }
+  }
+  return false;
+}
+
+// Marsaglia-Tsang gamma(a, 1) draw; stream = (g, base + iteration)
+__device__ inline double gamma_draw(double a, uint64_t g, uint32_t base, uint32_t gen,
+                                    uint64_t seed) {
+  double boost = 1.0;
+  uint32_t it = 0;
+  if (a < 1.0) {
+    u32x4 r = philox(g, base + 500, gen, seed);
+    boost = pow(uniform01(r.x), 1.0 / a);
+    a += 1.0;
+  }
+  const double dd = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * dd);
+  for (; it < 480; ++it) {
+    u32x4 r = philox(g, base + it, gen, seed);
+    double n0, n1;
+    box_muller(r.x, r.y, n0, n1);
+    double v = 1.0 + c * n0;
+    if (v <= 0.0) continue;
+    v = v * v * v;
+    double u = uniform01(r.z);
+    if (log(u) < 0.5 * n0 * n0 + dd - dd * v + dd * log(v)) return dd * v * boost;
+  }
+  return dd * boost;  // practically unreachable
+}
+
+__device__ __noinline__ double prior_draw1(int kind, const double* p, uint64_t g,
+                                     uint32_t base, uint32_t gen, uint64_t seed) {
+  u32x4 r = philox(g, base, gen, seed);
+  double n0, n1;
+  switch (kind) {
+    case ABC_PRIOR_NORM:
+      box_muller(r.x, r.y, n0, n1);
+      return p[0] + p[1] * n0;
+    case ABC_PRIOR_UNIFORM:
+      return p[0] + p[1] * uniform53(r.x, r.y);
+    case ABC_PRIOR_EXPON:
+      return p[0] - p[1] * log(uniform01(r.x));
+    case ABC_PRIOR_LAPLACE: {
+      double u = uniform01(r.x) - 0.5;
+      return p[0] - p[1] * copysign(1.0, u) * log1p(-2.0 * fabs(u));
+    }
+    case ABC_PRIOR_LOGNORM:
+      box_muller(r.x, r.y, n0, n1);
+      return p[1] + p[2] * exp(p[0] * n0);
+    case ABC_PRIOR_GAMMA:
+      return p[1] + p[2] * gamma_draw(p[0], g, base + 1, gen, seed);
+    case ABC_PRIOR_BETA: {
+      double x = gamma_draw(p[0], g, base + 1, gen, seed);
+      double y = gamma_draw(p[1], g, base + 1 + 256, gen, seed);
+      return p[2] + p[3] * x / (x + y);
+    }
+  }
+  return NAN;
+}
+
+__device__ __forceinline__ double prior_logpdf(const int32_t* kind,
+                                               const double* params, int d,
+                                               const double* th) {
+  double s = 0.0;
+  for (int k = 0; k < d; ++k) s += prior_logpdf1(kind[k], params + 4 * k, th[k]);
+  return s;
+}
+
+__device__ __forceinline__ int64_t upper_bound(const double* cdf, int64_t N,
+                                               double target) {
+  int64_t lo = 0, hi = N;  // first index with cdf[idx] > target
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (cdf[mid] > target) hi = mid; else lo = mid + 1;
+  }
+  return lo < N ? lo : N - 1;
+}
+
+// Ancestor = first index with cdf > target (np.searchsorted side="right",
+// clamped to N - 1).  With a guide table (guide[k] = that index for the
+// target k * total / N, abc_cdf_guide) the search starts in a bracket of
+// ~3 table bins: O(1) expected instead of log2 N dependent loads.
+__device__ __forceinline__ int64_t ancestor_search(const double* __restrict__ cdf,
+                                                   const int32_t* __restrict__ guide,
+                                                   int64_t N, double total,
+                                                   double target) {
+  if (guide == nullptr) return upper_bound(cdf, N, target);
+  const double step = total / (double)N;
+  int64_t k = (int64_t)floor(target / step) - 1;  // t_k < target (one-bin margin)
+  k = k < 0 ? 0 : (k > N - 1 ? N - 1 : k);
+  int64_t lo = guide[k];
+  int64_t hi = k + 3 < N ? (int64_t)guide[k + 3] + 1 : N;  // t_{k+3} > target
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (cdf[mid] > target) hi = mid; else lo = mid + 1;
+  }
+  return lo < N ? lo : N - 1;
+}
+
+// ---- exact support box ------------------------------------------------------
+// The support {x : prior_in_support1(kind, p, x)} of every kind is an
+// interval of doubles (y = (x - loc) / scale is monotone in x, and so is each
+// test on y), so it equals [lo, hi] for two doubles found by bisection over
+// the order-preserving integer image of the doubles, evaluating the very
+// predicate above.  The per-candidate re-draw test is then two compares.
+__device__ __forceinline__ uint64_t dkey(double x) {   // order-preserving
+  const uint64_t u = (uint64_t)__double_as_longlong(x);
+  return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+__device__ __forceinline__ double dval(uint64_t k) {
+  const uint64_t u = (k >> 63) ? (k & ~(1ull << 63)) : ~k;
+  return __longlong_as_double((long long)u);
+}
+__device__ __forceinline__ void support_bounds(int kind, const double* p, double* lo_hi) {
+  double c;  // a point inside the support
+  switch (kind) {
+    case ABC_PRIOR_UNIFORM: c = p[0] + 0.5 * p[1]; break;
+    case ABC_PRIOR_EXPON: c = p[0] + p[1]; break;
+    case ABC_PRIOR_LOGNORM: case ABC_PRIOR_GAMMA: c = p[1] + p[2]; break;
+    case ABC_PRIOR_BETA: c = p[2] + 0.5 * p[3]; break;
+    case ABC_PRIOR_NORM: case ABC_PRIOR_LAPLACE: c = p[0]; break;
+    default: c = 0.0;
+  }
+  if (!prior_in_support1(kind, p, c)) {  // empty (degenerate parameters)
+    lo_hi[0] = INFINITY;
+    lo_hi[1] = -INFINITY;
+    return;
+  }
+  const uint64_t kc = dkey(c);
+  // lowest member: P(hi) true, P(lo) false
+  uint64_t lo = dkey(-INFINITY), hi = kc;
+  if (prior_in_support1(kind, p, -INFINITY)) {
+    hi = lo;
+  } else {
+    while (hi - lo > 1) {
+      const uint64_t m = lo + (hi - lo) / 2;
+      if (prior_in_support1(kind, p, dval(m))) hi = m; else lo = m;
+    }
+  }
+  lo_hi[0] = dval(hi);
+  // highest member: P(lo) true, P(hi) false
+  lo = kc;
+  hi = dkey(INFINITY);
+  if (prior_in_support1(kind, p, INFINITY)) {
+    lo = hi;
+  } else {
+    while (hi - lo > 1) {
+      const uint64_t m = lo + (hi - lo) / 2;
+      if (prior_in_support1(kind, p, dval(m))) lo = m; else hi = m;
+    }
+  }
+  lo_hi[1] = dval(lo);
+}
+
+// ---- one proposal ----------------------------------------------------------
+struct ProposalArgs {
+  const double* X;       // population [N x d] (nullptr: draw from the prior)
+  const double* cdf;      // inclusive scan of w [N]
+  const int32_t* guide;   // cdf guide table [N] or nullptr
+  int64_t N;
+  const double* L;        // [d x d] row-major, or [N x d x d] per particle
+  const int32_t* kind;    // prior kinds [d]
+  const double* params;   // prior params [4 d]
+  int d;
+  int max_attempts;
+  uint64_t seed;
+  uint32_t gen;
+};
+
+// The support box of the block's prior in LDS (sbox: 2 * 64 doubles); every
+// thread of the block must call it (it synchronises).
+__device__ __forceinline__ void support_box_block(const int32_t* kind, const double* params,
+                                                  int d, double* sbox) {
+  if ((int)threadIdx.x < d) support_bounds(kind[threadIdx.x], params + 4 * threadIdx.x,
+                                           sbox + 2 * threadIdx.x);
+  __syncthreads();
+}
+
+// MODE: PROP_MVN (one shared L), PROP_LOCAL (per-particle L), PROP_PRIOR
+// (X == nullptr: draw from the prior).  Separate instantiations keep the
+// prior draw's calls out of the transition kernels' register allocation.
+constexpr int PROP_MVN = 0, PROP_LOCAL = 1, PROP_PRIOR = 2;
+
+// Candidate g: ancestor j ~ Cat(w), theta = X_j + L_j n (or a prior draw when
+// X == nullptr), re-drawn while theta is outside the prior support `box`
+// ([lo_k, hi_k] pairs from support_bounds).  th holds D (D > 0) or d <= 64
+// values.  The perturbation is accumulated one Box-Muller pair at a time in
+// q order, theta_k = fma(L_kq, n_q, theta_k) starting from X_jk (one code
+// copy of the transform).  Returns the attempts used, max_attempts + 1 when
+// every attempt fell outside the support (theta then holds the last one).
+template <int D, int MODE>
+__device__ __forceinline__ int propose_one(const ProposalArgs& A, const double* box,
+                                           uint64_t g, double* th, int64_t& j) {
+  const int d = D > 0 ? D : A.d;
+  j = -1;
+  const double total = (MODE != PROP_PRIOR) ? A.cdf[A.N - 1] : 0.0;
+  for (int att = 0; att < A.max_attempts; ++att) {
+    const uint32_t s0 = (uint32_t)att * SLOTS_PER_ATTEMPT;
+    if (MODE == PROP_PRIOR) {
+#pragma unroll
+      for (int k = 0; k < (D > 0 ? D : d); ++k)
+        th[k] = prior_draw1(A.kind[k], A.params + 4 * k, g,
+                            s0 + SLOT_PRIOR + 512u * k, A.gen, A.seed);
+    } else {
+      u32x4 r = philox(g, s0 + SLOT_ANCESTOR, A.gen, A.seed);
+      j = ancestor_search(A.cdf, A.guide, A.N, total, uniform53(r.x, r.y) * total);
+      // L is re-read per candidate (scalar loads for the shared factor): an
+      // opaque pointer stops the compiler hoisting d*d doubles out of the
+      // caller's candidate loop into registers
+      const double* Lb = A.L;
+      asm volatile("" : "+s"(Lb));
+      const double* Lj = MODE == PROP_LOCAL ? Lb + j * d * d : Lb;
+      const double* Xj = A.X + j * d;
+#pragma unroll
+      for (int k = 0; k < (D > 0 ? D : d); ++k) th[k] = Xj[k];
+#pragma unroll 1
+      for (int q = 0; q < d; q += 2) {
+        if ((q & 3) == 0) r = philox(g, s0 + SLOT_PERTURB + (uint32_t)(q >> 2), A.gen, A.seed);
+        double n0, n1;
+        box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1);
+#pragma unroll
+        for (int k = 0; k < (D > 0 ? D : d); ++k) {
+          th[k] = fma(Lj[k * d + q], n0, th[k]);
+          if (q + 1 < d) th[k] = fma(Lj[k * d + q + 1], n1, th[k]);
+        }
+      }
+    }
+    const double* bx = box;
+    asm volatile("" : "+s"(bx));
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < (D > 0 ? D : d); ++k) ok = ok && bx[2 * k] <= th[k] && th[k] <= bx[2 * k + 1];
+    if (ok) return att + 1;  // prior density > 0 (smc.py:654-656)
+  }
+  return A.max_attempts + 1;
+}
+
+// ---- LinearGaussianModel + PNormDistance -----------------------------------
+struct SimDistArgs {
+  const int32_t* src;     // x_k = a_k theta[src_k] + sigma_k e_k
+  const double* a;
+  const double* sigma;
+  const double* x0;       // observed sum stats [S]
+  const double* wf;       // PNorm weights * factors [S]
+  double p;
+  int S;
+};
+
+__device__ __forceinline__ double pterm(double v, double p) {
+  return (p == 1.0) ? v : (p == 2.0 ? v * v : pow(v, p));
+}
+// running p-norm state s (sum of |.|^p, or max for p = inf); order = k order
+__device__ __forceinline__ double pnorm_acc(double s, double v, double p) {
+  return isinf(p) ? fmax(s, v) : s + pterm(v, p);
+}
+__device__ __forceinline__ double pnorm_finish(double s, double p) {
+  return isinf(p) ? s : ((p == 1.0) ? s : (p == 2.0 ? sqrt(s) : pow(s, 1.0 / p)));
+}
+// one simulated statistic (simulate_lg_kernel's formula)
+__device__ __forceinline__ double lg_stat(const SimDistArgs& M, int k, double th_src,
+                                          double e) {
+  return M.a[k] * th_src + M.sigma[k] * e;
+}
+
+// Simulate statistics [q0, q1) (q0 even) of candidate g and fold them into
+// the p-norm state s in k order; x (nullable) receives the row.  Statistic k
+// uses normal k of the candidate's simulation stream (slot SLOT_SIM + k/4).
+// theta_{src_k} is read from tsrc[src_k * tstride] (an LDS column of the
+// calling thread: a register array indexed by src_k would go to scratch).
+__device__ __forceinline__ double sim_pnorm_range(const SimDistArgs& M,
+                                                  const double* tsrc, int tstride,
+                                                  uint64_t g, uint32_t gen,
+                                                  uint64_t seed, int q0, int q1,
+                                                  double s, double* x) {
+  u32x4 r;
+  if (q0 < q1 && (q0 & 3)) r = philox(g, SLOT_SIM + (uint32_t)(q0 >> 2), gen, seed);
+#pragma unroll 1
+  for (int q = q0; q < q1; q += 2) {
+    if ((q & 3) == 0) r = philox(g, SLOT_SIM + (uint32_t)(q >> 2), gen, seed);
+    double n2[2];
+    box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n2[0], n2[1]);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int k = q + t;
+      if (k < q1) {
+        const double xv = lg_stat(M, k, tsrc[M.src[k] * tstride], n2[t]);
+        if (x) x[k] = xv;
+        s = pnorm_acc(s, fabs(M.wf[k] * (xv - M.x0[k])), M.p);
+      }
+    }
+  }
+  return s;
+}
+
+}  // namespace abc

@@ -1,0 +1,357 @@
+// Fused candidate round: one launch runs the whole per-candidate closure of
+// pyabc/smc.py:588-724 for B candidates -- proposal with prior re-draw
+// (smc.py:610-662), LinearGaussianModel simulation (model.py:89-116),
+// PNormDistance (distance/distance.py:79-105) and the UniformAcceptor test
+// d <= eps (acceptor/acceptor.py:235-244) -- and keeps nothing per candidate
+// but one accept bit.  The sampler loop it serves is
+// sampler/singlecore.py:20-38 / multicore_evaluation_parallel.py:92-150
+// (draw until n accepted, keep the first n by evaluation index).
+//
+// Because every draw is keyed by (seed, generation, global index, slot), the
+// rows of the few accepted candidates are not stored by the round: the
+// regeneration kernel recomputes theta, prior log-density, ancestor, sum
+// stats and distance for the kept indices with the same device functions
+// (abc_candidate.h), bit for bit.  Per rejected candidate the round moves
+// ~1/8 byte to HBM instead of ~440 B for the staged pipeline.
+//
+// Filter mode (low acceptance): phase A proposes every candidate of a tile
+// and simulates only its first group of 4 statistics; the p-norm partial sum
+// of nonnegative terms can only grow, so a partial distance > eps rejects the
+// candidate exactly.  Survivors are queued in LDS and phase B evaluates them
+// in full, dense across the block's waves (no lane idles behind an early
+// exit).
+#include "abc_candidate.h"
+
+namespace abc {
+namespace {
+
+constexpr int FR_T = 256;                // threads per block
+constexpr int FR_CPT = 8;                // candidates per thread and tile
+constexpr int FR_TILE = FR_T * FR_CPT;   // candidates per block
+constexpr int FR_WORDS = FR_TILE / 64;   // 64-bit accept words per tile
+
+struct RoundArgs {
+  ProposalArgs P;
+  SimDistArgs M;
+  const double* box;  // prior support [d x (lo, hi)] (support_box_kernel)
+};
+
+// Full evaluation of candidate g: proposal + simulation + distance.  Returns
+// the distance (+inf when the proposal gave up on the prior support), the
+// attempts and the ancestor through the references; x (nullable) gets the row.
+// theta of the calling thread as the simulator's source column: an LDS
+// slab [D][FR_T] for D > 0, the (scratch) array itself for runtime d
+template <int D>
+struct ThetaSlab {
+  static constexpr int ROWS = D > 0 ? D : 1;
+  double* base;
+  __device__ __forceinline__ const double* put(const double* th) const {
+    if (D == 0) return th;
+#pragma unroll
+    for (int k = 0; k < ROWS; ++k) base[k * FR_T + threadIdx.x] = th[k];
+    return base + threadIdx.x;
+  }
+  static constexpr int stride() { return D > 0 ? FR_T : 1; }
+};
+
+// Full evaluation of candidate g: proposal + simulation + distance.  Returns
+// the distance (+inf when the proposal gave up on the prior support), the
+// attempts and the ancestor through the references; x (nullable) gets the row.
+template <int D, int MODE>
+__device__ __forceinline__ double evaluate_full(const RoundArgs& A, const ThetaSlab<D>& slab,
+                                                uint64_t g, double* th, int64_t& j,
+                                                int& att, double* x) {
+  att = propose_one<D, MODE>(A.P, A.box, g, th, j);
+  const double* ts = slab.put(th);
+  const double s = sim_pnorm_range(A.M, ts, slab.stride(), g, A.P.gen, A.P.seed, 0, A.M.S,
+                                   0.0, x);
+  const double dist = pnorm_finish(s, A.M.p);
+  return att <= A.P.max_attempts ? dist : INFINITY;
+}
+
+template <int D, int MODE>
+__global__ __launch_bounds__(FR_T) void fused_round_kernel(
+    RoundArgs A, int64_t idx0, int64_t B, double eps, int filter,
+    uint64_t* __restrict__ bits, int64_t* __restrict__ tile_cnt,
+    double* __restrict__ rec_x) {
+  constexpr int DM = D > 0 ? D : 64;
+  __shared__ uint32_t tbits[FR_TILE / 32];
+  __shared__ uint16_t queue[FR_TILE];
+  __shared__ int qn;
+  __shared__ double thl[ThetaSlab<D>::ROWS * FR_T];
+  const ThetaSlab<D> slab{thl};
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int d = D > 0 ? D : A.P.d;
+  const int64_t tile0 = (int64_t)blockIdx.x * FR_TILE;
+  if (tid < FR_TILE / 32) tbits[tid] = 0u;
+  if (tid == 0) qn = 0;
+  __syncthreads();
+  double th[DM];
+  int64_t j;
+  int att;
+  if (filter) {
+    // phase A: proposal + first group of 4 statistics; an exact early reject
+#pragma unroll 1
+    for (int it = 0; it < FR_CPT; ++it) {
+      const int loc = it * FR_T + tid;
+      const int64_t b = tile0 + loc;
+      if (b < B) {
+        const uint64_t g = (uint64_t)(idx0 + b);
+        att = propose_one<D, MODE>(A.P, A.box, g, th, j);
+        const double* ts = slab.put(th);
+        const double s = sim_pnorm_range(A.M, ts, slab.stride(), g, A.P.gen, A.P.seed, 0, 4,
+                                         0.0, nullptr);
+        if (att <= A.P.max_attempts && !(pnorm_finish(s, A.M.p) > eps)) {
+          const int pos = atomicAdd(&qn, 1);
+          queue[pos] = (uint16_t)loc;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // full evaluation: every candidate of the tile, or the phase-A survivors
+  // (dense over the block's waves)
+  const int n = filter ? qn : FR_TILE;
+#pragma unroll 1
+  for (int i = tid; i < n; i += FR_T) {
+    const int loc = filter ? (int)queue[i] : i;
+    const int64_t b = tile0 + loc;
+    if (b < B) {
+      double* xr = rec_x ? rec_x + b * A.M.S : nullptr;
+      const double dist = evaluate_full<D, MODE>(A, slab, (uint64_t)(idx0 + b), th, j, att, xr);
+      if (dist <= eps) atomicOr(&tbits[loc >> 5], 1u << (loc & 31));
+    }
+  }
+  __syncthreads();
+  // accept words of the tile + its count (wave 0)
+  if (wave == 0) {
+    int c = 0;
+    if (lane < FR_WORDS) {
+      const uint64_t w = (uint64_t)tbits[2 * lane] | ((uint64_t)tbits[2 * lane + 1] << 32);
+      const int64_t word = tile0 / 64 + lane;
+      if (word * 64 < B) bits[word] = w;
+      c = __popcll(w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0) tile_cnt[blockIdx.x] = c;
+  }
+}
+
+__global__ void support_box_kernel(const int32_t* __restrict__ kind,
+                                   const double* __restrict__ params, int d,
+                                   double* __restrict__ box) {
+  const int k = threadIdx.x;
+  if (k < d) support_bounds(kind[k], params + 4 * k, box + 2 * k);
+}
+
+// ---- order-preserving compaction of the accept bits -----------------------
+// exclusive scan of the tile counts (one block), total -> *count
+__global__ __launch_bounds__(256) void tile_scan_kernel(int64_t* __restrict__ cnt,
+                                                        int64_t n,
+                                                        int64_t* __restrict__ count) {
+  __shared__ int64_t sh[256];
+  const int t = threadIdx.x;
+  const int64_t per = (n + 255) / 256;
+  const int64_t b0 = t * per;
+  int64_t s = 0;
+  for (int64_t k = 0; k < per; ++k)
+    if (b0 + k < n) s += cnt[b0 + k];
+  sh[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int64_t add = (t >= o) ? sh[t - o] : 0;
+    __syncthreads();
+    sh[t] += add;
+    __syncthreads();
+  }
+  int64_t off = sh[t] - s;
+  for (int64_t k = 0; k < per; ++k)
+    if (b0 + k < n) { const int64_t v = cnt[b0 + k]; cnt[b0 + k] = off; off += v; }
+  if (t == 255) *count = sh[255];
+}
+
+// one lane per 64-bit word: positions of the set bits, in increasing order,
+// for output slots < cap
+__global__ __launch_bounds__(256) void bits_write_kernel(
+    const uint64_t* __restrict__ bits, int64_t nwords,
+    const int64_t* __restrict__ tile_off, int64_t cap, int64_t* __restrict__ idx) {
+  const int64_t wd = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  uint64_t w = wd < nwords ? bits[wd] : 0ull;
+  // exclusive popcount prefix among the FR_WORDS words of this tile
+  // (tiles are FR_WORDS = 32 aligned words: half a wave)
+  int c = __popcll(w);
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < FR_WORDS; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if ((lane & (FR_WORDS - 1)) >= o) incl += v;
+  }
+  if (wd >= nwords || w == 0ull) return;
+  int64_t pos = tile_off[wd / FR_WORDS] + (incl - c);
+  while (w != 0ull && pos < cap) {
+    const int bit = __ffsll((long long)w) - 1;
+    idx[pos++] = wd * 64 + bit;
+    w &= w - 1;
+  }
+}
+
+// ---- regeneration of kept rows ----------------------------------------------
+template <int D, int MODE>
+__global__ __launch_bounds__(256) void fused_regen_kernel(
+    RoundArgs A, int64_t idx0, const int64_t* __restrict__ idx, int64_t n,
+    double* __restrict__ theta, double* __restrict__ lp, int64_t* __restrict__ anc,
+    double* __restrict__ x, double* __restrict__ dist) {
+  constexpr int DM = D > 0 ? D : 64;
+  __shared__ double sbox[128];
+  __shared__ double thl[ThetaSlab<D>::ROWS * FR_T];
+  const ThetaSlab<D> slab{thl};
+  const int d = D > 0 ? D : A.P.d;
+  support_box_block(A.P.kind, A.P.params, d, sbox);
+  A.box = sbox;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double th[DM];
+  int64_t j;
+  int att;
+  const double dd = evaluate_full<D, MODE>(A, slab, (uint64_t)(idx0 + idx[i]), th, j, att,
+                                          x + i * A.M.S);
+#pragma unroll
+  for (int k = 0; k < (D > 0 ? D : d); ++k) theta[i * d + k] = th[k];
+  lp[i] = att <= A.P.max_attempts ? prior_logpdf(A.P.kind, A.P.params, d, th) : -INFINITY;
+  if (anc) anc[i] = j;
+  dist[i] = dd;
+}
+
+RoundArgs round_args(const abc_candidate_spec* s, const double* box) {
+  RoundArgs A;
+  A.box = box;
+  A.P = ProposalArgs{s->X, s->cdf, s->guide, s->N, s->L, s->prior_kind,
+                     s->prior_params, s->d, s->max_attempts, s->seed, s->generation};
+  A.M = SimDistArgs{s->src, s->a, s->sigma, s->x0, s->wf, s->p, s->S};
+  return A;
+}
+
+int check_spec(const abc_candidate_spec* s) {
+  ABC_CHECK_ARG(s != nullptr, "candidates: null spec");
+  ABC_CHECK_ARG(s->d >= 1 && s->d <= 64 && s->S >= 1, "candidates: bad d/S");
+  ABC_CHECK_ARG(s->max_attempts >= 1 && s->max_attempts < (1 << 15),
+                "candidates: bad max_attempts");
+  ABC_CHECK_ARG(s->prior_kind && s->prior_params && s->src && s->a && s->sigma && s->x0 &&
+                s->wf, "candidates: null pointer");
+  ABC_CHECK_ARG(s->X == nullptr || (s->cdf && s->L && s->N >= 1),
+                "candidates: population needs cdf, L, N");
+  ABC_CHECK_ARG(s->p >= 1.0, "candidates: p < 1");
+  return ABC_OK;
+}
+
+#define ABC_FUSED_DISPATCH(KERNEL, GRID, STREAM, ...)                          \
+  do {                                                                         \
+    const int mode_ = spec->X == nullptr ? PROP_PRIOR                          \
+                      : (spec->per_particle_L ? PROP_LOCAL : PROP_MVN);        \
+    switch (spec->d) {                                                         \
+      ABC_FUSED_CASE(KERNEL, 1, GRID, STREAM, __VA_ARGS__)                     \
+      ABC_FUSED_CASE(KERNEL, 2, GRID, STREAM, __VA_ARGS__)                     \
+      ABC_FUSED_CASE(KERNEL, 3, GRID, STREAM, __VA_ARGS__)                     \
+      ABC_FUSED_CASE(KERNEL, 4, GRID, STREAM, __VA_ARGS__)                     \
+      ABC_FUSED_CASE(KERNEL, 5, GRID, STREAM, __VA_ARGS__)                     \
+      ABC_FUSED_CASE(KERNEL, 6, GRID, STREAM, __VA_ARGS__)                     \
+      ABC_FUSED_CASE(KERNEL, 8, GRID, STREAM, __VA_ARGS__)                     \
+      ABC_FUSED_CASE(KERNEL, 10, GRID, STREAM, __VA_ARGS__)                    \
+      ABC_FUSED_CASE(KERNEL, 12, GRID, STREAM, __VA_ARGS__)                    \
+      ABC_FUSED_CASE(KERNEL, 16, GRID, STREAM, __VA_ARGS__)                    \
+      default:                                                                 \
+        ABC_FUSED_CASE_BODY(KERNEL, 0, GRID, STREAM, __VA_ARGS__)              \
+    }                                                                          \
+  } while (0)
+#define ABC_FUSED_CASE_BODY(KERNEL, DD, GRID, STREAM, ...)                     \
+  if (mode_ == PROP_MVN)                                                       \
+    hipLaunchKernelGGL((KERNEL<DD, PROP_MVN>), GRID, dim3(256), 0, STREAM,     \
+                       __VA_ARGS__);                                           \
+  else if (mode_ == PROP_LOCAL)                                                \
+    hipLaunchKernelGGL((KERNEL<DD, PROP_LOCAL>), GRID, dim3(256), 0, STREAM,   \
+                       __VA_ARGS__);                                           \
+  else                                                                         \
+    hipLaunchKernelGGL((KERNEL<DD, PROP_PRIOR>), GRID, dim3(256), 0, STREAM,   \
+                       __VA_ARGS__);                                           \
+  break;
+#define ABC_FUSED_CASE(KERNEL, DD, GRID, STREAM, ...)                          \
+  case DD: { ABC_FUSED_CASE_BODY(KERNEL, DD, GRID, STREAM, __VA_ARGS__) }
+
+}  // namespace
+}  // namespace abc
+
+using namespace abc;
+
+extern "C" size_t abc_candidates_workspace(int64_t B) {
+  const int64_t nt = ceil_div(B > 0 ? B : 1, FR_TILE);
+  size_t off = 0;
+  size_only<uint64_t>(off, (size_t)nt * FR_WORDS);  // accept bits
+  size_only<int64_t>(off, (size_t)nt);              // tile counts / offsets
+  size_only<double>(off, 128);                      // prior support box
+  return off + 256;
+}
+
+extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0,
+                                    int64_t B, double eps, int filter, int64_t cap,
+                                    int64_t* idx, int64_t* count, double* rec_x,
+                                    void* ws, size_t ws_bytes, void* stream) {
+  const int rc = check_spec(spec);
+  if (rc != ABC_OK) return rc;
+  ABC_CHECK_ARG(B >= 0 && cap >= 0 && count, "candidates_round: bad B/cap/count");
+  ABC_CHECK_ARG(B < (1ll << 40), "candidates_round: B too large");
+  ABC_CHECK_ARG(cap == 0 || idx, "candidates_round: null idx");
+  if (ws_bytes < abc_candidates_workspace(B))
+    return set_error(ABC_ERR_WORKSPACE, "candidates_round: workspace too small");
+  hipStream_t s = as_stream(stream);
+  if (B == 0) {
+    ABC_HIP(hipMemsetAsync(count, 0, sizeof(int64_t), s));
+    return ABC_OK;
+  }
+  // the filter is exact for p in {1, 2, inf} only (monotone finish) and
+  // pointless when the first group of 4 statistics is all of them
+  const double p = spec->p;
+  const int filt = (filter && rec_x == nullptr && spec->S > 4 &&
+                    (p == 1.0 || p == 2.0 || p == INFINITY)) ? 1 : 0;
+  const int64_t nt = ceil_div(B, FR_TILE);
+  Carver c(ws, ws_bytes);
+  uint64_t* bits = c.take<uint64_t>((size_t)nt * FR_WORDS);
+  int64_t* tcnt = c.take<int64_t>((size_t)nt);
+  double* box = c.take<double>(128);
+  if (!c.ok) return set_error(ABC_ERR_WORKSPACE, "candidates_round: workspace");
+  hipLaunchKernelGGL(support_box_kernel, dim3(1), dim3(64), 0, s, spec->prior_kind,
+                     spec->prior_params, spec->d, box);
+  ABC_LAUNCHED();
+  const RoundArgs A = round_args(spec, box);
+  ABC_CHECK_ARG(nt < (1ll << 31), "candidates_round: too many tiles");
+  ABC_FUSED_DISPATCH(fused_round_kernel, dim3((unsigned)nt), s, A, idx0, B, eps, filt,
+                     bits, tcnt, rec_x);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(256), 0, s, tcnt, nt, count);
+  ABC_LAUNCHED();
+  if (cap > 0) {
+    const int64_t nwords = ceil_div(B, 64);
+    hipLaunchKernelGGL(bits_write_kernel, dim3((unsigned)ceil_div(nwords, 256)), dim3(256), 0,
+                       s, bits, nwords, tcnt, cap, idx);
+    ABC_LAUNCHED();
+  }
+  return ABC_OK;
+}
+
+extern "C" int abc_candidates_regen(const abc_candidate_spec* spec, int64_t idx0,
+                                    const int64_t* idx, int64_t n, double* theta,
+                                    double* prior_logpdf, int64_t* ancestor, double* x,
+                                    double* dist, void* stream) {
+  const int rc = check_spec(spec);
+  if (rc != ABC_OK) return rc;
+  ABC_CHECK_ARG(n >= 0, "candidates_regen: n < 0");
+  if (n == 0) return ABC_OK;
+  ABC_CHECK_ARG(idx && theta && prior_logpdf && x && dist, "candidates_regen: null pointer");
+  const RoundArgs A = round_args(spec, nullptr);  // box: per block, in LDS
+  hipStream_t s = as_stream(stream);
+  ABC_FUSED_DISPATCH(fused_regen_kernel, dim3((unsigned)ceil_div(n, 256)), s, A, idx0, idx, n,
+                     theta, prior_logpdf, ancestor, x, dist);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}

@@ -9,167 +9,10 @@
 // Here each stage is a coalesced kernel over a batch of B candidates whose
 // randomness is a pure function of (seed, generation, global index, slot):
 // results do not depend on batch size, rank count or scheduling.
-#include "abc_common.h"
+#include "abc_candidate.h"
 
 namespace abc {
 namespace {
-
-constexpr double LOG_SQRT_2PI = 0.91893853320467274178;
-constexpr uint32_t SLOTS_PER_ATTEMPT = 65536;
-constexpr uint32_t SLOT_ANCESTOR = 0;
-constexpr uint32_t SLOT_PERTURB = 1;     // 4 normals per slot
-constexpr uint32_t SLOT_PRIOR = 32;      // + 512 k + iteration
-constexpr uint32_t SLOT_SIM = 0x40000000u;
-
-// normals q .. q+3 of one slot
-__device__ __forceinline__ void normals4(uint64_t g, uint32_t slot, uint32_t gen,
-                                         uint64_t seed, double n[4]) {
-  u32x4 r = philox(g, slot, gen, seed);
-  box_muller(r.x, r.y, n[0], n[1]);
-  box_muller(r.z, r.w, n[2], n[3]);
-}
-
-// ---- priors (scipy.stats pdf conventions, closed support [a, b]) ----------
-__device__ double prior_logpdf1(int kind, const double* p, double x) {
-  switch (kind) {
-    case ABC_PRIOR_FLAT:
-      return 0.0;
-    case ABC_PRIOR_NORM: {
-      double y = (x - p[0]) / p[1];
-      return -0.5 * y * y - LOG_SQRT_2PI - log(p[1]);
-    }
-    case ABC_PRIOR_UNIFORM: {
-      double y = (x - p[0]) / p[1];
-      return (y >= 0.0 && y <= 1.0) ? -log(p[1]) : -INFINITY;
-    }
-    case ABC_PRIOR_EXPON: {
-      double y = (x - p[0]) / p[1];
-      return (y >= 0.0) ? -y - log(p[1]) : -INFINITY;
-    }
-    case ABC_PRIOR_LAPLACE: {
-      double y = (x - p[0]) / p[1];
-      return -fabs(y) - log(2.0 * p[1]);
-    }
-    case ABC_PRIOR_LOGNORM: {  // s, loc, scale
-      double y = (x - p[1]) / p[2];
-      if (!(y > 0.0)) return -INFINITY;
-      double ly = log(y) / p[0];
-      return -0.5 * ly * ly - log(p[0] * y) - LOG_SQRT_2PI - log(p[2]);
-    }
-    case ABC_PRIOR_GAMMA: {  // a, loc, scale
-      double a = p[0], y = (x - p[1]) / p[2];
-      if (y < 0.0) return -INFINITY;
-      if (y == 0.0) return a < 1.0 ? INFINITY : (a == 1.0 ? -log(p[2]) : -INFINITY);
-      return (a - 1.0) * log(y) - y - lgamma(a) - log(p[2]);
-    }
-    case ABC_PRIOR_BETA: {  // a, b, loc, scale
-      double a = p[0], b = p[1], y = (x - p[2]) / p[3];
-      if (y < 0.0 || y > 1.0) return -INFINITY;
-      double lb = lgamma(a) + lgamma(b) - lgamma(a + b);
-      double t1 = (a == 1.0) ? 0.0 : (a - 1.0) * log(y);
-      double t2 = (b == 1.0) ? 0.0 : (b - 1.0) * log1p(-y);
-      return t1 + t2 - lb - log(p[3]);
-    }
-  }
-  return NAN;
-}
-
-// Marsaglia-Tsang gamma(a, 1) draw; stream = (g, base + iteration)
-__device__ double gamma_draw(double a, uint64_t g, uint32_t base, uint32_t gen,
-                             uint64_t seed) {
-  double boost = 1.0;
-  uint32_t it = 0;
-  if (a < 1.0) {
-    u32x4 r = philox(g, base + 500, gen, seed);
-    boost = pow(uniform01(r.x), 1.0 / a);
-    a += 1.0;
-  }
-  const double dd = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * dd);
-  for (; it < 480; ++it) {
-    u32x4 r = philox(g, base + it, gen, seed);
-    double n0, n1;
-    box_muller(r.x, r.y, n0, n1);
-    double v = 1.0 + c * n0;
-    if (v <= 0.0) continue;
-    v = v * v * v;
-    double u = uniform01(r.z);
-    if (log(u) < 0.5 * n0 * n0 + dd - dd * v + dd * log(v)) return dd * v * boost;
-  }
-  return dd * boost;  // practically unreachable
-}
-
-__device__ double prior_draw1(int kind, const double* p, uint64_t g,
-                              uint32_t base, uint32_t gen, uint64_t seed) {
-  u32x4 r = philox(g, base, gen, seed);
-  double n0, n1;
-  switch (kind) {
-    case ABC_PRIOR_NORM:
-      box_muller(r.x, r.y, n0, n1);
-      return p[0] + p[1] * n0;
-    case ABC_PRIOR_UNIFORM:
-      return p[0] + p[1] * uniform53(r.x, r.y);
-    case ABC_PRIOR_EXPON:
-      return p[0] - p[1] * log(uniform01(r.x));
-    case ABC_PRIOR_LAPLACE: {
-      double u = uniform01(r.x) - 0.5;
-      return p[0] - p[1] * copysign(1.0, u) * log1p(-2.0 * fabs(u));
-    }
-    case ABC_PRIOR_LOGNORM:
-      box_muller(r.x, r.y, n0, n1);
-      return p[1] + p[2] * exp(p[0] * n0);
-    case ABC_PRIOR_GAMMA:
-      return p[1] + p[2] * gamma_draw(p[0], g, base + 1, gen, seed);
-    case ABC_PRIOR_BETA: {
-      double x = gamma_draw(p[0], g, base + 1, gen, seed);
-      double y = gamma_draw(p[1], g, base + 1 + 256, gen, seed);
-      return p[2] + p[3] * x / (x + y);
-    }
-  }
-  return NAN;
-}
-
-__device__ __forceinline__ double prior_logpdf(const int32_t* kind,
-                                               const double* params, int d,
-                                               const double* th) {
-  double s = 0.0;
-  for (int k = 0; k < d; ++k) s += prior_logpdf1(kind[k], params + 4 * k, th[k]);
-  return s;
-}
-
-__device__ __forceinline__ int64_t upper_bound(const double* cdf, int64_t N,
-                                               double target) {
-  int64_t lo = 0, hi = N;  // first index with cdf[idx] > target
-  while (lo < hi) {
-    int64_t mid = (lo + hi) >> 1;
-    if (cdf[mid] > target) hi = mid; else lo = mid + 1;
-  }
-  return lo < N ? lo : N - 1;
-}
-
-// One thread per candidate.  L: [d x d] row-major (per-particle when
-// per_particle_L, the LocalTransition Cholesky factors).  D > 0 fixes d at
-// compile time so the per-candidate vectors live in registers (D = 0: any
-// d <= 64, arrays in scratch).
-// Ancestor = first index with cdf > target (np.searchsorted side="right",
-// clamped to N - 1).  With a guide table (guide[k] = that index for the
-// target k * total / N, abc_cdf_guide) the search starts in a bracket of
-// ~3 table bins: O(1) expected instead of log2 N dependent loads.
-__device__ __forceinline__ int64_t ancestor_search(const double* __restrict__ cdf,
-                                                   const int32_t* __restrict__ guide,
-                                                   int64_t N, double total,
-                                                   double target) {
-  if (guide == nullptr) return upper_bound(cdf, N, target);
-  const double step = total / (double)N;
-  int64_t k = (int64_t)floor(target / step) - 1;  // t_k < target (one-bin margin)
-  k = k < 0 ? 0 : (k > N - 1 ? N - 1 : k);
-  int64_t lo = guide[k];
-  int64_t hi = k + 3 < N ? (int64_t)guide[k + 3] + 1 : N;  // t_{k+3} > target
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (cdf[mid] > target) hi = mid; else lo = mid + 1;
-  }
-  return lo < N ? lo : N - 1;
-}
 
 __global__ void cdf_guide_kernel(const double* __restrict__ cdf, int64_t N,
                                  int32_t* __restrict__ guide) {
@@ -180,69 +23,25 @@ __global__ void cdf_guide_kernel(const double* __restrict__ cdf, int64_t N,
   guide[k] = (int32_t)upper_bound(cdf, N, t);
 }
 
-template <int D, bool PER_PARTICLE_L>
+template <int D, int MODE>
 __global__ __launch_bounds__(256) void propose_kernel(
-    const double* __restrict__ X, const double* __restrict__ cdf,
-    const int32_t* __restrict__ guide, int64_t N,
-    int d_rt, const double* __restrict__ L, const int32_t* __restrict__ kind,
-    const double* __restrict__ params, uint64_t seed, uint32_t gen,
-    int64_t idx0, int64_t B, int max_attempts, double* __restrict__ theta,
+    ProposalArgs A, int64_t idx0, int64_t B, double* __restrict__ theta,
     double* __restrict__ lp_out, int64_t* __restrict__ anc_out,
     int32_t* __restrict__ att_out) {
   constexpr int DM = D > 0 ? D : 64;
-  const int d = D > 0 ? D : d_rt;
+  __shared__ double sbox[128];
+  const int d = D > 0 ? D : A.d;
+  support_box_block(A.kind, A.params, d, sbox);
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
-  const uint64_t g = (uint64_t)(idx0 + b);
   double th[DM];
-  double lp = -INFINITY;
-  int64_t j = -1;
-  int att = 0;
-  const double total = (X != nullptr) ? cdf[N - 1] : 0.0;
-  for (; att < max_attempts; ++att) {
-    const uint32_t s0 = (uint32_t)att * SLOTS_PER_ATTEMPT;
-    if (X == nullptr) {
+  int64_t j;
+  const int att = propose_one<D, MODE>(A, sbox, (uint64_t)(idx0 + b), th, j);
 #pragma unroll
-      for (int k = 0; k < DM; ++k)
-        if (k < d)
-          th[k] = prior_draw1(kind[k], params + 4 * k, g, s0 + SLOT_PRIOR + 512u * k, gen, seed);
-    } else {
-      u32x4 r = philox(g, s0 + SLOT_ANCESTOR, gen, seed);
-      j = ancestor_search(cdf, guide, N, total, uniform53(r.x, r.y) * total);
-      double n[(DM + 3) / 4 * 4];
-#pragma unroll
-      for (int q = 0; q < DM; q += 4) {
-        if (q < d) {
-          double n4[4];
-          normals4(g, s0 + SLOT_PERTURB + (uint32_t)(q >> 2), gen, seed, n4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) n[q + e] = n4[e];
-        }
-      }
-      const double* Lj = PER_PARTICLE_L ? L + j * d * d : L;
-#pragma unroll
-      for (int k = 0; k < DM; ++k) {
-        if (k < d) {
-          double acc = X[j * d + k];
-#pragma unroll
-          for (int q = 0; q < DM; ++q)
-            if (q < d) acc += Lj[k * d + q] * n[q];
-          th[k] = acc;
-        }
-      }
-    }
-    lp = 0.0;
-#pragma unroll
-    for (int k = 0; k < DM; ++k)
-      if (k < d) lp += prior_logpdf1(kind[k], params + 4 * k, th[k]);
-    if (lp > -INFINITY) break;  // prior density > 0 (smc.py:654-656)
-  }
-#pragma unroll
-  for (int k = 0; k < DM; ++k)
-    if (k < d) theta[b * d + k] = th[k];
-  lp_out[b] = lp;
+  for (int k = 0; k < (D > 0 ? D : d); ++k) theta[b * d + k] = th[k];
+  lp_out[b] = att <= A.max_attempts ? prior_logpdf(A.kind, A.params, d, th) : -INFINITY;
   if (anc_out) anc_out[b] = j;
-  if (att_out) att_out[b] = (lp > -INFINITY) ? att + 1 : max_attempts + 1;
+  if (att_out) att_out[b] = att;
 }
 
 template <bool PPL>
@@ -251,11 +50,15 @@ void launch_propose(int d, dim3 grid, hipStream_t s, const double* X,
                     const int32_t* kind, const double* params, uint64_t seed,
                     uint32_t gen, int64_t idx0, int64_t B, int max_attempts,
                     double* theta, double* lp, int64_t* anc, int32_t* att) {
-#define ABC_PROPOSE_CASE(DD)                                                     \
-  case DD:                                                                       \
-    hipLaunchKernelGGL((propose_kernel<DD, PPL>), grid, dim3(256), 0, s, X, cdf, \
-                       guide, N, d, L, kind, params, seed, gen, idx0, B,         \
-                       max_attempts, theta, lp, anc, att);                       \
+  const ProposalArgs A{X, cdf, guide, N, L, kind, params, d, max_attempts, seed, gen};
+#define ABC_PROPOSE_CASE(DD)                                                        \
+  case DD:                                                                          \
+    if (X == nullptr)                                                               \
+      hipLaunchKernelGGL((propose_kernel<DD, PROP_PRIOR>), grid, dim3(256), 0, s, A, \
+                         idx0, B, theta, lp, anc, att);                             \
+    else                                                                            \
+      hipLaunchKernelGGL((propose_kernel<DD, PPL ? PROP_LOCAL : PROP_MVN>), grid,    \
+                         dim3(256), 0, s, A, idx0, B, theta, lp, anc, att);         \
     break;
   switch (d) {
     ABC_PROPOSE_CASE(1) ABC_PROPOSE_CASE(2) ABC_PROPOSE_CASE(3)
@@ -296,10 +99,7 @@ __global__ __launch_bounds__(256) void simulate_lg_kernel(
   }
 }
 
-// ---- PNormDistance ---------------------------------------------------------
-__device__ __forceinline__ double pterm(double v, double p) {
-  return (p == 1.0) ? v : (p == 2.0 ? v * v : pow(v, p));
-}
+// ---- PNormDistance (pterm / pnorm_acc: abc_candidate.h) -------------------
 
 __global__ __launch_bounds__(256) void pnorm_row_kernel(
     const double* __restrict__ x, int64_t B, int S,
@@ -414,10 +214,27 @@ __global__ __launch_bounds__(CT_T) void accept_write_kernel(
     if (base + k < B && d[base + k] <= eps) idx[pos++] = base + k;
 }
 
+__global__ void mask_gave_up_kernel(double* __restrict__ d, const int32_t* __restrict__ att,
+                                    int64_t B, int max_attempts) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B && att[b] > max_attempts) d[b] = INFINITY;
+}
+
 }  // namespace
 }  // namespace abc
 
 using namespace abc;
+
+extern "C" int abc_mask_gave_up(double* dist, const int32_t* attempts, int64_t B,
+                                int max_attempts, void* stream) {
+  ABC_CHECK_ARG(B >= 0, "mask_gave_up: B < 0");
+  if (B == 0) return ABC_OK;
+  ABC_CHECK_ARG(dist && attempts, "mask_gave_up: null pointer");
+  hipLaunchKernelGGL(mask_gave_up_kernel, dim3((unsigned)ceil_div(B, 256)), dim3(256), 0,
+                     as_stream(stream), dist, attempts, B, max_attempts);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
 
 extern "C" int abc_cdf_guide(const double* cdf, int64_t N, int32_t* guide,
                              void* stream) {

@@ -82,6 +82,16 @@ class PNormDistance(Distance):
         wf = gpu.as_dev(self.weight_vector(t, keys), device=xmat.device)
         return gpu.pnorm(xmat, x0vec, wf, float(self.p), out=out)
 
+    def fused_pnorm(self, t, keys, device):
+        """(wf device [S], p) for the fused candidate kernel, or None when a
+        subclass replaced the distance itself."""
+        cls = type(self)
+        if cls.device_call is not PNormDistance.device_call or \
+                cls.__call__ is not PNormDistance.__call__ or \
+                cls.weight_vector is not PNormDistance.weight_vector:
+            return None
+        return gpu.as_dev(self.weight_vector(t, keys), device=device), float(self.p)
+
     # -- reference per-particle interface ----------------------------------
     def __call__(self, x: dict, x_0: dict, t: int = None, par: dict = None):
         self.format_weights_and_factors(t, x_0.keys())

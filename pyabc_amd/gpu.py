@@ -250,6 +250,13 @@ def pnorm(x, x0, wf, pval, out=None):
     return out
 
 
+def mask_gave_up(dist, att, max_attempts):
+    """dist[b] = +inf where att[b] > max_attempts (in place)."""
+    nat.call("abc_mask_gave_up", p(dist), p(att), dist.numel(), int(max_attempts),
+             stream_ptr())
+    return dist
+
+
 def accept_compact(d, eps, idx_out=None, count_out=None):
     B = d.numel()
     idx = torch.empty(max(B, 1), dtype=I64, device=d.device) if idx_out is None else idx_out
@@ -259,6 +266,76 @@ def accept_compact(d, eps, idx_out=None, count_out=None):
     nat.call("abc_accept_compact", p(d), B, float(eps), p(idx), p(cnt), p(ws),
              ws.numel(), stream_ptr())
     return idx, cnt
+
+
+class CandidateRound:
+    """The device description of one generation's candidate closure for the
+    fused kernels (abc_candidate_spec): proposal (MVN / LocalTransition
+    arrays, or X=None for the prior), LinearGaussianModel (src, a, sigma),
+    PNormDistance (x0, wf, p).  Holds the tensors the struct points to."""
+
+    def __init__(self, d, S, prior_kind, prior_params, src, a, sigma, x0, wf,
+                 p, seed, generation, max_attempts, X=None, cdf=None,
+                 guide=None, L=None, per_particle_L=False):
+        self._keep = [t for t in (prior_kind, prior_params, src, a, sigma, x0,
+                                  wf, X, cdf, guide, L) if t is not None]
+        for t in self._keep:
+            assert t.is_contiguous() and t.is_cuda
+        if src.dtype != torch.int32 or prior_kind.dtype != torch.int32:
+            raise TypeError("CandidateRound: src / prior_kind must be int32")
+        self.d, self.S = int(d), int(S)
+        self.spec = nat.CandidateSpec()
+        s = self.spec
+        s.d, s.S = self.d, self.S
+        s.X, s.cdf, s.guide = _ptr(X), _ptr(cdf), _ptr(guide)
+        s.N = 0 if X is None else int(X.shape[0])
+        s.L, s.per_particle_L = _ptr(L), int(bool(per_particle_L))
+        s.prior_kind, s.prior_params = _ptr(prior_kind), _ptr(prior_params)
+        s.max_attempts = int(max_attempts)
+        s.src, s.a, s.sigma = _ptr(src), _ptr(a), _ptr(sigma)
+        s.x0, s.wf, s.p = _ptr(x0), _ptr(wf), float(p)
+        s.seed = int(seed) & (2 ** 64 - 1)
+        s.generation = int(generation) & 0xFFFFFFFF
+        self.device = prior_params.device
+
+    def run(self, idx0, B, eps, cap, filter=True, rec_x=None, idx_out=None,
+            count_out=None):
+        """One round (abc_candidates_round): (idx [cap] int64 positions of the
+        first cap accepted, count [1] int64 accepted in the round)."""
+        import ctypes as C
+        idx = (torch.empty(max(int(cap), 1), dtype=I64, device=self.device)
+               if idx_out is None else idx_out)
+        cnt = (torch.empty(1, dtype=I64, device=self.device)
+               if count_out is None else count_out)
+        if rec_x is not None and tuple(rec_x.shape) != (int(B), self.S):
+            raise ValueError("CandidateRound.run: rec_x must be [B, S]")
+        nb = nat.query("abc_candidates_workspace", int(B))
+        ws = workspace(nb, "candidates")
+        nat.call("abc_candidates_round", C.addressof(self.spec), int(idx0), int(B),
+                 float(eps), int(bool(filter)), int(cap), p(idx), p(cnt), p(rec_x),
+                 p(ws), ws.numel(), stream_ptr())
+        return idx, cnt
+
+    def regen(self, idx0, idx):
+        """Rows of the candidates idx0 + idx[i] (abc_candidates_regen):
+        theta [n, d], prior log-density [n], ancestor [n], x [n, S], dist [n]."""
+        import ctypes as C
+        n = int(idx.numel())
+        dev = self.device
+        theta = torch.empty((n, self.d), dtype=F64, device=dev)
+        lp = torch.empty(n, dtype=F64, device=dev)
+        anc = torch.empty(n, dtype=I64, device=dev)
+        x = torch.empty((n, self.S), dtype=F64, device=dev)
+        dist = torch.empty(n, dtype=F64, device=dev)
+        if n:
+            nat.call("abc_candidates_regen", C.addressof(self.spec), int(idx0),
+                     p(idx.contiguous()), n, p(theta), p(lp), p(anc), p(x), p(dist),
+                     stream_ptr())
+        return theta, lp, anc, x, dist
+
+
+def _ptr(t):
+    return None if t is None else p(t)
 
 
 def gather_rows(x, idx, n=None):

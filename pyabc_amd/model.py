@@ -119,6 +119,8 @@ class LinearGaussianModel(VectorizedModel):
                       else np.asarray(sigma, dtype=np.float64))
         if not (len(self.src) == len(self.a) == len(self.sigma) == S):
             raise ValueError("src, a, sigma need one entry per sum stat")
+        if S and (self.src.min() < 0 or self.src.max() >= len(self.parameter_names)):
+            raise ValueError("src entries must index the parameters")
         self._dev = None
 
     def _device_arrays(self, device):
@@ -128,6 +130,14 @@ class LinearGaussianModel(VectorizedModel):
                          gpu.as_dev(self.a, device=device),
                          gpu.as_dev(self.sigma, device=device))
         return self._dev
+
+    def fused_simulator(self, device):
+        """(src int32, a, sigma) device arrays for the fused candidate kernel
+        (abc_candidate_spec); None when a subclass replaced the simulator."""
+        if type(self)._run is not LinearGaussianModel._run or \
+                type(self).simulate_batch is not VectorizedModel.simulate_batch:
+            return None
+        return self._device_arrays(device)
 
     def _run(self, theta, seed, generation, idx0):
         from . import gpu

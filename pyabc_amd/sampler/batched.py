@@ -115,13 +115,26 @@ class BatchedGPUSampler(Sampler):
     """
 
     def __init__(self, batch_size=None, max_batch_size=1 << 22, seed=None,
-                 max_attempts=10000, check_max_eval=False):
+                 max_attempts=10000, check_max_eval=False, fused=True,
+                 max_fused_batch_size=1 << 31, filter_below=0.15,
+                 record_budget_bytes=1 << 31):
         super().__init__()
         self.check_max_eval = check_max_eval
         self.batch_size = batch_size
         self.max_batch_size = max_batch_size
         self.seed = seed
         self.max_attempts = max_attempts
+        # fused candidate rounds (abc_candidates_round): one kernel per round,
+        # one accept bit per candidate, accepted rows regenerated; used when
+        # the model is a LinearGaussianModel, the distance a PNormDistance,
+        # the acceptor uniform and the transition an MVN / LocalTransition
+        self.fused = fused
+        self.max_fused_batch_size = max_fused_batch_size
+        self.filter_below = filter_below          # early-reject mode below this rate
+        self.record_budget_bytes = record_budget_bytes  # rec rows per fused round
+        # first m recorded candidates are all that is used
+        # (ABCSMC.max_nr_recorded_particles, smc.py:998-1001)
+        self.max_nr_recorded = np.inf
         self._acc_rate = None
         self.last_stats = {}
 
@@ -153,6 +166,9 @@ class BatchedGPUSampler(Sampler):
         gen = spec.t & 0xFFFFFFFF
         record = self.sample_factory.record_rejected
         d = len(spec.param_names)
+        fr = None if all_accepted else self._fused_round(spec, seed, gen, dev)
+        if fr is not None:
+            return self._sample_fused(n, fr, spec, max_eval, record, dev, rank, ws)
 
         acc_theta, acc_lp, acc_d, acc_x, acc_anc, acc_w = [], [], [], [], [], []
         rec_x = []
@@ -162,6 +178,7 @@ class BatchedGPUSampler(Sampler):
         rec_extra = [] if (stochastic and record) else None
         keeps = []          # per round: accepted rows kept by each rank
         rec_keeps = []      # per round: recorded rows of each rank
+        rec_left = self.max_nr_recorded
         n_acc = 0
         base = 0
         n_eval = 0
@@ -171,9 +188,10 @@ class BatchedGPUSampler(Sampler):
             if self.check_max_eval and n_eval >= max_eval:
                 ok = False
                 break
-            B = self._round_size(n - n_acc, ws)
+            B = self._limit_to_max_eval(self._round_size(n - n_acc, ws), max_eval,
+                                        n_eval, ws)
             lo, _ = dd.rank_range(base, B, rank)
-            theta, lp, anc = self._propose(spec, B, seed, gen, lo, d)
+            theta, lp, anc, att = self._propose(spec, B, seed, gen, lo, d)
             x = spec.model.simulate_batch(theta, seed, gen, lo)
             if all_accepted or spec.distance is None:
                 dist = gpu.torch.full((B,), np.inf, dtype=gpu.F64, device=dev)
@@ -182,6 +200,11 @@ class BatchedGPUSampler(Sampler):
             else:
                 dist = spec.distance.device_call(x, spec.x0vec, spec.t,
                                                  spec.sum_stat_keys)
+                # a proposal that exhausted max_attempts never enters the
+                # population (the reference loops until the prior density is
+                # positive, smc.py:649-662)
+                if att is not None:
+                    gpu.mask_gave_up(dist, att, self.max_attempts)
                 if stochastic:
                     key, accw = gpu.stochastic_accept(dist, *spec.stochastic,
                                                       seed, gen, lo)
@@ -232,7 +255,9 @@ class BatchedGPUSampler(Sampler):
                 if stochastic:
                     acc_w.append(got[-1])
             if record:
-                rec_x.append(x[:rec_rows])
+                rec_all, rec_left = self._cap_records(rec_all, rec_left)
+                rec_rows = int(rec_all[rank])
+                rec_x.append(x[:rec_rows].clone() if rec_rows < B // 2 else x[:rec_rows])
                 rec_keeps.append(rec_all)
                 if rec_extra is not None:
                     rec_extra.append((theta[:rec_rows], dist[:rec_rows],
@@ -267,6 +292,160 @@ class BatchedGPUSampler(Sampler):
         return ColumnarSample(cols, recorded, spec.sum_stat_keys,
                               record, ok and n_acc == n, records=records)
 
+    # ---- fused candidate rounds ------------------------------------------
+    def _fused_round(self, spec, seed, gen, dev):
+        """gpu.CandidateRound of this generation, or None when some piece has
+        no fused form (custom simulator / distance, stochastic acceptor)."""
+        if not self.fused or getattr(spec, "stochastic", None) is not None \
+                or spec.distance is None:
+            return None
+        sim = (spec.model.fused_simulator(dev)
+               if hasattr(spec.model, "fused_simulator") else None)
+        fp = (spec.distance.fused_pnorm(spec.t, spec.sum_stat_keys, dev)
+              if hasattr(spec.distance, "fused_pnorm") else None)
+        if sim is None or fp is None:
+            return None
+        prop = {}
+        if spec.transition is not None:
+            arrays = getattr(spec.transition, "proposal_arrays", None)
+            if arrays is None:
+                return None
+            prop = arrays()
+        src, a, sigma = sim
+        wf, pval = fp
+        return gpu.CandidateRound(len(spec.param_names), len(spec.sum_stat_keys),
+                                  spec.prior_kind, spec.prior_params, src, a,
+                                  sigma, spec.x0vec, wf, pval, seed, gen,
+                                  self.max_attempts, **prop)
+
+    def _fused_size(self, need, ws, rate, measured, S, record):
+        """Candidates per rank for the next fused round: need / rate, with a
+        6% margin once the rate was measured in this generation (the previous
+        generation's rate is optimistic as eps shrinks, so the first round
+        rarely overshoots), capped by the launch and record budgets."""
+        if self.batch_size is not None:
+            return int(self.batch_size)
+        r = rate if rate else 0.5
+        b = need / max(r, 1e-12) * (1.06 if measured else 1.0) / ws + 4096
+        cap = self.max_fused_batch_size
+        if record:
+            cap = min(cap, max(self.record_budget_bytes // (8 * S), 4096))
+        return int(min(max(b, 4096), cap))
+
+    def _limit_to_max_eval(self, B, max_eval, n_eval, ws):
+        """With check_max_eval no round goes past max_eval evaluations
+        (singlecore.py:25-31 checks before every simulation; with several
+        ranks the overshoot is below one candidate per rank)."""
+        if not self.check_max_eval or not np.isfinite(max_eval):
+            return B
+        left = int(math.ceil(max_eval)) - int(n_eval)
+        return int(max(1, min(B, left // ws)))
+
+    def _cap_records(self, rec_all, rec_left):
+        """Keep only the first max_nr_recorded recorded candidates in global
+        order (round-major, then rank); returns (rows per rank, rows left)."""
+        if not np.isfinite(rec_left):
+            return rec_all, rec_left
+        out = np.zeros_like(rec_all)
+        left = int(rec_left)
+        for q in range(len(rec_all)):
+            out[q] = min(int(rec_all[q]), left)
+            left -= int(out[q])
+        return out, left
+
+    def _sample_fused(self, n, fr, spec, max_eval, record, dev, rank, ws):
+        """sample_until_n_accepted on fused rounds: per round one
+        abc_candidates_round launch (accept bits -> indices of the first
+        `need` accepted) and one host read; the kept rows are regenerated
+        (abc_candidates_regen) bit-identical to the staged kernels."""
+        torch = gpu.torch
+        S = len(spec.sum_stat_keys)
+        cols = {k: [] for k in ("theta", "lp", "dist", "x", "anc")}
+        rec_x, rec_keeps, keeps = [], [], []
+        rec_left = self.max_nr_recorded
+        n_acc = n_eval = base = rounds = 0
+        ok = True
+        rate, measured = self._acc_rate, False
+        tot_B = tot_cnt = 0
+        filtered = 0
+        while n_acc < n:
+            if self.check_max_eval and n_eval >= max_eval:
+                ok = False
+                break
+            need = n - n_acc
+            B = self._limit_to_max_eval(self._fused_size(need, ws, rate, measured, S, record),
+                                        max_eval, n_eval, ws)
+            lo, _ = dd.rank_range(base, B, rank)
+            rx = (torch.empty((B, S), dtype=gpu.F64, device=dev)
+                  if record and rec_left > 0 else None)
+            filt = rate is not None and rate < self.filter_below and rx is None
+            filtered += int(filt)
+            idx, cnt = fr.run(lo, B, spec.eps, cap=need, filter=filt, rec_x=rx)
+            if ws == 1:
+                # one read: the count and the index of the need-th accepted
+                kk = min(need, B)
+                both = torch.cat([cnt.view(1), idx[kk - 1:kk]]).cpu()
+                cnt_local, pos_hint = int(both[0]), int(both[1])
+            else:
+                cnt_local = cnt
+            counts = dd.allgather_counts(cnt_local, dev)
+            keep = dd.cutoff(counts, need)
+            total_keep = int(keep.sum())
+            k_mine = int(keep[rank])
+            rec_all = np.full(ws, B, dtype=np.int64)
+            if n_acc + total_keep >= n:
+                c_rank = int(np.nonzero(keep)[0][-1])
+                if ws == 1:
+                    pos = pos_hint
+                else:
+                    pos = self._local_cutoff_pos(idx, keep[c_rank]) if rank == c_rank else -1
+                    pos = dd.allgather_counts(pos, dev)[c_rank]
+                evaluated = c_rank * B + pos + 1
+                rec_all[c_rank] = pos + 1
+                rec_all[c_rank + 1:] = 0
+            else:
+                evaluated = ws * B
+            if k_mine:
+                th, lp, anc, x, dist = fr.regen(lo, idx[:k_mine])
+                for k, v in zip(("theta", "lp", "dist", "x", "anc"),
+                                (th, lp, dist, x, anc)):
+                    cols[k].append(v)
+            if record:
+                if rx is None:
+                    rec_all = np.zeros(ws, dtype=np.int64)
+                rec_all, rec_left = self._cap_records(rec_all, rec_left)
+                rr = int(rec_all[rank])
+                if rx is not None:
+                    rec_x.append(rx[:rr].clone() if rr < B // 2 else rx[:rr])
+                rec_keeps.append(rec_all)
+            keeps.append(keep)
+            n_acc += total_keep
+            n_eval += evaluated
+            base += ws * B
+            rounds += 1
+            tot_B += ws * B
+            tot_cnt += int(counts.sum())
+            rate, measured = max(int(counts.sum()) / float(ws * B), 1e-12), True
+        self._acc_rate = max(tot_cnt / float(max(tot_B, 1)), 1e-12)
+        self.nr_evaluations_ = int(n_eval)
+        self.last_stats = dict(rounds=rounds, evaluations=int(n_eval),
+                               accepted=int(n_acc), fused=True,
+                               candidates=int(tot_B), filtered_rounds=filtered)
+        if n_acc < n:
+            ok = False
+        out = self._assemble(spec, cols["theta"], cols["lp"], cols["dist"],
+                             cols["x"], dev, fr.d, False, keeps,
+                             cols["anc"] if spec.transition is not None else ())
+        recorded = None
+        if record:
+            recorded = self._gather_recorded(rec_x, rec_keeps, dev, ws)
+            if recorded is None:
+                recorded = torch.empty((0, S), dtype=gpu.F64, device=dev)
+        elif out is not None:
+            recorded = out.sum_stats
+        return ColumnarSample(out, recorded, spec.sum_stat_keys, record,
+                              ok and n_acc == n)
+
     def _gather_recorded(self, pieces, rec_keeps, dev, ws):
         """Concatenate this rank's recorded rows and, over several ranks,
         all-gather them back into global candidate-index order."""
@@ -291,7 +470,7 @@ class BatchedGPUSampler(Sampler):
             th, lp, anc, att = spec.transition.propose_device(
                 B, spec.prior_kind, spec.prior_params, seed=seed,
                 generation=gen, idx0=lo, max_attempts=self.max_attempts)
-        return th, lp, anc
+        return th, lp, anc, att
 
     @staticmethod
     def global_order(keeps):

@@ -475,6 +475,9 @@ class ABCSMC:
         self._initialize_dist_eps_acc(t0)
         self.distance_function.configure_sampler(self.sampler)
         self.eps.configure_sampler(self.sampler)
+        if hasattr(self.sampler, "max_nr_recorded"):
+            # the batched sampler keeps only the recorded rows that are used
+            self.sampler.max_nr_recorded = self.max_nr_recorded_particles
         t_max = t0 + max_nr_populations - 1
         t = t0
         while t <= t_max:

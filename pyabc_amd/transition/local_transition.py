@@ -134,6 +134,12 @@ class LocalTransition(Transition):
                            idx0, B, max_attempts, d, per_particle_L=True,
                            guide=self._dev_guide)
 
+    def proposal_arrays(self):
+        """Device arrays for the fused candidate kernel: per-particle
+        Cholesky factors (local_transition.py:141-145)."""
+        return dict(X=self._dev_X, cdf=self._dev_cdf, guide=self._dev_guide,
+                    L=self._dev_chol, per_particle_L=True)
+
     def rvs_single(self):
         theta = self.propose_device(1)[0].cpu().numpy()[0]
         return pd.Series(theta, index=self.X.columns)

@@ -222,6 +222,12 @@ class MultivariateNormalTransition(Transition):
                            generation, idx0, B, max_attempts, d,
                            guide=self._dev_guide)
 
+    def proposal_arrays(self):
+        """Device arrays of the proposal for the fused candidate kernel
+        (abc_candidate_spec): population, weight scan, guide, shared L."""
+        return dict(X=self._dev_X, cdf=self._dev_cdf, guide=self._dev_guide,
+                    L=self._dev_L, per_particle_L=False)
+
     def rvs(self, size: int = None) -> Union[pd.Series, pd.DataFrame]:
         n = 1 if size is None else size
         theta = self.propose_device(n)[0].cpu().numpy()

@@ -1,0 +1,269 @@
+"""Fused candidate rounds (abc_candidates_round / abc_candidates_regen).
+
+The fused kernel runs the per-candidate closure (pyabc/smc.py:588-724:
+proposal + prior re-draw, LinearGaussianModel, PNormDistance, d <= eps) in
+one launch and keeps one accept bit per candidate; accepted rows are
+regenerated.  Parity bar: the accept set, ancestors, theta, prior
+log-density, sum stats and distances are BIT-IDENTICAL to the staged kernels
+(abc_propose -> abc_simulate_linear_gaussian -> abc_pnorm ->
+abc_accept_compact) on the same inputs (distances of rows wider than 32
+statistics to 1e-13: abc_pnorm sums those in another order), in plain and
+early-reject (filter)
+modes, for the MVN, LocalTransition and prior (t = 0) proposals; and the
+accept set equals the numpy oracle's replay of the same Philox streams away
+from |d - eps| < 1e-12 (oracle/sampler.py).
+"""
+import numpy as np
+import pytest
+
+import oracle
+import oracle.sampler as osamp
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from pyabc_amd import gpu
+    return gpu.require_device()
+
+
+def T(a, dtype=None):
+    from pyabc_amd import gpu
+    return gpu.as_dev(a, dtype=dtype)
+
+
+KIND = {"norm": 0, "uniform": 1, "expon": 2, "laplace": 3, "lognorm": 4,
+        "gamma": 5, "beta": 6}
+
+
+def _case(d, S, N=3000, mode="mvn", seed=0, kinds=None, params=None, p=2.0,
+          src=None, a=None, sigma=None, x0=1.0):
+    """Device arrays of one generation's closure + the staged reference."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(seed)
+    X = rng.normal(0.5, 0.8, (N, d))
+    w = np.exp(0.5 * rng.standard_normal(N))
+    w /= w.sum()
+    kinds = kinds or ["norm"] * d
+    params = (np.tile([0.0, 1.0, 0, 0], (d, 1)) if params is None
+              else np.asarray(params, float))
+    src = np.arange(S) % d if src is None else np.asarray(src)
+    a = np.ones(S) if a is None else np.asarray(a, float)
+    sigma = np.full(S, 0.5) if sigma is None else np.asarray(sigma, float)
+    wf = np.ones(S)
+    c = dict(d=d, S=S, kind=T([KIND[k] for k in kinds], torch.int32),
+             params=T(params.ravel()), src=T(src, torch.int32), a=T(a),
+             sigma=T(sigma), x0=T(np.full(S, x0)), wf=T(wf), p=p,
+             host=dict(X=X, w=w, kinds=kinds, params=params, src=src, a=a,
+                       sigma=sigma, x0=np.full(S, x0), wf=wf))
+    if mode == "prior":
+        c.update(X=None, cdf=None, guide=None, L=None, ppl=False)
+        return c
+    Xd, wd = T(X), T(w)
+    cdf = gpu.inclusive_scan(wd)
+    c.update(X=Xd, cdf=cdf, guide=gpu.cdf_guide(cdf))
+    if mode == "mvn":
+        Lh = np.linalg.cholesky(0.2 * np.eye(d) + 0.05)
+        c.update(L=T(Lh), ppl=False)
+        c["host"]["L"] = Lh
+    else:   # per-particle factors (LocalTransition)
+        A = rng.normal(0, 0.3, (N, d, d))
+        cov = A @ np.transpose(A, (0, 2, 1)) + 0.05 * np.eye(d)
+        Lh = np.linalg.cholesky(cov)
+        c.update(L=T(Lh), ppl=True)
+        c["host"]["L"] = Lh
+    return c
+
+
+def _round(c, seed=11, gen=3, max_attempts=1000):
+    from pyabc_amd import gpu
+    return gpu.CandidateRound(c["d"], c["S"], c["kind"], c["params"], c["src"],
+                              c["a"], c["sigma"], c["x0"], c["wf"], c["p"],
+                              seed, gen, max_attempts, X=c["X"], cdf=c["cdf"],
+                              guide=c["guide"], L=c["L"],
+                              per_particle_L=c["ppl"])
+
+
+def _staged(c, lo, B, eps, seed=11, gen=3, max_attempts=1000):
+    from pyabc_amd import gpu
+    th, lp, anc, att = gpu.propose(c["X"], c["cdf"], c["L"], c["kind"], c["params"],
+                                   seed, gen, lo, B, max_attempts, c["d"],
+                                   per_particle_L=c["ppl"], guide=c["guide"])
+    x = gpu.simulate_linear_gaussian(th, c["src"], c["a"], c["sigma"], seed, gen, lo)
+    dist = gpu.pnorm(x, c["x0"], c["wf"], c["p"])
+    gpu.mask_gave_up(dist, att, max_attempts)
+    idx, cnt = gpu.accept_compact(dist, eps)
+    n = int(cnt.cpu())
+    return dict(theta=th, lp=lp, anc=anc, x=x, dist=dist, idx=idx[:n], n=n)
+
+
+def _eps_for(dist, rate):
+    return float(torch.quantile(dist[torch.isfinite(dist)][:200000], rate))
+
+
+def _check_equal(c, fr, ref, lo, B, eps, filt):
+    idx, cnt = fr.run(lo, B, eps, cap=max(ref["n"], 1), filter=filt)
+    n = int(cnt.cpu())
+    assert n == ref["n"]
+    assert torch.equal(idx[:n], ref["idx"])
+    th, lp, anc, x, dist = fr.regen(lo, idx[:n])
+    sel = ref["idx"]
+    assert torch.equal(th, ref["theta"][sel])
+    assert torch.equal(x, ref["x"][sel])
+    if c["S"] <= 32:
+        assert torch.equal(dist, ref["dist"][sel])
+    else:   # abc_pnorm sums wide rows lane-strided + wave tree (other order)
+        torch.testing.assert_close(dist, ref["dist"][sel], rtol=1e-13, atol=0)
+    assert torch.equal(lp, ref["lp"][sel])
+    if c["X"] is not None:
+        assert torch.equal(anc, ref["anc"][sel])
+    return n
+
+
+@pytest.mark.parametrize("mode,d,S", [("mvn", 10, 10), ("mvn", 1, 1), ("mvn", 3, 7),
+                                      ("local", 5, 5), ("prior", 10, 10),
+                                      ("mvn", 4, 256), ("mvn", 7, 13)])
+@pytest.mark.parametrize("rate", [0.3, 0.01])
+def test_fused_equals_staged(dev, mode, d, S, rate):
+    c = _case(d, S, mode=mode, seed=d + S)
+    lo, B = 123_456_789, 100_003
+    probe = _staged(c, lo, B, np.inf)
+    eps = _eps_for(probe["dist"], rate)
+    ref = _staged(c, lo, B, eps)
+    fr = _round(c)
+    for filt in (False, True):
+        n = _check_equal(c, fr, ref, lo, B, eps, filt)
+    assert n > 0
+
+
+@pytest.mark.parametrize("p", [1.0, np.inf, 3.0])
+def test_fused_pnorm_orders(dev, p):
+    c = _case(6, 11, p=p, seed=5)
+    lo, B = 0, 50_000
+    eps = _eps_for(_staged(c, lo, B, np.inf)["dist"], 0.05)
+    ref = _staged(c, lo, B, eps)
+    fr = _round(c)
+    for filt in (False, True):
+        _check_equal(c, fr, ref, lo, B, eps, filt)
+
+
+def test_fused_prior_kinds_and_gave_up(dev):
+    """Bounded priors: proposals outside the support are re-drawn with the
+    same streams; with max_attempts = 2 some exhaust it and are rejected in
+    both paths (never accepted with zero prior density)."""
+    kinds = ["uniform", "expon", "gamma", "beta", "lognorm", "laplace"]
+    params = [[0.0, 1.0, 0, 0], [0.2, 0.5, 0, 0], [2.0, 0.0, 1.0, 0],
+              [2.0, 3.0, 0.0, 1.0], [0.5, 0.0, 1.0, 0], [0.0, 1.0, 0, 0]]
+    c = _case(6, 6, kinds=kinds, params=params, seed=9)
+    c["host"]["X"] = np.abs(c["host"]["X"]) * 0.5 + 0.1
+    from pyabc_amd import gpu
+    c["X"] = T(c["host"]["X"])
+    lo, B = 77, 60_000
+    for max_att in (1000, 2):
+        ref = _staged(c, lo, B, 1e300, max_attempts=max_att)
+        fr = _round(c, max_attempts=max_att)
+        n = _check_equal(c, fr, ref, lo, B, 1e300, False)
+        if max_att == 2:
+            assert 0 < n < B     # some gave up and were rejected
+        assert torch.isfinite(fr.regen(lo, ref["idx"][:1000])[1]).all()
+    # prior mode (t = 0) with the same bounded kinds
+    c0 = _case(6, 6, mode="prior", kinds=kinds, params=params, seed=9)
+    ref = _staged(c0, lo, B, 1e300)
+    _check_equal(c0, _round(c0), ref, lo, B, 1e300, False)
+
+
+def test_fused_edges(dev):
+    """Ragged B (1, 63, 64, 65, 2047, 2049), cap below the count, count 0,
+    record rows for every candidate."""
+    c = _case(3, 4, seed=1)
+    fr = _round(c)
+    for B in (1, 63, 64, 65, 2047, 2049, 10_000):
+        ref = _staged(c, 5, B, 1.0)
+        idx, cnt = fr.run(5, B, 1.0, cap=max(ref["n"], 1))
+        assert int(cnt.cpu()) == ref["n"]
+        assert torch.equal(idx[:ref["n"]], ref["idx"])
+    ref = _staged(c, 5, 10_000, 1.5)
+    assert ref["n"] > 20
+    idx, cnt = fr.run(5, 10_000, 1.5, cap=7)
+    assert int(cnt.cpu()) == ref["n"] and torch.equal(idx[:7], ref["idx"][:7])
+    idx, cnt = fr.run(5, 10_000, -1.0, cap=3)
+    assert int(cnt.cpu()) == 0
+    rec = torch.empty((10_000, 4), dtype=torch.float64, device=dev)
+    idx, cnt = fr.run(5, 10_000, 1.5, cap=ref["n"], rec_x=rec)
+    assert torch.equal(rec, ref["x"]) and int(cnt.cpu()) == ref["n"]
+
+
+def test_fused_vs_oracle_replay(dev):
+    """Accept set against the numpy oracle's replay of the same streams
+    (theta, x to 1e-12; masks equal away from |d - eps| < 1e-12)."""
+    c = _case(10, 10, N=2000, seed=4)
+    h = c["host"]
+    lo, B, seed, gen = 999, 20_000, 11, 3
+    th, lp, anc, att = osamp.propose_mvn(h["X"], h["w"], h["L"], seed, gen, lo, B,
+                                         h["kinds"], h["params"])
+    x = osamp.simulate_linear_gaussian(th, h["src"], h["a"], h["sigma"], seed, gen, lo)
+    d = oracle.pnorm(x, h["x0"], p=2)
+    eps = float(np.quantile(d, 0.05))
+    fr = _round(c)
+    idx, cnt = fr.run(lo, B, eps, cap=B)
+    n = int(cnt.cpu())
+    got = np.zeros(B, bool)
+    got[idx[:n].cpu().numpy()] = True
+    want = d <= eps
+    near = np.abs(d - eps) < 1e-12
+    assert np.array_equal(got[~near], want[~near])
+    tg, lpg, ancg, xg, dg = fr.regen(lo, idx[:n])
+    sel = idx[:n].cpu().numpy()
+    np.testing.assert_array_equal(ancg.cpu().numpy(), anc[sel])
+    np.testing.assert_allclose(tg.cpu().numpy(), th[sel], rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(xg.cpu().numpy(), x[sel], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(dg.cpu().numpy(), d[sel], rtol=1e-12)
+    np.testing.assert_allclose(lpg.cpu().numpy(), lp[sel], rtol=1e-12)
+
+
+def _abc(fused, adaptive=False, pop=4000, max_fused=1 << 31, local=False, S=10):
+    import pyabc_amd as pa
+    d = 4 if local else 10
+    names = [f"p{k}" for k in range(d)]
+    keys = [f"y{k}" for k in range(S)]
+    rng = np.random.default_rng(1234)
+    model = pa.LinearGaussianModel(names, keys, src=[k % d for k in range(S)],
+                                   a=rng.uniform(0.5, 2, S),
+                                   sigma=10 ** rng.uniform(-1, 0.5, S))
+    prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
+    dist = (pa.AdaptivePNormDistance(p=2) if adaptive else pa.PNormDistance(p=2))
+    tr = pa.LocalTransition(k=50, k_fraction=None) if local else pa.MultivariateNormalTransition()
+    sampler = pa.BatchedGPUSampler(seed=77, fused=fused,
+                                   max_fused_batch_size=max_fused)
+    np.random.seed(3)
+    abc = pa.ABCSMC(model, prior, dist, population_size=pop, transitions=tr,
+                    eps=pa.QuantileEpsilon(alpha=0.5), sampler=sampler)
+    abc.new("sqlite://", {k: 0.5 for k in keys})
+    return abc
+
+
+@pytest.mark.parametrize("adaptive,local,max_fused,S",
+                         [(False, False, 1 << 31, 10), (True, False, 1 << 31, 24),
+                          (False, False, 5000, 10), (False, True, 1 << 31, 6)])
+def test_sampler_fused_equals_staged(dev, adaptive, local, max_fused, S):
+    """Whole generations: fused and staged samplers give the same populations,
+    weights, epsilons and evaluation counts (several rounds per generation
+    with a small fused batch)."""
+    runs = []
+    for fused in (False, True):
+        abc = _abc(fused, adaptive=adaptive, max_fused=max_fused, local=local, S=S)
+        h = abc.run(max_nr_populations=4)
+        pops = [h.get_population_device(t) for t in range(h.max_t + 1)]
+        runs.append((abc, pops, [g["n_sim"] for g in abc.generation_log],
+                     [g["eps"] for g in abc.generation_log]))
+        if fused:
+            assert abc.sampler.last_stats.get("fused")
+    (_, p0, n0, e0), (_, p1, n1, e1) = runs
+    assert n0 == n1 and e0 == e1
+    for a, b in zip(p0, p1):
+        assert torch.equal(a.theta, b.theta)
+        assert torch.equal(a.weights, b.weights)
+        assert torch.equal(a.distances, b.distances)
+        assert torch.equal(a.sum_stats, b.sum_stats)
