@@ -106,6 +106,12 @@ class KernelTimer:
         nat.call("abc_profile_end", ctypes.addressof(ms), ctypes.addressof(n))
         flops = sum(2.0 * d * M * N for (M, N, d) in self.shapes)
         pairs = sum(M * N for (M, N, d) in self.shapes)
+        self.channels = {}
+        for name, ch in (("candidates", nat.ABC_PROF_CANDIDATES),
+                         ("regen", nat.ABC_PROF_REGEN)):
+            cm, cn = ctypes.c_double(0.0), ctypes.c_int64(0)
+            nat.call("abc_profile_channel", ch, ctypes.addressof(cm), ctypes.addressof(cn))
+            self.channels[name] = (cm.value, int(cn.value))
         return ms.value, int(n.value), flops, pairs
 
 
@@ -197,8 +203,11 @@ def main():
     warm = max(args.warmup, 1)
     clock = {}
 
+    cand_per_gen = []
+
     def on_generation(t):
         done = len(abc.generation_log)
+        cand_per_gen.append(int(abc.sampler.last_stats.get("candidates", 0)))
         if done == warm:
             barrier()
             timer.begin()
@@ -241,6 +250,26 @@ def main():
              "f64": "mvn_lse_kernel<double> (f64 MFMA cross term + exp2 + LSE)",
              "f32": "mvn_lse_kernel<float> (f32 MFMA cross term + exp2 + LSE)"}
     traffic, traffic_src = measured_traffic(args, n_pop)
+    # per-stage split of the timed region (HIP events on the launch streams)
+    c_ms, c_n = timer.channels["candidates"]
+    r_ms, r_n = timer.channels["regen"]
+    timed_cands = cand_per_gen[n_before:n_before + steps]
+    n_cand = int(sum(timed_cands))
+    stages = {"density_gemm_ms": k_ms, "candidate_rounds_ms": c_ms,
+              "regen_ms": r_ms,
+              "other_ms": 1e3 * elapsed - k_ms - c_ms - r_ms,
+              "note": ("other = fit (moments, eigh, guide, x3 pack), epsilon "
+                       "quantile, weights, compaction, host gaps")}
+    cand = {"kernel": "fused_round_kernel (proposal + prior re-draw + "
+                      "LinearGaussian simulation + p-norm + accept bit)",
+            "candidates": n_cand, "launches": c_n,
+            "candidates_per_s": n_cand / (c_ms * 1e-3) if c_ms else None,
+            "bytes_per_candidate": {"written": 0.125,
+                                    "read_cached": 8 * (args.dim + 3) + 8},
+            "bound": ("VALU issue: ~1460 VALU instructions per candidate "
+                      "(PMC, profiles/r02_fused_pmc.txt): Philox4x32-10 + "
+                      "fp64 Box-Muller dominate; not HBM"),
+            "candidates_per_generation": timed_cands}
     # unique bytes one launch must move: the population and candidate
     # operand images (KB blocks of 32 f16 per row) + the fp64 result
     kb = kpad // 32 if args.precision == "x3" else None
@@ -287,6 +316,8 @@ def main():
             "pair_evals_per_s": pair_evals,
             "acceptance_rate_last": n_pop / gens[-1]["n_sim"] if gens else None,
             "generation_ms": [round(1e3 * g["seconds"], 3) for g in gens],
+            "stages": stages,
+            "candidate_kernel": cand,
             "roofline": {"bound": "mfma", "kernel": kname[args.precision],
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                          "frac": achieved / peak,

@@ -61,6 +61,13 @@ int abc_version(void);
  * and returns the summed elapsed time and the number of launches. */
 int abc_profile_begin(void);
 int abc_profile_end(double* total_ms, int64_t* launches);
+/* The other timing channels of the last begin/end window: ABC_PROF_DENSITY
+ * (what abc_profile_end returns), ABC_PROF_CANDIDATES (the fused candidate
+ * round kernel), ABC_PROF_REGEN (regeneration of kept rows). */
+#define ABC_PROF_DENSITY 0
+#define ABC_PROF_CANDIDATES 1
+#define ABC_PROF_REGEN 2
+int abc_profile_channel(int channel, double* total_ms, int64_t* launches);
 
 /* ---- reductions used by the fits ------------------------------------------
  * Replaces the numpy work in MultivariateNormalTransition.fit

@@ -53,8 +53,9 @@ def uniform53(x0, x1):
 
 
 def normal_pairs(x0, x1):
-    """Box-Muller on two u32 streams -> two standard normals (float64 here;
-    the device evaluates the same formula in fp32)."""
+    """Box-Muller on two u32 streams -> two standard normals (float64).
+    The device evaluates the same formula with a table-driven fp64 transform
+    (abc_common.h box_muller) that agrees to a few ulp."""
     u1 = uniform01(x0)
     u2 = uniform01(x1)
     r = np.sqrt(-2.0 * np.log(u1))

@@ -25,6 +25,7 @@ SIGNATURES = {
     "abc_version": (I32, []),
     "abc_profile_begin": (I32, []),
     "abc_profile_end": (I32, [P, P]),
+    "abc_profile_channel": (I32, [I32, P, P]),
     "abc_weighted_moments_workspace": (SZ, [I64, I32]),
     "abc_weighted_moments": (I32, [P, P, I64, I32, P, P, SZ, P]),
     "abc_scan_workspace": (SZ, [I64]),
@@ -99,6 +100,7 @@ ABC_ERR_HIP = -2
 ABC_ERR_WORKSPACE = -3
 ABC_ERR_NOT_ENOUGH_PARTICLES = -4
 ABC_ERR_UNSUPPORTED = -5
+ABC_PROF_DENSITY, ABC_PROF_CANDIDATES, ABC_PROF_REGEN = 0, 1, 2
 ABC_PREC_F64 = 0
 ABC_PREC_F32 = 1
 ABC_PREC_X3 = 2

@@ -31,10 +31,11 @@ constexpr uint32_t SLOT_SIM = 0x40000000u;
 // normals q .. q+3 of one slot (Box-Muller pairs; only the first `need`
 // (1..4) are produced -- the pair the caller does not use is skipped)
 __device__ __forceinline__ void normals4(uint64_t g, uint32_t slot, uint32_t gen,
-                                         uint64_t seed, double n[4], int need = 4) {
+                                         uint64_t seed, double n[4], int need = 4,
+                                         const double* tab = BM_TAB) {
   u32x4 r = philox(g, slot, gen, seed);
-  box_muller(r.x, r.y, n[0], n[1]);
-  if (need > 2) box_muller(r.z, r.w, n[2], n[3]);
+  box_muller(r.x, r.y, n[0], n[1], tab);
+  if (need > 2) box_muller(r.z, r.w, n[2], n[3], tab);
 }
 
 // ---- priors (scipy.stats pdf conventions, closed support [a, b]) ----------
@@ -217,6 +218,34 @@ __device__ __forceinline__ int64_t ancestor_search(const double* __restrict__ cd
   return lo < N ? lo : N - 1;
 }
 
+// The guide-table search split in two: the bracket loads are issued first
+// (ancestor_bracket) and the search finished later (ancestor_finish), so
+// independent work can run while they are in flight.  Same result as
+// ancestor_search.
+struct AncestorBracket { int64_t lo, hi; };
+__device__ __forceinline__ AncestorBracket ancestor_bracket(const int32_t* __restrict__ guide,
+                                                            int64_t N, double total,
+                                                            double target) {
+  if (guide == nullptr) return {0, N};
+  const double step = total / (double)N;
+  int64_t k = (int64_t)floor(target / step) - 1;  // t_k < target (one-bin margin)
+  k = k < 0 ? 0 : (k > N - 1 ? N - 1 : k);
+  const int64_t k3 = k + 3 < N ? k + 3 : N - 1;
+  // both loads unconditional (no branch, so no wait at the join)
+  const int64_t lo = guide[k];
+  const int64_t g3 = guide[k3];
+  return {lo, k + 3 < N ? g3 + 1 : N};  // t_{k+3} > target
+}
+__device__ __forceinline__ int64_t ancestor_finish(const double* __restrict__ cdf, int64_t N,
+                                                   double target, AncestorBracket b) {
+  int64_t lo = b.lo, hi = b.hi;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (cdf[mid] > target) hi = mid; else lo = mid + 1;
+  }
+  return lo < N ? lo : N - 1;
+}
+
 // ---- exact support box ------------------------------------------------------
 // The support {x : prior_in_support1(kind, p, x)} of every kind is an
 // interval of doubles (y = (x - loc) / scale is monotone in x, and so is each
@@ -287,73 +316,10 @@ struct ProposalArgs {
   uint32_t gen;
 };
 
-// The support box of the block's prior in LDS (sbox: 2 * 64 doubles); every
-// thread of the block must call it (it synchronises).
-__device__ __forceinline__ void support_box_block(const int32_t* kind, const double* params,
-                                                  int d, double* sbox) {
-  if ((int)threadIdx.x < d) support_bounds(kind[threadIdx.x], params + 4 * threadIdx.x,
-                                           sbox + 2 * threadIdx.x);
-  __syncthreads();
-}
-
 // MODE: PROP_MVN (one shared L), PROP_LOCAL (per-particle L), PROP_PRIOR
 // (X == nullptr: draw from the prior).  Separate instantiations keep the
 // prior draw's calls out of the transition kernels' register allocation.
 constexpr int PROP_MVN = 0, PROP_LOCAL = 1, PROP_PRIOR = 2;
-
-// Candidate g: ancestor j ~ Cat(w), theta = X_j + L_j n (or a prior draw when
-// X == nullptr), re-drawn while theta is outside the prior support `box`
-// ([lo_k, hi_k] pairs from support_bounds).  th holds D (D > 0) or d <= 64
-// values.  The perturbation is accumulated one Box-Muller pair at a time in
-// q order, theta_k = fma(L_kq, n_q, theta_k) starting from X_jk (one code
-// copy of the transform).  Returns the attempts used, max_attempts + 1 when
-// every attempt fell outside the support (theta then holds the last one).
-template <int D, int MODE>
-__device__ __forceinline__ int propose_one(const ProposalArgs& A, const double* box,
-                                           uint64_t g, double* th, int64_t& j) {
-  const int d = D > 0 ? D : A.d;
-  j = -1;
-  const double total = (MODE != PROP_PRIOR) ? A.cdf[A.N - 1] : 0.0;
-  for (int att = 0; att < A.max_attempts; ++att) {
-    const uint32_t s0 = (uint32_t)att * SLOTS_PER_ATTEMPT;
-    if (MODE == PROP_PRIOR) {
-#pragma unroll
-      for (int k = 0; k < (D > 0 ? D : d); ++k)
-        th[k] = prior_draw1(A.kind[k], A.params + 4 * k, g,
-                            s0 + SLOT_PRIOR + 512u * k, A.gen, A.seed);
-    } else {
-      u32x4 r = philox(g, s0 + SLOT_ANCESTOR, A.gen, A.seed);
-      j = ancestor_search(A.cdf, A.guide, A.N, total, uniform53(r.x, r.y) * total);
-      // L is re-read per candidate (scalar loads for the shared factor): an
-      // opaque pointer stops the compiler hoisting d*d doubles out of the
-      // caller's candidate loop into registers
-      const double* Lb = A.L;
-      asm volatile("" : "+s"(Lb));
-      const double* Lj = MODE == PROP_LOCAL ? Lb + j * d * d : Lb;
-      const double* Xj = A.X + j * d;
-#pragma unroll
-      for (int k = 0; k < (D > 0 ? D : d); ++k) th[k] = Xj[k];
-#pragma unroll 1
-      for (int q = 0; q < d; q += 2) {
-        if ((q & 3) == 0) r = philox(g, s0 + SLOT_PERTURB + (uint32_t)(q >> 2), A.gen, A.seed);
-        double n0, n1;
-        box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1);
-#pragma unroll
-        for (int k = 0; k < (D > 0 ? D : d); ++k) {
-          th[k] = fma(Lj[k * d + q], n0, th[k]);
-          if (q + 1 < d) th[k] = fma(Lj[k * d + q + 1], n1, th[k]);
-        }
-      }
-    }
-    const double* bx = box;
-    asm volatile("" : "+s"(bx));
-    bool ok = true;
-#pragma unroll
-    for (int k = 0; k < (D > 0 ? D : d); ++k) ok = ok && bx[2 * k] <= th[k] && th[k] <= bx[2 * k + 1];
-    if (ok) return att + 1;  // prior density > 0 (smc.py:654-656)
-  }
-  return A.max_attempts + 1;
-}
 
 // ---- LinearGaussianModel + PNormDistance -----------------------------------
 struct SimDistArgs {
@@ -366,6 +332,122 @@ struct SimDistArgs {
   int S;
 };
 
+// Per-block constants in LDS, read at wave-uniform addresses (broadcast).
+// Kept out of global memory on purpose: the kernels also store to global
+// memory, so the compiler cannot prove these arrays unclobbered and would
+// fetch every element with a per-lane vector load (~120 per candidate).
+constexpr int SIM_SMAX = 256;     // fused path: S <= SIM_SMAX
+constexpr int LT_DMAX = 16;       // shared L staged for d <= 16
+struct BlockConsts {
+  double bmt[BM_TAB_SIZE];        // Box-Muller tables (BM_TAB)
+  double LT[LT_DMAX * LT_DMAX];   // shared L, transposed: LT[q d + k] = L[k d + q]
+  double box[2 * 64];             // prior support [lo, hi] per dimension
+  double2 as[SIM_SMAX];           // (a_k, sigma_k)
+  double2 wx[SIM_SMAX];           // (wf_k, x0_k)
+  int32_t src[SIM_SMAX];
+  double total;                   // cdf[N - 1]
+};
+
+// Fill C (every thread of the block calls it; synchronises).  BOX_FROM_SRC:
+// copy the precomputed support box box_src, else bisect here
+// (support_bounds).
+template <int D, int MODE, bool BOX_FROM_SRC = false>
+__device__ __forceinline__ void stage_block_consts(BlockConsts& C, const ProposalArgs& A,
+                                                   const SimDistArgs* M,
+                                                   const double* box_src) {
+  const int t = threadIdx.x, nt = blockDim.x;
+  const int d = D > 0 ? D : A.d;
+  for (int k = t; k < BM_TAB_SIZE; k += nt) C.bmt[k] = BM_TAB[k];
+  if (MODE == PROP_MVN && D > 0 && D <= LT_DMAX)
+    for (int e = t; e < d * d; e += nt) C.LT[(e % d) * d + e / d] = A.L[e];
+  if (BOX_FROM_SRC) {
+    for (int k = t; k < 2 * d; k += nt) C.box[k] = box_src[k];
+  } else if (t < d) {
+    support_bounds(A.kind[t], A.params + 4 * t, C.box + 2 * t);
+  }
+  if (M)
+    for (int k = t; k < M->S && k < SIM_SMAX; k += nt) {
+      C.as[k] = make_double2(M->a[k], M->sigma[k]);
+      C.wx[k] = make_double2(M->wf[k], M->x0[k]);
+      C.src[k] = M->src[k];
+    }
+  if (t == 0) C.total = (MODE != PROP_PRIOR) ? A.cdf[A.N - 1] : 0.0;
+  __syncthreads();
+}
+
+// Candidate g: ancestor j ~ Cat(w), theta = X_j + L_j n (or a prior draw when
+// X == nullptr), re-drawn while theta is outside the prior support C.box.
+// th holds D (D > 0) or d <= 64 values.  The perturbation is accumulated one
+// Box-Muller pair at a time in q order, theta_k = fma(L_kq, n_q, theta_k)
+// starting from X_jk (one code copy of the transform).  Returns the attempts
+// used, max_attempts + 1 when every attempt fell outside the support (theta
+// then holds the last one).
+template <int D, int MODE>
+__device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockConsts& C,
+                                           uint64_t g, double* th, int64_t& j) {
+  constexpr bool LT_LDS = MODE == PROP_MVN && D > 0 && D <= LT_DMAX;
+  const int d = D > 0 ? D : A.d;
+  j = -1;
+  const double total = C.total;
+  for (int att = 0; att < A.max_attempts; ++att) {
+    const uint32_t s0 = (uint32_t)att * SLOTS_PER_ATTEMPT;
+    // an opaque zero offset on the LDS constants: without it the compiler
+    // hoists the loop-invariant L / box reads out of the caller's candidate
+    // loop into ~100 registers and halves the occupancy
+    int oz = 0;
+    asm volatile("" : "+s"(oz));
+    const double* LT = C.LT + oz;
+    const double* box = C.box + oz;
+    if (MODE == PROP_PRIOR) {
+#pragma unroll
+      for (int k = 0; k < (D > 0 ? D : d); ++k)
+        th[k] = prior_draw1(A.kind[k], A.params + 4 * k, g,
+                            s0 + SLOT_PRIOR + 512u * k, A.gen, A.seed);
+    } else {
+      // the ancestor's guide bracket is loaded first and the perturbation
+      // L n (independent of j) is computed while those loads are in flight;
+      // the search and the X_j row come after: theta_k = X_jk + (L n)_k
+      u32x4 r = philox(g, s0 + SLOT_ANCESTOR, A.gen, A.seed);
+      const double target = uniform53(r.x, r.y) * total;
+      AncestorBracket br = ancestor_bracket(A.guide, A.N, total, target);
+#pragma unroll
+      for (int k = 0; k < (D > 0 ? D : d); ++k) th[k] = 0.0;
+      const double* Lj = A.L;
+      if (MODE == PROP_LOCAL) {
+        // per-particle factor: needs j first
+        j = ancestor_finish(A.cdf, A.N, target, br);
+        Lj = A.L + j * d * d;
+      }
+#pragma unroll 1
+      for (int q = 0; q < d; q += 2) {
+        if ((q & 3) == 0) r = philox(g, s0 + SLOT_PERTURB + (uint32_t)(q >> 2), A.gen, A.seed);
+        double n0, n1;
+        box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1, C.bmt);
+        const bool two = q + 1 < d;
+#pragma unroll
+        for (int k = 0; k < (D > 0 ? D : d); ++k) {
+          const double l0 = LT_LDS ? LT[q * d + k] : Lj[k * d + q];
+          th[k] = fma(l0, n0, th[k]);
+          if (two) {
+            const double l1 = LT_LDS ? LT[(q + 1) * d + k] : Lj[k * d + q + 1];
+            th[k] = fma(l1, n1, th[k]);
+          }
+        }
+      }
+      if (MODE != PROP_LOCAL) j = ancestor_finish(A.cdf, A.N, target, br);
+      const double* Xj = A.X + j * d;
+#pragma unroll
+      for (int k = 0; k < (D > 0 ? D : d); ++k) th[k] = Xj[k] + th[k];
+    }
+    bool ok = true;  // branch-free (&& would branch per comparison)
+#pragma unroll
+    for (int k = 0; k < (D > 0 ? D : d); ++k)
+      ok = ok & (box[2 * k] <= th[k]) & (th[k] <= box[2 * k + 1]);
+    if (ok) return att + 1;  // prior density > 0 (smc.py:654-656)
+  }
+  return A.max_attempts + 1;
+}
+
 __device__ __forceinline__ double pterm(double v, double p) {
   return (p == 1.0) ? v : (p == 2.0 ? v * v : pow(v, p));
 }
@@ -377,17 +459,17 @@ __device__ __forceinline__ double pnorm_finish(double s, double p) {
   return isinf(p) ? s : ((p == 1.0) ? s : (p == 2.0 ? sqrt(s) : pow(s, 1.0 / p)));
 }
 // one simulated statistic (simulate_lg_kernel's formula)
-__device__ __forceinline__ double lg_stat(const SimDistArgs& M, int k, double th_src,
-                                          double e) {
-  return M.a[k] * th_src + M.sigma[k] * e;
+__device__ __forceinline__ double lg_stat(double a, double sigma, double th_src, double e) {
+  return a * th_src + sigma * e;
 }
 
-// Simulate statistics [q0, q1) (q0 even) of candidate g and fold them into
-// the p-norm state s in k order; x (nullable) receives the row.  Statistic k
-// uses normal k of the candidate's simulation stream (slot SLOT_SIM + k/4).
-// theta_{src_k} is read from tsrc[src_k * tstride] (an LDS column of the
-// calling thread: a register array indexed by src_k would go to scratch).
-__device__ __forceinline__ double sim_pnorm_range(const SimDistArgs& M,
+// Simulate statistics [q0, q1) (q0 even, q1 <= SIM_SMAX) of candidate g and
+// fold them into the p-norm state s in k order; x (nullable) receives the
+// row.  Statistic k uses normal k of the candidate's simulation stream (slot
+// SLOT_SIM + k/4).  theta_{src_k} is read from tsrc[src_k * tstride] (an LDS
+// column of the calling thread: a register array indexed by src_k would go
+// to scratch).
+__device__ __forceinline__ double sim_pnorm_range(const SimDistArgs& M, const BlockConsts& C,
                                                   const double* tsrc, int tstride,
                                                   uint64_t g, uint32_t gen,
                                                   uint64_t seed, int q0, int q1,
@@ -398,14 +480,15 @@ __device__ __forceinline__ double sim_pnorm_range(const SimDistArgs& M,
   for (int q = q0; q < q1; q += 2) {
     if ((q & 3) == 0) r = philox(g, SLOT_SIM + (uint32_t)(q >> 2), gen, seed);
     double n2[2];
-    box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n2[0], n2[1]);
+    box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n2[0], n2[1], C.bmt);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int k = q + t;
       if (k < q1) {
-        const double xv = lg_stat(M, k, tsrc[M.src[k] * tstride], n2[t]);
+        const double2 as = C.as[k], wx = C.wx[k];
+        const double xv = lg_stat(as.x, as.y, tsrc[C.src[k] * tstride], n2[t]);
         if (x) x[k] = xv;
-        s = pnorm_acc(s, fabs(M.wf[k] * (xv - M.x0[k])), M.p);
+        s = pnorm_acc(s, fabs(wx.x * (xv - wx.y)), M.p);
       }
     }
   }

@@ -36,9 +36,6 @@ struct RoundArgs {
   const double* box;  // prior support [d x (lo, hi)] (support_box_kernel)
 };
 
-// Full evaluation of candidate g: proposal + simulation + distance.  Returns
-// the distance (+inf when the proposal gave up on the prior support), the
-// attempts and the ancestor through the references; x (nullable) gets the row.
 // theta of the calling thread as the simulator's source column: an LDS
 // slab [D][FR_T] for D > 0, the (scratch) array itself for runtime d
 template <int D>
@@ -58,13 +55,13 @@ struct ThetaSlab {
 // the distance (+inf when the proposal gave up on the prior support), the
 // attempts and the ancestor through the references; x (nullable) gets the row.
 template <int D, int MODE>
-__device__ __forceinline__ double evaluate_full(const RoundArgs& A, const ThetaSlab<D>& slab,
-                                                uint64_t g, double* th, int64_t& j,
-                                                int& att, double* x) {
-  att = propose_one<D, MODE>(A.P, A.box, g, th, j);
+__device__ __forceinline__ double evaluate_full(const RoundArgs& A, const BlockConsts& C,
+                                                const ThetaSlab<D>& slab, uint64_t g,
+                                                double* th, int64_t& j, int& att, double* x) {
+  att = propose_one<D, MODE>(A.P, C, g, th, j);
   const double* ts = slab.put(th);
-  const double s = sim_pnorm_range(A.M, ts, slab.stride(), g, A.P.gen, A.P.seed, 0, A.M.S,
-                                   0.0, x);
+  const double s = sim_pnorm_range(A.M, C, ts, slab.stride(), g, A.P.gen, A.P.seed, 0,
+                                   A.M.S, 0.0, x);
   const double dist = pnorm_finish(s, A.M.p);
   return att <= A.P.max_attempts ? dist : INFINITY;
 }
@@ -75,6 +72,8 @@ __global__ __launch_bounds__(FR_T) void fused_round_kernel(
     uint64_t* __restrict__ bits, int64_t* __restrict__ tile_cnt,
     double* __restrict__ rec_x) {
   constexpr int DM = D > 0 ? D : 64;
+  __shared__ BlockConsts C;
+  stage_block_consts<D, MODE, true>(C, A.P, &A.M, A.box);
   __shared__ uint32_t tbits[FR_TILE / 32];
   __shared__ uint16_t queue[FR_TILE];
   __shared__ int qn;
@@ -97,10 +96,10 @@ __global__ __launch_bounds__(FR_T) void fused_round_kernel(
       const int64_t b = tile0 + loc;
       if (b < B) {
         const uint64_t g = (uint64_t)(idx0 + b);
-        att = propose_one<D, MODE>(A.P, A.box, g, th, j);
+        att = propose_one<D, MODE>(A.P, C, g, th, j);
         const double* ts = slab.put(th);
-        const double s = sim_pnorm_range(A.M, ts, slab.stride(), g, A.P.gen, A.P.seed, 0, 4,
-                                         0.0, nullptr);
+        const double s = sim_pnorm_range(A.M, C, ts, slab.stride(), g, A.P.gen, A.P.seed, 0,
+                                         4, 0.0, nullptr);
         if (att <= A.P.max_attempts && !(pnorm_finish(s, A.M.p) > eps)) {
           const int pos = atomicAdd(&qn, 1);
           queue[pos] = (uint16_t)loc;
@@ -118,7 +117,8 @@ __global__ __launch_bounds__(FR_T) void fused_round_kernel(
     const int64_t b = tile0 + loc;
     if (b < B) {
       double* xr = rec_x ? rec_x + b * A.M.S : nullptr;
-      const double dist = evaluate_full<D, MODE>(A, slab, (uint64_t)(idx0 + b), th, j, att, xr);
+      const double dist = evaluate_full<D, MODE>(A, C, slab, (uint64_t)(idx0 + b), th, j, att,
+                                                  xr);
       if (dist <= eps) atomicOr(&tbits[loc >> 5], 1u << (loc & 31));
     }
   }
@@ -204,18 +204,17 @@ __global__ __launch_bounds__(256) void fused_regen_kernel(
     double* __restrict__ theta, double* __restrict__ lp, int64_t* __restrict__ anc,
     double* __restrict__ x, double* __restrict__ dist) {
   constexpr int DM = D > 0 ? D : 64;
-  __shared__ double sbox[128];
   __shared__ double thl[ThetaSlab<D>::ROWS * FR_T];
+  __shared__ BlockConsts C;
+  stage_block_consts<D, MODE>(C, A.P, &A.M, nullptr);
   const ThetaSlab<D> slab{thl};
   const int d = D > 0 ? D : A.P.d;
-  support_box_block(A.P.kind, A.P.params, d, sbox);
-  A.box = sbox;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   double th[DM];
   int64_t j;
   int att;
-  const double dd = evaluate_full<D, MODE>(A, slab, (uint64_t)(idx0 + idx[i]), th, j, att,
+  const double dd = evaluate_full<D, MODE>(A, C, slab, (uint64_t)(idx0 + idx[i]), th, j, att,
                                           x + i * A.M.S);
 #pragma unroll
   for (int k = 0; k < (D > 0 ? D : d); ++k) theta[i * d + k] = th[k];
@@ -236,6 +235,9 @@ RoundArgs round_args(const abc_candidate_spec* s, const double* box) {
 int check_spec(const abc_candidate_spec* s) {
   ABC_CHECK_ARG(s != nullptr, "candidates: null spec");
   ABC_CHECK_ARG(s->d >= 1 && s->d <= 64 && s->S >= 1, "candidates: bad d/S");
+  if (s->S > SIM_SMAX)
+    return set_error(ABC_ERR_UNSUPPORTED, "candidates: S > %d (use the staged kernels)",
+                     SIM_SMAX);
   ABC_CHECK_ARG(s->max_attempts >= 1 && s->max_attempts < (1 << 15),
                 "candidates: bad max_attempts");
   ABC_CHECK_ARG(s->prior_kind && s->prior_params && s->src && s->a && s->sigma && s->x0 &&
@@ -325,8 +327,10 @@ extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0
   ABC_LAUNCHED();
   const RoundArgs A = round_args(spec, box);
   ABC_CHECK_ARG(nt < (1ll << 31), "candidates_round: too many tiles");
+  profile_start(s, ABC_PROF_CANDIDATES);
   ABC_FUSED_DISPATCH(fused_round_kernel, dim3((unsigned)nt), s, A, idx0, B, eps, filt,
                      bits, tcnt, rec_x);
+  profile_stop(s, ABC_PROF_CANDIDATES);
   ABC_LAUNCHED();
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(256), 0, s, tcnt, nt, count);
   ABC_LAUNCHED();
@@ -350,8 +354,10 @@ extern "C" int abc_candidates_regen(const abc_candidate_spec* spec, int64_t idx0
   ABC_CHECK_ARG(idx && theta && prior_logpdf && x && dist, "candidates_regen: null pointer");
   const RoundArgs A = round_args(spec, nullptr);  // box: per block, in LDS
   hipStream_t s = as_stream(stream);
+  profile_start(s, ABC_PROF_REGEN);
   ABC_FUSED_DISPATCH(fused_regen_kernel, dim3((unsigned)ceil_div(n, 256)), s, A, idx0, idx, n,
                      theta, prior_logpdf, ancestor, x, dist);
+  profile_stop(s, ABC_PROF_REGEN);
   ABC_LAUNCHED();
   return ABC_OK;
 }

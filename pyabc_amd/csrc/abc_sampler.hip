@@ -29,14 +29,14 @@ __global__ __launch_bounds__(256) void propose_kernel(
     double* __restrict__ lp_out, int64_t* __restrict__ anc_out,
     int32_t* __restrict__ att_out) {
   constexpr int DM = D > 0 ? D : 64;
-  __shared__ double sbox[128];
+  __shared__ BlockConsts C;
+  stage_block_consts<D, MODE>(C, A, nullptr, nullptr);
   const int d = D > 0 ? D : A.d;
-  support_box_block(A.kind, A.params, d, sbox);
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   double th[DM];
   int64_t j;
-  const int att = propose_one<D, MODE>(A, sbox, (uint64_t)(idx0 + b), th, j);
+  const int att = propose_one<D, MODE>(A, C, (uint64_t)(idx0 + b), th, j);
 #pragma unroll
   for (int k = 0; k < (D > 0 ? D : d); ++k) theta[b * d + k] = th[k];
   lp_out[b] = att <= A.max_attempts ? prior_logpdf(A.kind, A.params, d, th) : -INFINITY;
@@ -86,13 +86,15 @@ __global__ __launch_bounds__(256) void simulate_lg_kernel(
     const double* __restrict__ sigma, uint64_t seed, uint32_t gen,
     int64_t idx0, double* __restrict__ x) {
   // one thread per (candidate, group of 4 stats): coalesced over k
+  __shared__ double sbmt[BM_TAB_SIZE];
+  stage_bm_tab(sbmt);
   const int G = (S + 3) >> 2;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= B * G) return;
   const int64_t b = e / G;
   const int q = (int)(e % G) * 4;
   double n4[4];
-  normals4((uint64_t)(idx0 + b), SLOT_SIM + (uint32_t)(q >> 2), gen, seed, n4);
+  normals4((uint64_t)(idx0 + b), SLOT_SIM + (uint32_t)(q >> 2), gen, seed, n4, 4, sbmt);
   for (int t = 0; t < 4 && q + t < S; ++t) {
     const int k = q + t;
     x[b * S + k] = a[k] * theta[b * d + src[k]] + sigma[k] * n4[t];

@@ -114,6 +114,8 @@ class BatchedGPUSampler(Sampler):
         same name (singlecore.py:14-26); off by default, as there.
     """
 
+    FUSED_MAX_STATS = 256     # abc_candidates_round: S <= SIM_SMAX
+
     def __init__(self, batch_size=None, max_batch_size=1 << 22, seed=None,
                  max_attempts=10000, check_max_eval=False, fused=True,
                  max_fused_batch_size=1 << 31, filter_below=0.15,
@@ -303,7 +305,7 @@ class BatchedGPUSampler(Sampler):
                if hasattr(spec.model, "fused_simulator") else None)
         fp = (spec.distance.fused_pnorm(spec.t, spec.sum_stat_keys, dev)
               if hasattr(spec.distance, "fused_pnorm") else None)
-        if sim is None or fp is None:
+        if sim is None or fp is None or len(spec.sum_stat_keys) > self.FUSED_MAX_STATS:
             return None
         prop = {}
         if spec.transition is not None:
