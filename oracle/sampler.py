@@ -63,8 +63,19 @@ def prior_logpdf(theta, kinds, params):
     return lp
 
 
+def propose_local(X, w, chol, seed, generation, idx0, B, kinds=None, params=None,
+                  max_attempts=1000):
+    """Device abc_local_propose replayed (LocalTransition.rvs,
+    pyabc/transition/local_transition.py:141-145: j ~ Cat(w), theta ~
+    N(X_j, cov_j)): theta = X_j + chol_j n with the per-particle Cholesky
+    factor chol [N, d, d]; same Philox streams and re-draw loop as
+    propose_mvn."""
+    return propose_mvn(X, w, chol, seed, generation, idx0, B, kinds, params,
+                       max_attempts, per_particle=True)
+
+
 def propose_mvn(X, w, L, seed, generation, idx0, B, kinds=None, params=None,
-                max_attempts=1000):
+                max_attempts=1000, per_particle=False):
     """Device abc_propose replayed: returns theta, prior logpdf, ancestor,
     attempts."""
     X = np.asarray(X, dtype=np.float64)
@@ -88,7 +99,10 @@ def propose_mvn(X, w, L, seed, generation, idx0, B, kinds=None, params=None,
         u = uniform53(r[:, 0], r[:, 1])
         j = np.minimum(np.searchsorted(cdf, u * total, side="right"), N - 1)
         n = normals(ii, s0 + SLOT_PERTURB, d, generation, seed)
-        th = X[j] + n @ np.asarray(L).T
+        if per_particle:
+            th = X[j] + np.einsum("bkq,bq->bk", np.asarray(L)[j], n)
+        else:
+            th = X[j] + n @ np.asarray(L).T
         l = prior_logpdf(th, kinds, params)
         pos = np.nonzero(todo)[0]
         theta[pos], lp[pos], anc[pos] = th, l, j

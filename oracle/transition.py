@@ -118,7 +118,32 @@ def local_k(n, dim, k=None, k_fraction=0.25):
     return max([k_, 10, dim])
 
 
-def local_fit(X, w, k=None, k_fraction=0.25, scaling=1.0, EPS=1e-3):
+def _local_cov(X, w, i, nq, d, scaling, EPS):
+    """Covariance of particle i (local_transition.py:77-96, 125-139) from its
+    nq - 1 nearest neighbours (ties by index), EPS loop of :112-123."""
+    n = len(X)
+    d2 = ((X - X[i]) ** 2).sum(1)
+    order = np.lexsort((np.arange(n), d2))[:nq]
+    if nq > 1:
+        nb = order[1:]
+        deltas = X[nb] - X[i]
+        lw = w[nb]
+    else:
+        deltas = np.abs(X)
+        lw = np.array([1.0])
+    cov = smart_cov(deltas, lw / lw.sum())
+    if np.abs(cov.sum()) == 0:
+        for kd in range(d):
+            cov[kd, kd] = np.abs(X[0, kd])
+    cov = cov * scaling
+    det = np.linalg.det(cov)
+    while det <= 0:
+        cov += np.identity(d) * EPS
+        det = np.linalg.det(cov)
+    return cov
+
+
+def local_fit(X, w, k=None, k_fraction=0.25, scaling=1.0, EPS=1e-3, rows=None):
     """pyabc/transition/local_transition.py:77-96, 112-139.
 
     k+1 nearest neighbours per particle (column 0 = self is dropped), local
@@ -126,7 +151,8 @@ def local_fit(X, w, k=None, k_fraction=0.25, scaling=1.0, EPS=1e-3):
     the neighbours), ``diag(|X[0]|)`` fallback for an all-zero covariance,
     scaled; then ``while det <= 0: cov += EPS * I``.  Neighbour order: by
     distance, ties by index (cKDTree's tie order is unspecified -- parity at
-    exact ties is unpinned).
+    exact ties is unpinned).  rows: only these particles (each costs one
+    O(N log N) sort, so a random subset checks a large population).
     """
     X = np.asarray(X, dtype=np.float64)
     w = np.asarray(w, dtype=np.float64).copy()
@@ -135,27 +161,10 @@ def local_fit(X, w, k=None, k_fraction=0.25, scaling=1.0, EPS=1e-3):
     n, d = X.shape
     kk = local_k(n, d, k, k_fraction)
     nq = min(kk + 1, n)
-    covs = np.empty((n, d, d))
-    for i in range(n):
-        d2 = ((X - X[i]) ** 2).sum(1)
-        order = np.lexsort((np.arange(n), d2))[:nq]
-        if nq > 1:
-            nb = order[1:]
-            deltas = X[nb] - X[i]
-            lw = w[nb]
-        else:
-            deltas = np.abs(X)
-            lw = np.array([1.0])
-        cov = smart_cov(deltas, lw / lw.sum())
-        if np.abs(cov.sum()) == 0:
-            for kd in range(d):
-                cov[kd, kd] = np.abs(X[0, kd])
-        cov = cov * scaling
-        det = np.linalg.det(cov)
-        while det <= 0:
-            cov += np.identity(d) * EPS
-            det = np.linalg.det(cov)
-        covs[i] = cov
+    rows = np.arange(n) if rows is None else np.asarray(rows)
+    covs = np.empty((len(rows), d, d))
+    for o, i in enumerate(rows):
+        covs[o] = _local_cov(X, w, int(i), nq, d, scaling, EPS)
     inv = np.linalg.inv(covs)
     dets = np.linalg.det(covs)
     normalization = np.sqrt((2 * np.pi) ** d * dets)

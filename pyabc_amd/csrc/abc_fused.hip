@@ -66,11 +66,12 @@ __device__ __forceinline__ double evaluate_full(const RoundArgs& A, const BlockC
   return att <= A.P.max_attempts ? dist : INFINITY;
 }
 
-template <int D, int MODE>
-__global__ __launch_bounds__(FR_T) void fused_round_kernel(
-    RoundArgs A, int64_t idx0, int64_t B, double eps, int filter,
+template <int D, int MODE, bool FILTER>
+__device__ __forceinline__ void round_body(
+    RoundArgs A, int64_t idx0, int64_t B, double eps,
     uint64_t* __restrict__ bits, int64_t* __restrict__ tile_cnt,
     double* __restrict__ rec_x) {
+  constexpr bool filter = FILTER;
   constexpr int DM = D > 0 ? D : 64;
   __shared__ BlockConsts C;
   stage_block_consts<D, MODE, true>(C, A.P, &A.M, A.box);
@@ -88,7 +89,7 @@ __global__ __launch_bounds__(FR_T) void fused_round_kernel(
   double th[DM];
   int64_t j;
   int att;
-  if (filter) {
+  if (FILTER) {
     // phase A: proposal + first group of 4 statistics; an exact early reject
 #pragma unroll 1
     for (int it = 0; it < FR_CPT; ++it) {
@@ -136,6 +137,22 @@ __global__ __launch_bounds__(FR_T) void fused_round_kernel(
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
     if (lane == 0) tile_cnt[blockIdx.x] = c;
   }
+}
+
+// the plain and the early-reject round as separate kernels (a runtime
+// switch would give both the register allocation of the larger one)
+template <int D, int MODE>
+__global__ __launch_bounds__(FR_T) void fused_round_plain(RoundArgs A, int64_t idx0, int64_t B,
+                                                          double eps, uint64_t* bits,
+                                                          int64_t* tile_cnt, double* rec_x) {
+  round_body<D, MODE, false>(A, idx0, B, eps, bits, tile_cnt, rec_x);
+}
+template <int D, int MODE>
+__global__ __launch_bounds__(FR_T) void fused_round_filter(RoundArgs A, int64_t idx0,
+                                                           int64_t B, double eps,
+                                                           uint64_t* bits, int64_t* tile_cnt,
+                                                           double* rec_x) {
+  round_body<D, MODE, true>(A, idx0, B, eps, bits, tile_cnt, nullptr);
 }
 
 __global__ void support_box_kernel(const int32_t* __restrict__ kind,
@@ -328,8 +345,12 @@ extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0
   const RoundArgs A = round_args(spec, box);
   ABC_CHECK_ARG(nt < (1ll << 31), "candidates_round: too many tiles");
   profile_start(s, ABC_PROF_CANDIDATES);
-  ABC_FUSED_DISPATCH(fused_round_kernel, dim3((unsigned)nt), s, A, idx0, B, eps, filt,
-                     bits, tcnt, rec_x);
+  if (filt)
+    ABC_FUSED_DISPATCH(fused_round_filter, dim3((unsigned)nt), s, A, idx0, B, eps, bits, tcnt,
+                       rec_x);
+  else
+    ABC_FUSED_DISPATCH(fused_round_plain, dim3((unsigned)nt), s, A, idx0, B, eps, bits, tcnt,
+                       rec_x);
   profile_stop(s, ABC_PROF_CANDIDATES);
   ABC_LAUNCHED();
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(256), 0, s, tcnt, nt, count);

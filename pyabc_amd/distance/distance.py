@@ -168,10 +168,10 @@ class AdaptivePNormDistance(PNormDistance):
         if isinstance(all_sum_stats, SumStatMatrix) and all_sum_stats.keys == keys:
             mat = all_sum_stats.data
         elif kern is not None:
-            rows = [[float(s[k]) for k in keys] for s in all_sum_stats]
             if any(not all(k in s for k in keys) for s in all_sum_stats):
-                mat = None     # ragged: per-key path below
+                mat = None     # ragged: per-key path below (distance.py:278-283)
             else:
+                rows = [[float(s[k]) for k in keys] for s in all_sum_stats]
                 mat = gpu.as_dev(np.asarray(rows, dtype=np.float64).reshape(-1, len(keys)))
         else:
             mat = None

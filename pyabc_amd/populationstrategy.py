@@ -102,6 +102,9 @@ class AdaptivePopulationSize(PopulationStrategy):
             self.nr_particles = max(min(int(cv_estimate.n_estimated),
                                         self.max_population_size),
                                     self.min_population_size)
+        # the bootstrap draws come from each process's own numpy RNG: with
+        # several ranks, rank 0's size is the one every rank samples
+        self.nr_particles = _agree_across_ranks(int(self.nr_particles))
         self.cv_estimate_ = cv_estimate
         logger.info("Change nr particles {} -> {}".format(
             reference_nr_part, self.nr_particles))
@@ -110,6 +113,20 @@ class AdaptivePopulationSize(PopulationStrategy):
         if t == -1 and self.nr_calibration_particles is not None:
             return self.nr_calibration_particles
         return self.nr_particles
+
+
+def _agree_across_ranks(n):
+    """Rank 0's value on every rank of the default process group (no-op
+    without one)."""
+    from .sampler import distributed as dd
+    rank, ws = dd.world()
+    if ws == 1:
+        return n
+    import torch
+    dev = (torch.device("cuda", torch.cuda.current_device())
+           if torch.cuda.is_available() and dd.dist.get_backend() == "nccl"
+           else torch.device("cpu"))
+    return dd.broadcast_int(n, dev)
 
 
 class ListPopulationSize(PopulationStrategy):

@@ -23,6 +23,7 @@ overshoot is counted (the reference's MulticoreEval counts its overshoot,
 multicore_evaluation_parallel.py:138).  Recorded sum stats (record_rejected)
 are all candidates up to that cutoff, in index order (SingleCore semantics).
 """
+import logging
 import math
 
 import numpy as np
@@ -33,6 +34,8 @@ from ..population import ColumnarParticles, Particle, Population
 from ..parameters import Parameter
 from . import distributed as dd
 from .base import Sampler
+
+logger = logging.getLogger("Sampler")
 
 
 class ColumnarSample:
@@ -137,6 +140,10 @@ class BatchedGPUSampler(Sampler):
         # first m recorded candidates are all that is used
         # (ABCSMC.max_nr_recorded_particles, smc.py:998-1001)
         self.max_nr_recorded = np.inf
+        # HBM held by the recorded rows of one generation (all ranks' rows
+        # in global order count); past it the first rows that fit are kept,
+        # as if max_nr_recorded_particles had been set (logged)
+        self.record_device_budget_bytes = 64 << 30
         self._acc_rate = None
         self.last_stats = {}
 
@@ -180,7 +187,7 @@ class BatchedGPUSampler(Sampler):
         rec_extra = [] if (stochastic and record) else None
         keeps = []          # per round: accepted rows kept by each rank
         rec_keeps = []      # per round: recorded rows of each rank
-        rec_left = self.max_nr_recorded
+        rec_left = self._record_limit(len(spec.sum_stat_keys))
         n_acc = 0
         base = 0
         n_eval = 0
@@ -343,6 +350,11 @@ class BatchedGPUSampler(Sampler):
         left = int(math.ceil(max_eval)) - int(n_eval)
         return int(max(1, min(B, left // ws)))
 
+    def _record_limit(self, S):
+        budget_rows = self.record_device_budget_bytes // (8 * max(S, 1))
+        self._budget_capped = budget_rows < self.max_nr_recorded
+        return min(self.max_nr_recorded, budget_rows)
+
     def _cap_records(self, rec_all, rec_left):
         """Keep only the first max_nr_recorded recorded candidates in global
         order (round-major, then rank); returns (rows per rank, rows left)."""
@@ -353,6 +365,9 @@ class BatchedGPUSampler(Sampler):
         for q in range(len(rec_all)):
             out[q] = min(int(rec_all[q]), left)
             left -= int(out[q])
+        if left == 0 and out.sum() < rec_all.sum() and self._budget_capped:
+            logger.warning("recorded sum stats exceed record_device_budget_bytes "
+                           "(%d); keeping the first rows only", self.record_device_budget_bytes)
         return out, left
 
     def _sample_fused(self, n, fr, spec, max_eval, record, dev, rank, ws):
@@ -364,7 +379,7 @@ class BatchedGPUSampler(Sampler):
         S = len(spec.sum_stat_keys)
         cols = {k: [] for k in ("theta", "lp", "dist", "x", "anc")}
         rec_x, rec_keeps, keeps = [], [], []
-        rec_left = self.max_nr_recorded
+        rec_left = self._record_limit(S)
         n_acc = n_eval = base = rounds = 0
         ok = True
         rate, measured = self._acc_rate, False
