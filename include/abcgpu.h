@@ -117,7 +117,10 @@ int abc_normalize_weights(double* w, int64_t N, double* stats, void* ws,
  *   exact fp64 log-kernel value becomes the candidate's exponent offset, which
  *   replaces the X3 kernel's max pre-pass over the population (a quarter of
  *   its MFMA work).  Invalid rows (outside [0, N) or w <= 0) send the
- *   candidate to the fp64 rescue path. */
+ *   candidate to the fp64 rescue path.  With hints, candidates whose hinted
+ *   offset proves too far below their maximum are re-run through the exact
+ *   (unhinted) pass on a gathered subset: the call then reads that count
+ *   back (one stream synchronisation). */
 size_t abc_mvn_packed_bytes(int64_t N, int r, int prec);
 int abc_mvn_pack_population(const double* X, const double* w, int64_t N, int d,
                             const double* mu, const double* U, int r,

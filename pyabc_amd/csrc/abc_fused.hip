@@ -163,29 +163,71 @@ __global__ void support_box_kernel(const int32_t* __restrict__ kind,
 }
 
 // ---- order-preserving compaction of the accept bits -----------------------
-// exclusive scan of the tile counts (one block), total -> *count
-__global__ __launch_bounds__(256) void tile_scan_kernel(int64_t* __restrict__ cnt,
-                                                        int64_t n,
-                                                        int64_t* __restrict__ count) {
-  __shared__ int64_t sh[256];
+// exclusive scan of the tile counts in place, total -> *count: per block of
+// SC_N tiles a local scan (scan_partial: block sums), one block scans the
+// block sums (scan_top), then each block adds its offset (scan_apply)
+constexpr int SC_T = 256, SC_PER = 4, SC_N = SC_T * SC_PER;
+
+__device__ __forceinline__ int64_t block_exscan(int64_t v, int64_t* sh, int64_t& total) {
   const int t = threadIdx.x;
-  const int64_t per = (n + 255) / 256;
-  const int64_t b0 = t * per;
-  int64_t s = 0;
-  for (int64_t k = 0; k < per; ++k)
-    if (b0 + k < n) s += cnt[b0 + k];
-  sh[t] = s;
+  sh[t] = v;
   __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {
+  for (int o = 1; o < SC_T; o <<= 1) {
     const int64_t add = (t >= o) ? sh[t - o] : 0;
     __syncthreads();
     sh[t] += add;
     __syncthreads();
   }
-  int64_t off = sh[t] - s;
+  total = sh[SC_T - 1];
+  const int64_t ex = sh[t] - v;
+  __syncthreads();
+  return ex;
+}
+
+__global__ __launch_bounds__(SC_T) void scan_partial(const int64_t* __restrict__ cnt,
+                                                     int64_t n, int64_t* __restrict__ bsum) {
+  __shared__ int64_t sh[SC_T];
+  const int64_t b0 = (int64_t)blockIdx.x * SC_N + threadIdx.x * SC_PER;
+  int64_t v = 0;
+#pragma unroll
+  for (int k = 0; k < SC_PER; ++k)
+    if (b0 + k < n) v += cnt[b0 + k];
+  int64_t tot;
+  block_exscan(v, sh, tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(SC_T) void scan_top(int64_t* __restrict__ bsum, int64_t nb,
+                                                 int64_t* __restrict__ count) {
+  __shared__ int64_t sh[SC_T];
+  const int64_t per = (nb + SC_T - 1) / SC_T;
+  const int64_t b0 = threadIdx.x * per;
+  int64_t v = 0;
   for (int64_t k = 0; k < per; ++k)
-    if (b0 + k < n) { const int64_t v = cnt[b0 + k]; cnt[b0 + k] = off; off += v; }
-  if (t == 255) *count = sh[255];
+    if (b0 + k < nb) v += bsum[b0 + k];
+  int64_t tot;
+  int64_t off = block_exscan(v, sh, tot);
+  for (int64_t k = 0; k < per; ++k)
+    if (b0 + k < nb) { const int64_t x = bsum[b0 + k]; bsum[b0 + k] = off; off += x; }
+  if (threadIdx.x == 0) *count = tot;
+}
+
+__global__ __launch_bounds__(SC_T) void scan_apply(int64_t* __restrict__ cnt, int64_t n,
+                                                   const int64_t* __restrict__ boff) {
+  __shared__ int64_t sh[SC_T];
+  const int64_t b0 = (int64_t)blockIdx.x * SC_N + threadIdx.x * SC_PER;
+  int64_t c[SC_PER];
+  int64_t v = 0;
+#pragma unroll
+  for (int k = 0; k < SC_PER; ++k) {
+    c[k] = b0 + k < n ? cnt[b0 + k] : 0;
+    v += c[k];
+  }
+  int64_t tot;
+  int64_t off = block_exscan(v, sh, tot) + boff[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < SC_PER; ++k)
+    if (b0 + k < n) { cnt[b0 + k] = off; off += c[k]; }
 }
 
 // one lane per 64-bit word: positions of the set bits, in increasing order,
@@ -309,6 +351,7 @@ extern "C" size_t abc_candidates_workspace(int64_t B) {
   size_only<uint64_t>(off, (size_t)nt * FR_WORDS);  // accept bits
   size_only<int64_t>(off, (size_t)nt);              // tile counts / offsets
   size_only<double>(off, 128);                      // prior support box
+  size_only<int64_t>(off, (size_t)ceil_div(nt, SC_N));  // scan block sums
   return off + 256;
 }
 
@@ -338,6 +381,7 @@ extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0
   uint64_t* bits = c.take<uint64_t>((size_t)nt * FR_WORDS);
   int64_t* tcnt = c.take<int64_t>((size_t)nt);
   double* box = c.take<double>(128);
+  int64_t* bsum = c.take<int64_t>((size_t)ceil_div(nt, SC_N));
   if (!c.ok) return set_error(ABC_ERR_WORKSPACE, "candidates_round: workspace");
   hipLaunchKernelGGL(support_box_kernel, dim3(1), dim3(64), 0, s, spec->prior_kind,
                      spec->prior_params, spec->d, box);
@@ -353,7 +397,12 @@ extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0
                        rec_x);
   profile_stop(s, ABC_PROF_CANDIDATES);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(256), 0, s, tcnt, nt, count);
+  const int64_t nb = ceil_div(nt, SC_N);
+  hipLaunchKernelGGL(scan_partial, dim3((unsigned)nb), dim3(SC_T), 0, s, tcnt, nt, bsum);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(scan_top, dim3(1), dim3(SC_T), 0, s, bsum, nb, count);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(scan_apply, dim3((unsigned)nb), dim3(SC_T), 0, s, tcnt, nt, bsum);
   ABC_LAUNCHED();
   if (cap > 0) {
     const int64_t nwords = ceil_div(B, 64);

@@ -501,104 +501,105 @@ __global__ void x3_combine_kernel(const double* __restrict__ part_o,
 // Rescue of the listed candidates over the stored whitened population:
 // s_ij = lw_j - |z_i - y_j|^2 / 2 (log2 units, the same s as the MFMA path)
 // in fp64, accumulated as an online (max, sum) pair in fp64 with f32 exp2 of
-// the fp64 difference (1e-7 relative per term).  Grid (slice, group): block
-// (sx, gy) takes groups of RQ candidates and the population rows of slice sx;
-// each row of Y is loaded once per group.  (max, sum) partials go to pm / pl
-// [slice][q] (the main kernel's partial arrays, free again after combine).
-constexpr int RQ = 16;
-
+// the fp64 difference (1e-7 relative per term).
 __device__ __forceinline__ void online_add(double s, double& m, double& l) {
   const double dl = s - m;
-  if (dl > 0.0) { l = l * (double)__builtin_amdgcn_exp2f((float)-dl) + 1.0; m = s; }
+  // a new maximum rescales the running sum in fp64 (rare; an f32 factor
+  // here compounds over a long scan), terms below it take the f32 exp2
+  if (dl > 0.0) { l = l * exp2(-dl) + 1.0; m = s; }
   else l += (double)__builtin_amdgcn_exp2f((float)dl);
 }
 
-__device__ __forceinline__ void online_merge(double& m, double& l, double mo, double lo) {
-  if (!(lo > 0.0)) return;
-  if (!(l > 0.0)) { m = mo; l = lo; return; }
-  if (mo > m) { l = l * exp2(m - mo) + lo; m = mo; }
-  else l += lo * exp2(mo - m);
+// Rescue v2: one rescued candidate per lane with its whitened coordinates
+// in registers; the population is cut in RS slices that depend on N only
+// (so a candidate's summation order -- and its bits -- do not depend on how
+// many others are rescued or on the sharding) and streamed through 64-row
+// LDS tiles read at broadcast addresses.  Block = one wave = 64 candidates x
+// one slice; (max, sum) partials go to pm / pl [slice][q - q0] (the main
+// kernel's partial arrays, free after combine), candidates [q0, q0 + cap)
+// per launch pair.
+constexpr int RS_ROWS = 4096;   // population rows per slice (at least)
+constexpr int RS_MAXS = 256;    // slices at most
+constexpr int RS_GY = 8;        // candidate-group blocks per slice
+
+__host__ __device__ inline int rescue_slices(int64_t N) {
+  const int64_t s = (N + RS_ROWS - 1) / RS_ROWS;
+  return (int)(s < 1 ? 1 : (s > RS_MAXS ? RS_MAXS : s));
 }
 
-__global__ __launch_bounds__(256) void x3_rescue_kernel(
+__global__ __launch_bounds__(64) void x3_rescue_kernel(
     const int64_t* __restrict__ rescue, const unsigned int* __restrict__ nrescue,
-    const double* __restrict__ x, int d, const double* __restrict__ mu,
-    const double* __restrict__ U, int r, const double* __restrict__ Y,
-    const double* __restrict__ lw, int64_t N, double* __restrict__ pm,
-    double* __restrict__ pl, int64_t Mpad) {
-  __shared__ double z[RQ][MAX_R];
-  __shared__ double sm[4][RQ], sl[4][RQ];
-  const unsigned int n = *nrescue;
-  const int64_t per = (N + gridDim.x - 1) / gridDim.x;
+    int64_t q0, int64_t cap, const double* __restrict__ x, int d,
+    const double* __restrict__ mu, const double* __restrict__ U, int r,
+    const double* __restrict__ Y, const double* __restrict__ lw, int64_t N,
+    double* __restrict__ pm, double* __restrict__ pl) {
+  __shared__ double ty[64 * MAX_R];
+  __shared__ double tl[64];
+  const int64_t n = (int64_t)*nrescue;
+  const int64_t nq = n - q0 < cap ? n - q0 : cap;   // this launch's candidates
+  const int lane = threadIdx.x;
+  const int ns = gridDim.x;
+  const int64_t per = (N + ns - 1) / ns;
   const int64_t j0 = (int64_t)blockIdx.x * per;
   const int64_t j1 = j0 + per < N ? j0 + per : N;
-  for (unsigned int q0 = blockIdx.y * RQ; q0 < n; q0 += gridDim.y * RQ) {
-    const int nq = (int)(n - q0 < (unsigned)RQ ? n - q0 : RQ);
-    for (int e = threadIdx.x; e < RQ * r; e += blockDim.x) {
-      const int c = e / r, k = e % r;
-      double acc = 0.0;
-      if (c < nq) {
-        const int64_t i = rescue[q0 + c];
+  for (int64_t g0 = (int64_t)blockIdx.y * 64; g0 < nq; g0 += (int64_t)gridDim.y * 64) {
+    const int64_t q = g0 + lane;
+    const bool act = q < nq;
+    double z[MAX_R];
+    const int64_t i = act ? rescue[q0 + q] : 0;
+#pragma unroll
+    for (int k = 0; k < MAX_R; ++k) {
+      if (k < r) {
+        double acc = 0.0;
         for (int cc = 0; cc < d; ++cc) acc += (x[i * d + cc] - mu[cc]) * U[cc * r + k];
+        z[k] = acc * SQRT_LOG2E;
       }
-      z[c][k] = acc * SQRT_LOG2E;
     }
-    __syncthreads();
-    double m[RQ], l[RQ];
+    double m = -INFINITY, l = 0.0;
+    for (int64_t jt = j0; jt < j1; jt += 64) {
+      const int cnt = (int)(j1 - jt < 64 ? j1 - jt : 64);
+      __syncthreads();
+      for (int e = lane; e < cnt * r; e += 64) ty[e] = Y[jt * r + e];
+      if (lane < cnt) tl[lane] = lw[jt + lane];
+      __syncthreads();
+      for (int t = 0; t < cnt; ++t) {
+        const double lwj = tl[t];
+        if (!(lwj > -INFINITY)) continue;
+        double q2 = 0.0;
 #pragma unroll
-    for (int c = 0; c < RQ; ++c) { m[c] = -INFINITY; l[c] = 0.0; }
-    for (int64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
-      const double lwj = lw[j];
-      if (!(lwj > -INFINITY)) continue;
-      double q2[RQ];
-#pragma unroll
-      for (int c = 0; c < RQ; ++c) q2[c] = 0.0;
-      for (int k = 0; k < r; ++k) {
-        const double yk = Y[j * r + k];
-#pragma unroll
-        for (int c = 0; c < RQ; ++c) { const double t = z[c][k] - yk; q2[c] += t * t; }
+        for (int k = 0; k < MAX_R; ++k) {
+          if (k < r) {
+            const double dz = z[k] - ty[t * r + k];
+            q2 = fma(dz, dz, q2);
+          }
+        }
+        online_add(lwj - 0.5 * q2, m, l);
       }
-#pragma unroll
-      for (int c = 0; c < RQ; ++c) online_add(lwj - 0.5 * q2[c], m[c], l[c]);
     }
-    const int wv = threadIdx.x >> 6;
-#pragma unroll
-    for (int c = 0; c < RQ; ++c) {
-      double mc = m[c], lc = l[c];
-      for (int o = 32; o > 0; o >>= 1) {
-        const double mo = __shfl_xor(mc, o, 64), lo = __shfl_xor(lc, o, 64);
-        online_merge(mc, lc, mo, lo);
-      }
-      if ((threadIdx.x & 63) == 0) { sm[wv][c] = mc; sl[wv][c] = lc; }
+    if (act) {
+      pm[(int64_t)blockIdx.x * cap + q] = m;
+      pl[(int64_t)blockIdx.x * cap + q] = l;
     }
-    __syncthreads();
-    if (threadIdx.x < nq) {
-      const int c = threadIdx.x;
-      double mc = -INFINITY, lc = 0.0;
-      for (int k = 0; k < 4; ++k) online_merge(mc, lc, sm[k][c], sl[k][c]);
-      pm[(int64_t)blockIdx.x * Mpad + q0 + c] = mc;
-      pl[(int64_t)blockIdx.x * Mpad + q0 + c] = lc;
-    }
-    __syncthreads();
   }
 }
 
 __global__ void x3_rescue_final(const int64_t* __restrict__ rescue,
-                                const unsigned int* __restrict__ nrescue,
-                                int nslice, const double* __restrict__ pm,
-                                const double* __restrict__ pl, int64_t Mpad,
-                                double log_const, double* __restrict__ out) {
-  const unsigned int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= *nrescue) return;
+                                const unsigned int* __restrict__ nrescue, int64_t q0,
+                                int64_t cap, int nslice, const double* __restrict__ pm,
+                                const double* __restrict__ pl, double log_const,
+                                double* __restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = (int64_t)*nrescue;
+  if (q >= cap || q0 + q >= n) return;
   double mx = -INFINITY;
   for (int c = 0; c < nslice; ++c)
-    if (pl[(int64_t)c * Mpad + q] > 0.0) mx = fmax(mx, pm[(int64_t)c * Mpad + q]);
+    if (pl[(int64_t)c * cap + q] > 0.0) mx = fmax(mx, pm[(int64_t)c * cap + q]);
   double t = 0.0;
   for (int c = 0; c < nslice; ++c) {
-    const double l = pl[(int64_t)c * Mpad + q];
-    if (l > 0.0) t += l * exp2(pm[(int64_t)c * Mpad + q] - mx);
+    const double l = pl[(int64_t)c * cap + q];
+    if (l > 0.0) t += l * exp2(pm[(int64_t)c * cap + q] - mx);
   }
-  out[rescue[q]] = t > 0.0 ? log_const + LN2 * (mx + log2(t)) : -INFINITY;
+  out[rescue[q0 + q]] = t > 0.0 ? log_const + LN2 * (mx + log2(t)) : -INFINITY;
 }
 
 template <int SIDE>
@@ -621,6 +622,22 @@ void launch_pack(int r, dim3 grid, hipStream_t s, const double* P, const double*
     default: ABC_PACK_CASE(0)
   }
 #undef ABC_PACK_CASE
+}
+
+// rows of the rescued candidates (x [M x d] -> xs [n x d]) and their
+// densities back (outs [n] -> out at the rescued positions)
+__global__ void x3_gather_rescued(const int64_t* __restrict__ rescue, int64_t n,
+                                  const double* __restrict__ x, int d,
+                                  double* __restrict__ xs) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * d) return;
+  xs[e] = x[rescue[e / d] * d + e % d];
+}
+__global__ void x3_scatter_rescued(const int64_t* __restrict__ rescue, int64_t n,
+                                   const double* __restrict__ outs,
+                                   double* __restrict__ out) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) out[rescue[q]] = outs[q];
 }
 
 struct PlanX3 {
@@ -790,15 +807,52 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
                      hint ? (const float*)cand_o : (const float*)nullptr, out,
                      rescue, nres);
   ABC_LAUNCHED();
-  const int gy = (int)(1024 / p.nchunk > 1 ? 1024 / p.nchunk : 1);
-  hipLaunchKernelGGL(x3_rescue_kernel, dim3((unsigned)p.nchunk, (unsigned)gy),
-                     dim3(256), 0, s, rescue, nres, x, d, mu, U, r,
-                     (const double*)x3_Y(packed, N, r),
-                     (const double*)x3_lw(packed, N, r), N, po, pl, p.Mpad);
-  ABC_LAUNCHED();
-  hipLaunchKernelGGL(x3_rescue_final, dim3((unsigned)ceil_div(M, 256)), dim3(256),
-                     0, s, rescue, nres, p.nchunk, po, pl, p.Mpad, log_const, out);
-  ABC_LAUNCHED();
+  if (hint) {
+    // Hinted candidates whose ancestor offset was far below their true
+    // maximum (or outside the limb range / underflowing) are re-run through
+    // the unhinted pass -- exact max pre-pass, still MFMA -- on a gathered
+    // subset, in the partial arrays freed by the combine.  One host read of
+    // their count; a candidate's result stays independent of M and of its
+    // position (same chunking), so sharded runs keep identical bits.
+    unsigned int nh = 0;
+    ABC_HIP(hipMemcpyAsync(&nh, nres, sizeof(nh), hipMemcpyDeviceToHost, s));
+    ABC_HIP(hipStreamSynchronize(s));
+    if (nh == 0) return ABC_OK;
+    const size_t free_bytes = (size_t)p.nchunk * p.Mpad * sizeof(double) * 2;
+    Carver sub(po, free_bytes);
+    double* xs = sub.take<double>((size_t)nh * d);
+    double* outs = sub.take<double>((size_t)nh);
+    const size_t need = plan_x3_ws(make_plan_x3(nh, N, r));
+    void* ws2 = sub.take<char>(need + 256);
+    if (sub.ok) {
+      hipLaunchKernelGGL(x3_gather_rescued, dim3((unsigned)ceil_div((int64_t)nh * d, 256)),
+                         dim3(256), 0, s, rescue, (int64_t)nh, x, d, xs);
+      ABC_LAUNCHED();
+      const int rc2 = x3_logpdf(xs, nh, d, packed, X, w, N, mu, U, r, log_const, log_norm,
+                                outs, nullptr, ws2, need + 256, s);
+      if (rc2) return rc2;
+      hipLaunchKernelGGL(x3_scatter_rescued, dim3((unsigned)ceil_div(nh, 256)), dim3(256), 0,
+                         s, rescue, (int64_t)nh, outs, out);
+      ABC_LAUNCHED();
+      return ABC_OK;
+    }
+    // (more than ~1/4 of the launch rescued: the fp64 path below)
+  }
+  // fp64 rescue of the listed candidates (count on the device): launch
+  // pairs over slot ranges of the partial arrays' capacity; pairs past the
+  // count exit at once
+  const int ns = rescue_slices(N);
+  const int64_t cap = (int64_t)p.nchunk * p.Mpad / ns;
+  for (int64_t q0 = 0; q0 < M; q0 += cap) {
+    hipLaunchKernelGGL(x3_rescue_kernel, dim3((unsigned)ns, (unsigned)RS_GY), dim3(64), 0, s,
+                       rescue, nres, q0, cap, x, d, mu, U, r,
+                       (const double*)x3_Y(packed, N, r),
+                       (const double*)x3_lw(packed, N, r), N, po, pl);
+    ABC_LAUNCHED();
+    hipLaunchKernelGGL(x3_rescue_final, dim3((unsigned)ceil_div(cap < M ? cap : M, 256)),
+                       dim3(256), 0, s, rescue, nres, q0, cap, ns, po, pl, log_const, out);
+    ABC_LAUNCHED();
+  }
   return ABC_OK;
 }
 

@@ -121,11 +121,7 @@ def allgather_rows_ordered(tensors, keeps, device):
             pad[:n_mine, c0:c0 + wdt] = c
         c0 += wdt
     out = torch.empty((ws * pad.shape[0], C), dtype=pad.dtype, device=pad.device)
-    if pad.is_cuda and dist.get_backend() == "gloo":
-        # gloo's flat all-gather is CPU-only; multi-rank tests on one GPU
-        dist.all_gather(list(out.chunk(ws)), pad)
-    else:
-        dist.all_gather_into_tensor(out, pad)
+    all_gather_flat(out, pad)
     # piece (round r, rank q) starts at q * nmax + rows q kept in rounds < r
     round_off = np.cumsum(k, axis=0) - k
     pieces = [(int(q * pad.shape[0] + round_off[r, q]), int(k[r, q]))
@@ -140,6 +136,20 @@ def allgather_rows_ordered(tensors, keeps, device):
         res.append(piece.reshape((full.shape[0],) + tuple(t.shape[1:])).contiguous())
         c0 += wdt
     return res
+
+
+def all_gather_flat(out, t):
+    """dist.all_gather_into_tensor(out, t) on every backend: RCCL (nccl)
+    gathers device tensors directly; gloo, whose flat all-gather takes host
+    tensors only, gets host copies (multi-rank runs on one GPU, CPU tests).
+    The caller's packing and cutting are the same code either way."""
+    if t.is_cuda and dist.get_backend() == "gloo":
+        host = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(host, t.cpu())
+        out.copy_(host)
+    else:
+        dist.all_gather_into_tensor(out, t)
+    return out
 
 
 def broadcast_int(v, device):

@@ -278,6 +278,51 @@ def gen_e2e10(seeds=(0, 1, 2, 3), pop=1000, gens=5):
         json.dump(out, f, indent=1)
 
 
+def gen_e2e_samples(seeds=(0, 1, 2, 3)):
+    """Final-population samples and weights of the reference's c1 run
+    (N = 1000, 8 generations, as gen_e2e) and 10-D run (N = 1000, 5
+    generations, as gen_e2e10), same seeds: the targets of the weighted
+    two-sample KS tests (tests/test_gpu_e2e.py), the reference's own
+    criterion being test_nondeterministic/test_abc_smc_algorithm.py:309-394."""
+    out = {}
+    for s in seeds:
+        np.random.seed(s)
+
+        def model(p):
+            return {"y": p["x"] + 0.5 * np.random.randn()}
+        abc = pyabc.ABCSMC(model, pyabc.Distribution(x=pyabc.RV("norm", 0, 1)),
+                           pyabc.PNormDistance(), population_size=1000,
+                           sampler=pyabc.SingleCoreSampler())
+        abc.new("sqlite://", {"y": 2.0})
+        h = abc.run(max_nr_populations=8)
+        df, w = h.get_distribution(0, h.max_t)
+        out[f"c1_seed{s}__x"] = df["x"].values
+        out[f"c1_seed{s}__w"] = w
+        out[f"c1_seed{s}__eps"] = h.get_all_populations()["epsilon"].values
+        print("samples c1", s, float((df["x"].values * w).sum()), flush=True)
+    d = 10
+    nm = [f"p{k}" for k in range(d)]
+    keys = [f"y{k}" for k in range(d)]
+    for s in seeds:
+        np.random.seed(s)
+
+        def model(p):
+            return {keys[k]: p[nm[k]] + 0.5 * np.random.randn()
+                    for k in range(d)}
+        prior = pyabc.Distribution(**{n: pyabc.RV("norm", 0, 1) for n in nm})
+        abc = pyabc.ABCSMC(model, prior, pyabc.PNormDistance(),
+                           population_size=1000, eps=QuantileEpsilon(alpha=0.5),
+                           sampler=pyabc.SingleCoreSampler())
+        abc.new("sqlite://", {k: 1.0 for k in keys})
+        h = abc.run(max_nr_populations=5)
+        df, w = h.get_distribution(0, h.max_t)
+        out[f"d10_seed{s}__X"] = df[nm].values
+        out[f"d10_seed{s}__w"] = w
+        out[f"d10_seed{s}__eps"] = h.get_all_populations()["epsilon"].values
+        print("samples d10", s, (df[nm].values * w[:, None]).sum(0).mean(), flush=True)
+    np.savez_compressed(os.path.join(HERE, "e2e_reference_samples.npz"), **out)
+
+
 def gen_cv(seeds=tuple(range(24))):
     """Bootstrapped KDE CV (pyabc/cv/bootstrap.py:44-110) and the population
     size predicted from it (transition/predict_population_size.py).
@@ -544,6 +589,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if "--e2e10" in sys.argv:
         gen_e2e10()
+        sys.exit(0)
+    if "--e2e-samples" in sys.argv:
+        gen_e2e_samples()
         sys.exit(0)
     gen_mvn()
     gen_local()

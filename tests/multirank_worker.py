@@ -40,8 +40,15 @@ def main():
     else:
         dist, eps, acceptor = (pa.PNormDistance(p=2),
                                pa.QuantileEpsilon(alpha=0.5), None)
+    pop = int(os.environ.get("POP", "20000"))
+    if os.environ.get("MODE") == "adaptive_popsize":
+        # every rank fits the same bootstraps from its own numpy stream;
+        # rank 0's size must be the one every rank samples
+        np.random.seed(1000 + rank)
+        pop = pa.AdaptivePopulationSize(pop, mean_cv=0.2, n_bootstrap=3,
+                                        max_population_size=3 * pop)
     abc = pa.ABCSMC(model, prior, dist,
-                    population_size=int(os.environ.get("POP", "20000")),
+                    population_size=pop,
                     transitions=pa.MultivariateNormalTransition(),
                     eps=eps, acceptor=acceptor,
                     sampler=pa.BatchedGPUSampler(seed=77, batch_size=None))
@@ -52,7 +59,8 @@ def main():
         pops = h.get_all_populations()
         np.savez(os.environ["OUT"], theta=df.values, w=w,
                  eps=pops["epsilon"].values[1:],
-                 samples=pops["samples"].values[1:])
+                 samples=pops["samples"].values[1:],
+                 sizes=pops["particles"].values[1:])
     if ws > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

@@ -119,9 +119,45 @@ def _install_cpu_doubles(monkeypatch_like):
     monkeypatch_like(g, "importance_weights", importance_weights)
 
 
-def _run(n, eps, batch, record):
+class _FusedRound:
+    """abc_candidates_round / _regen doubles (oracle replay of the same
+    streams): accept positions of a round, and the rows of kept ones."""
+
+    def __init__(self, spec):
+        self.pop = spec.transition.pop
+        self.d = D
+
+    def _rows(self, lo, B):
+        pop = self.pop
+        th, lp, anc, _ = osamp.propose_mvn(pop.X, pop.w, pop.L, SEED, GEN, lo, B,
+                                           ["norm"] * D, np.tile([0, 1, 0, 0], (D, 1)))
+        x = osamp.simulate_linear_gaussian(th, np.arange(D), np.ones(D),
+                                           np.full(D, 0.5), SEED, GEN, lo)
+        return th, lp, anc, x, oracle.pnorm(x, np.ones(D))
+
+    def run(self, lo, B, eps, cap, filter=True, rec_x=None):
+        *_, x, d = self._rows(lo, B)
+        acc = np.nonzero(d <= eps)[0]
+        idx = torch.zeros(max(int(cap), 1), dtype=torch.int64)
+        k = min(int(cap), len(acc))
+        idx[:k] = torch.from_numpy(acc[:k])
+        if rec_x is not None:
+            rec_x.copy_(torch.from_numpy(x))
+        return idx, torch.tensor([len(acc)])
+
+    def regen(self, lo, idx):
+        i = idx.numpy()
+        B = int(i.max()) + 1 if len(i) else 0
+        th, lp, anc, x, d = self._rows(lo, B)
+        return tuple(torch.from_numpy(np.ascontiguousarray(a[i]))
+                     for a in (th, lp, anc, x, d))
+
+
+def _run(n, eps, batch, record, fused=False):
     from pyabc_amd.sampler import BatchedGPUSampler
-    s = BatchedGPUSampler(batch_size=batch, seed=SEED)
+    s = BatchedGPUSampler(batch_size=batch, seed=SEED, fused=fused)
+    if fused:
+        s._fused_round = lambda spec, seed, gen, dev: _FusedRound(spec)
     s.sample_factory.record_rejected = record
     sample = s.sample_until_n_accepted(n, _Spec(eps))
     c = sample._cols
@@ -132,26 +168,33 @@ def _run(n, eps, batch, record):
                 rec=(rec.numpy() if rec is not None else np.zeros(0)))
 
 
-def _worker(rank, ws, port, out_dir, n, eps, batch, record):
+def _worker(rank, ws, port, out_dir, n, eps, batch, record, fused=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
         _install_cpu_doubles(setattr)
-        res = _run(n, eps, batch, record)
+        res = _run(n, eps, batch, record, fused)
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("n,batch,record", [(300, 256, True), (37, 64, False),
                                             (1, 128, True)])
-def test_sharded_sampler_matches_single_rank(monkeypatch, n, batch, record):
+def test_sharded_sampler_matches_single_rank(monkeypatch, n, batch, record, fused):
+    """Staged and fused sampler loops: 2 gloo ranks == 1 rank, and the
+    fused loop == the staged loop (same streams, same cutoff)."""
     eps = 1.6
     _install_cpu_doubles(monkeypatch.setattr)
-    ref = _run(n, eps, batch * 2, record)   # 1 rank, same global round size
+    ref = _run(n, eps, batch * 2, record, fused)   # 1 rank, same global round size
+    if fused:
+        staged = _run(n, eps, batch * 2, record, False)
+        for k in ("theta", "w", "d", "x", "n_eval", "rec"):
+            np.testing.assert_array_equal(ref[k], staged[k], err_msg=k)
     with tempfile.TemporaryDirectory() as tmp:
         mp.start_processes(_worker, args=(2, _free_port(), tmp, n, eps, batch,
-                                          record),
+                                          record, fused),
                            nprocs=2, join=True, start_method="spawn")
         for rank in range(2):
             got = dict(np.load(os.path.join(tmp, f"r{rank}.npz")))

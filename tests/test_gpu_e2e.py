@@ -82,6 +82,86 @@ def test_c1_batched_matches_analytic_and_reference():
         assert 0.3 < pops["samples"].values[-1] / ref_samples < 3
 
 
+def kish_ess(w):
+    w = np.asarray(w, dtype=np.float64)
+    return w.sum() ** 2 / (w ** 2).sum()
+
+
+def weighted_ks(x1, w1, x2, w2):
+    """sup_x |F1(x) - F2(x)| of two weighted empirical CDFs."""
+    x = np.concatenate([x1, x2])
+    order = np.argsort(x, kind="stable")
+    step = np.concatenate([np.asarray(w1) / np.sum(w1), -np.asarray(w2) / np.sum(w2)])[order]
+    xs = x[order]
+    diff = np.cumsum(step)
+    last = np.r_[xs[1:] != xs[:-1], True]      # evaluate after each tie group
+    return float(np.max(np.abs(diff[last])))
+
+
+def ks_critical(w1, w2, alpha):
+    """Two-sample KS critical value at level alpha with the Kish effective
+    sample sizes of the two weighted samples."""
+    e1, e2 = kish_ess(w1), kish_ess(w2)
+    return np.sqrt(-0.5 * np.log(alpha / 2)) * np.sqrt((e1 + e2) / (e1 * e2))
+
+
+def _pool(xs, ws):
+    return (np.concatenate(xs),
+            np.concatenate([np.asarray(w) / np.sum(w) / len(ws) for w in ws]))
+
+
+def test_c1_ks_vs_reference_samples():
+    """Config c1 (N = 1000, 8 generations): the weighted two-sample KS
+    statistic between 4 pooled runs of this engine and 4 pooled reference
+    runs (tests/golden/e2e_reference_samples.npz, pyABC 0.10.5) stays below
+    the alpha = 0.001 critical value at the Kish effective sample sizes --
+    the reference's own conjugate-model criterion is a sup-CDF distance
+    (test_abc_smc_algorithm.py:309-394)."""
+    g = np.load(os.path.join(GOLDEN, "e2e_reference_samples.npz"))
+    rx, rw = _pool([g[f"c1_seed{s}__x"] for s in range(4)],
+                   [g[f"c1_seed{s}__w"] for s in range(4)])
+    xs, ws = [], []
+    for seed in range(4):
+        h = c1_abc(seed=seed).run(max_nr_populations=8)
+        df, w = h.get_distribution(0, h.max_t)
+        xs.append(df["x"].values)
+        ws.append(w)
+    x, w = _pool(xs, ws)
+    D = weighted_ks(x, w, rx, rw)
+    crit = ks_critical(w, rw, 1e-3)
+    assert D < crit, (D, crit)
+
+
+def test_d10_ks_vs_reference_samples():
+    """10-D conjugate model (N = 1000, 5 generations, QuantileEpsilon(0.5)):
+    per-marginal weighted KS between 4 pooled runs and 4 pooled reference
+    runs below the alpha = 0.001 / 10 (Bonferroni) critical value."""
+    import pyabc_amd as pa
+    g = np.load(os.path.join(GOLDEN, "e2e_reference_samples.npz"))
+    d = 10
+    rX, rw = _pool([g[f"d10_seed{s}__X"] for s in range(4)],
+                   [g[f"d10_seed{s}__w"] for s in range(4)])
+    names = [f"p{k}" for k in range(d)]
+    keys = [f"y{k}" for k in range(d)]
+    Xs, ws = [], []
+    for seed in range(4):
+        np.random.seed(seed)
+        model = pa.LinearGaussianModel(names, keys, src=list(range(d)), sigma=[0.5] * d)
+        prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
+        abc = pa.ABCSMC(model, prior, pa.PNormDistance(), population_size=1000,
+                        eps=pa.QuantileEpsilon(alpha=0.5),
+                        sampler=pa.BatchedGPUSampler(seed=50 + seed))
+        abc.new("sqlite://", {k: 1.0 for k in keys})
+        h = abc.run(max_nr_populations=5)
+        df, w = h.get_distribution(0, h.max_t)
+        Xs.append(df[names].values)
+        ws.append(w)
+    X, w = _pool(Xs, ws)
+    crit = ks_critical(w, rw, 1e-3 / d)
+    D = [weighted_ks(X[:, k], w, rX[:, k], rw) for k in range(d)]
+    assert max(D) < crit, (D, crit)
+
+
 def test_c1_single_core_per_particle_path():
     import pyabc_amd as pa
     abc = c1_abc(pop=200, sampler=pa.SingleCoreSampler())

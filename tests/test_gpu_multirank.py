@@ -59,3 +59,14 @@ def test_sharded_stochastic_generations_bit_identical(tmp_path):
     got = _run(tmp_path, 2, "stochastic")
     for k in ("theta", "w", "eps", "samples"):
         np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{k} @ 2 ranks")
+
+
+def test_sharded_adaptive_population_size(tmp_path):
+    """AdaptivePopulationSize with 1 vs 2 ranks whose numpy streams differ
+    (rank-dependent seeds): the broadcast size keeps the ranks in step, and
+    rank 0's run equals the single-rank run."""
+    ref = _run(tmp_path, 1, "adaptive_popsize")
+    got = _run(tmp_path, 2, "adaptive_popsize")
+    assert len(set(ref["sizes"])) > 1          # the size did adapt
+    for k in ("theta", "w", "eps", "samples", "sizes"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)

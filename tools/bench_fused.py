@@ -23,13 +23,15 @@ def main():
     ap.add_argument("--B", type=int, default=1 << 28)
     ap.add_argument("--N", type=int, default=1_000_000)
     ap.add_argument("--d", type=int, default=10)
+    ap.add_argument("--S", type=int, default=None, help="statistics (default d)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--staged", action="store_true")
     a = ap.parse_args()
     import torch
     from pyabc_amd import gpu
     dev = gpu.require_device()
-    d, N, S = a.d, a.N, a.d
+    d, N = a.d, a.N
+    S = a.S or a.d
     g = torch.Generator(device="cpu").manual_seed(0)
     X = (0.8 + np.sqrt(0.2) * torch.randn(N, d, generator=g, dtype=torch.float64)).to(dev)
     w = torch.ones(N, dtype=torch.float64, device=dev) / N
@@ -39,7 +41,7 @@ def main():
     guide = gpu.cdf_guide(cdf)
     kind = torch.zeros(d, dtype=torch.int32, device=dev)
     params = torch.tensor(np.tile([0.0, 1.0, 0, 0], d), dtype=torch.float64, device=dev)
-    src = torch.arange(S, dtype=torch.int32, device=dev)
+    src = torch.arange(S, dtype=torch.int32, device=dev) % d
     one = torch.ones(S, dtype=torch.float64, device=dev)
     half = torch.full((S,), 0.5, dtype=torch.float64, device=dev)
     fr = gpu.CandidateRound(d, S, kind, params, src, one, half, one.clone(), one.clone(),
