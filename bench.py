@@ -111,7 +111,8 @@ class KernelTimer:
         pairs = sum(M * N for (M, N, d) in self.shapes)
         self.channels = {}
         for name, ch in (("candidates", nat.ABC_PROF_CANDIDATES),
-                         ("regen", nat.ABC_PROF_REGEN)):
+                         ("regen", nat.ABC_PROF_REGEN),
+                         ("rescue", nat.ABC_PROF_RESCUE)):
             cm, cn = ctypes.c_double(0.0), ctypes.c_int64(0)
             nat.call("abc_profile_channel", ch, ctypes.addressof(cm), ctypes.addressof(cn))
             self.channels[name] = (cm.value, int(cn.value))
@@ -305,11 +306,12 @@ def main():
     # per-stage split of the timed region (HIP events on the launch streams)
     c_ms, c_n = timer.channels["candidates"]
     r_ms, r_n = timer.channels["regen"]
+    x_ms, x_n = timer.channels["rescue"]
     timed_cands = cand_per_gen[n_before:n_before + steps]
     n_cand = int(sum(timed_cands))
     stages = {"density_gemm_ms": k_ms, "candidate_rounds_ms": c_ms,
-              "regen_ms": r_ms,
-              "other_ms": 1e3 * elapsed - k_ms - c_ms - r_ms,
+              "regen_ms": r_ms, "density_rescue_ms": x_ms,
+              "other_ms": 1e3 * elapsed - k_ms - c_ms - r_ms - x_ms,
               "note": ("other = fit (moments, eigh, guide, x3 pack), epsilon "
                        "quantile, weights, compaction, host gaps")}
     cand = {"kernel": "fused_round_kernel (proposal + prior re-draw + "

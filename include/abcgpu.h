@@ -63,10 +63,12 @@ int abc_profile_begin(void);
 int abc_profile_end(double* total_ms, int64_t* launches);
 /* The other timing channels of the last begin/end window: ABC_PROF_DENSITY
  * (what abc_profile_end returns), ABC_PROF_CANDIDATES (the fused candidate
- * round kernel), ABC_PROF_REGEN (regeneration of kept rows). */
+ * round kernel), ABC_PROF_REGEN (regeneration of kept rows),
+ * ABC_PROF_RESCUE (the exact density pass over rescued candidates). */
 #define ABC_PROF_DENSITY 0
 #define ABC_PROF_CANDIDATES 1
 #define ABC_PROF_REGEN 2
+#define ABC_PROF_RESCUE 3
 int abc_profile_channel(int channel, double* total_ms, int64_t* launches);
 
 /* ---- reductions used by the fits ------------------------------------------

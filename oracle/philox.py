@@ -52,11 +52,61 @@ def uniform53(x0, x1):
     return (a * 67108864.0 + b) / 9007199254740992.0
 
 
+_BM = None
+
+
+def _bm_tables():
+    global _BM
+    if _BM is None:
+        import os
+        t = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "bm_tables.npz"))
+        _BM = {k: t[k] for k in t.files}
+    return _BM
+
+
 def normal_pairs(x0, x1):
-    """Box-Muller on two u32 streams -> two standard normals (float64).
-    The device evaluates the same formula with a table-driven fp64 transform
-    (abc_common.h box_muller) that agrees to a few ulp."""
-    u1 = uniform01(x0)
-    u2 = uniform01(x1)
-    r = np.sqrt(-2.0 * np.log(u1))
-    return r * np.cos(2 * np.pi * u2), r * np.sin(2 * np.pi * u2)
+    """Box-Muller on two u32 streams -> two standard normals, R cos / R sin of
+    2 pi u2 with R = sqrt(-2 ln u1), u = uniform01.  Restates the device
+    transform (pyabc_amd/csrc/abc_common.h box_muller) operation for
+    operation in float32 -- table-driven log and sin/cos, every operation
+    correctly rounded, sqrt through float64 -- so the normals replay the
+    device BIT FOR BIT (tests/test_gpu_kernels.py).  Tables:
+    oracle/bm_tables.npz (tools/gen_bm_tables.py)."""
+    T = _bm_tables()
+    f32 = np.float32
+    a = np.asarray(x0, dtype=np.uint32).astype(np.uint64)
+    b = np.asarray(x1, dtype=np.uint32).astype(np.uint64)
+    m1 = ((a >> np.uint64(9)) << np.uint64(1)) | np.uint64(1)
+    yi = np.uint64(1 << 24) - m1
+    # series branch: u1 > 1 - 2^-8
+    y = yi.astype(np.float32) * f32(2.0 ** -24)
+    z = y * f32(0.2) + f32(0.25)
+    z = z * y + f32(1 / 3)
+    z = z * y + f32(0.5)
+    z = z * y + f32(1.0)
+    v_series = z * y
+    # table branch
+    e = (np.frexp(m1.astype(np.float64))[1] - 1).astype(np.uint64)
+    t = (m1 << (np.uint64(31) - e)) & np.uint64(0xFFFFFFFF)
+    i = ((t >> np.uint64(24)) & np.uint64(127)).astype(np.int64)
+    delta = ((t >> np.uint64(8)) & np.uint64(0xFFFF)).astype(np.float32) * f32(2.0 ** -23)
+    r = delta * T["inv"][i]
+    p = r * f32(-0.25) + f32(1 / 3)
+    p = p * r - f32(0.5)
+    p = p * r + f32(1.0)
+    p = p * r
+    k = (np.uint64(24) - e).astype(np.float32)
+    LN2_HI, LN2_LO = f32(float.fromhex("0x1.62e4p-1")), f32(float.fromhex("0x1.7f7d1cp-20"))
+    v_table = (k * LN2_HI - T["hi"][i]) + ((k * LN2_LO - T["lo"][i]) - p)
+    v = np.where(yi < np.uint64(1 << 16), v_series, v_table).astype(np.float32)
+    R = np.sqrt((f32(2.0) * v).astype(np.float64)).astype(np.float32)
+    m2 = ((b >> np.uint64(9)) << np.uint64(1)) | np.uint64(1)
+    ia = (m2 >> np.uint64(16)).astype(np.int64)
+    bb = (m2 & np.uint64(0xFFFF)).astype(np.float32) * f32(float.fromhex("0x1.921fb6p-22"))
+    b2 = bb * bb
+    sb = bb - (bb * b2) * f32(1 / 6)
+    cb = f32(1.0) - b2 * (f32(0.5) - b2 * f32(1 / 24))
+    sa, ca = T["sc"][ia, 0], T["sc"][ia, 1]
+    sn = sa * cb + ca * sb
+    cs = ca * cb - sa * sb
+    return (R * cs).astype(np.float64), (R * sn).astype(np.float64)

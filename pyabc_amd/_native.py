@@ -100,7 +100,7 @@ ABC_ERR_HIP = -2
 ABC_ERR_WORKSPACE = -3
 ABC_ERR_NOT_ENOUGH_PARTICLES = -4
 ABC_ERR_UNSUPPORTED = -5
-ABC_PROF_DENSITY, ABC_PROF_CANDIDATES, ABC_PROF_REGEN = 0, 1, 2
+ABC_PROF_DENSITY, ABC_PROF_CANDIDATES, ABC_PROF_REGEN, ABC_PROF_RESCUE = 0, 1, 2, 3
 ABC_PREC_F64 = 0
 ABC_PREC_F32 = 1
 ABC_PREC_X3 = 2

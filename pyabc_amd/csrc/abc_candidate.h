@@ -32,7 +32,7 @@ constexpr uint32_t SLOT_SIM = 0x40000000u;
 // (1..4) are produced -- the pair the caller does not use is skipped)
 __device__ __forceinline__ void normals4(uint64_t g, uint32_t slot, uint32_t gen,
                                          uint64_t seed, double n[4], int need = 4,
-                                         const double* tab = BM_TAB) {
+                                         const float* tab = BM_TAB) {
   u32x4 r = philox(g, slot, gen, seed);
   box_muller(r.x, r.y, n[0], n[1], tab);
   if (need > 2) box_muller(r.z, r.w, n[2], n[3], tab);
@@ -339,7 +339,7 @@ struct SimDistArgs {
 constexpr int SIM_SMAX = 256;     // fused path: S <= SIM_SMAX
 constexpr int LT_DMAX = 16;       // shared L staged for d <= 16
 struct BlockConsts {
-  double bmt[BM_TAB_SIZE];        // Box-Muller tables (BM_TAB)
+  float bmt[BM_TAB_SIZE];         // Box-Muller tables (BM_TAB)
   double LT[LT_DMAX * LT_DMAX];   // shared L, transposed: LT[q d + k] = L[k d + q]
   double box[2 * 64];             // prior support [lo, hi] per dimension
   double2 as[SIM_SMAX];           // (a_k, sigma_k)

@@ -81,91 +81,74 @@ __device__ __forceinline__ double uniform53(uint32_t a, uint32_t b) {
 }  // namespace abc
 #include "abc_bm_tables.h"
 namespace abc {
-__device__ __forceinline__ void stage_bm_tab(double* lds) {
+__device__ __forceinline__ void stage_bm_tab(float* lds) {
   for (int k = threadIdx.x; k < BM_TAB_SIZE; k += blockDim.x) lds[k] = BM_TAB[k];
   __syncthreads();
 }
 
-// Box-Muller in fp64: n0 = R cos(2 pi u2), n1 = R sin(2 pi u2),
-// R = sqrt(-2 ln u1), u = uniform01 (the formula of oracle.philox.normal_pairs).
-// The uniforms carry 24 significant bits (u = m 2^-24, m odd), so the
-// transform is table-driven instead of calling the general fp64 log /
-// sincospi / sqrt (~200 VALU instructions per pair, most of the candidate
-// kernels' work):
-//   ln: m = 2^e f, f in [1, 2); with c = 1 + (i + 1/2)/256 for the top 8
-//     fraction bits i, ln f = -ln(INV_C[i]) + log1p(f INV_C[i] - 1), the
-//     table value a double-double and log1p a degree-7 series on
-//     |r| < 2^-8; -ln u1 = (24 - e) ln2 - ln f, where the leading
-//     difference is exact when it cancels (Sterbenz), so the result is good to
-//     ~1 ulp even for u1 -> 1;
-//   sqrt: v_rsq_f64 seed + two Newton steps + one residual correction;
+// Box-Muller: n0 = R cos(2 pi u2), n1 = R sin(2 pi u2), R = sqrt(-2 ln u1),
+// u = uniform01 (24 significant bits: u = m 2^-24, m odd).  The transform is
+// evaluated in fp32 -- the precision its 24-bit inputs carry -- with only
+// correctly rounded operations in a fixed order (no contraction; sqrt through
+// fp64, exact after the final rounding; 4 KB of tables), so that
+// oracle/philox.py normal_pairs replays it bit for bit in numpy float32:
+//   ln: m = 2^e f, f = c_i + delta with c_i = 1 + i/128 for the top 7
+//     fraction bits i (delta exact); ln f = ln c_i + log1p(delta / c_i),
+//     the table value an fp32 pair and log1p a degree-4 series on
+//     [0, 2^-7); -ln u1 = (24 - e) ln2 - ln f, whose leading difference is
+//     exact where it cancels; for u1 > 1 - 2^-8 the series of -ln(1 - y),
+//     y = 1 - u1 exact (a rare branch);
 //   sin/cos: angle = pi i / 128 + pi j 2^-23 (i, j = high 8 / low 16 bits of
-//     m2): table sin/cos of the first + degree-7/8 series of the second,
+//     m2): table sin/cos of the first, degree-3/4 series of the second,
 //     combined by the angle-addition formulas.
-// Agrees with the libm formula to a few ulp (the oracle tests' 1e-12).
-
-// tab: BM_TAB or a copy of it in LDS (the hot kernels stage one per block:
-// three random-index table reads per pair from global memory cost more
-// latency than the arithmetic they save)
+// Within ~4 fp32 ulp of R of the exact transform (tests/test_gpu_fused.py).
+// tab: BM_TAB or a copy of it in LDS (the hot kernels stage one per block).
 __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, double& n0,
-                                           double& n1, const double* tab = BM_TAB) {
-  constexpr double LN2_HI = 0x1.62e42fefa3800p-1;   // 42 significant bits
-  constexpr double LN2_LO = 0x1.ef35793c76730p-45;  // ln 2 - LN2_HI
-  // ---- R = sqrt(-2 ln u1), u1 = m1 2^-24
+                                           double& n1, const float* tab = BM_TAB) {
+#pragma clang fp contract(off)
+  constexpr float LN2_HI = 0x1.62e4p-1f;      // 17 significant bits
+  constexpr float LN2_LO = 0x1.7f7d1cp-20f;   // ln 2 - LN2_HI
+  constexpr float C3 = 0x1.555556p-2f, C5 = 0x1.99999ap-3f;  // 1/3, 1/5
+  constexpr float C6 = 0x1.555556p-3f, C24 = 0x1.555556p-5f;  // 1/6, 1/24
+  constexpr float PI_2M23 = 0x1.921fb6p-22f;  // pi 2^-23
+  // ---- v = -ln u1, u1 = m1 2^-24
   const uint32_t m1 = ((a >> 9) << 1) | 1u;
-  const int e = 31 - __clz((int)m1);                // floor(log2 m1), 0..23
-  const uint32_t t = m1 << (31 - e);                // leading one at bit 31
-  const int i = (int)((t >> 23) & 255u);
-  const double f = (double)(t >> 8) * 0x1p-23;      // m1 / 2^e in [1, 2), exact
-  const double ic = tab[BM_TAB_LOG + 2 * i], lh = tab[BM_TAB_LOG + 2 * i + 1];
-  const double ll = tab[BM_TAB_LO + i];
-  const double r = fma(f, ic, -1.0);
-  double q = fma(r, 1.0 / 7.0, -1.0 / 6.0);
-  q = fma(r, q, 1.0 / 5.0);
-  q = fma(r, q, -1.0 / 4.0);
-  q = fma(r, q, 1.0 / 3.0);
-  q = fma(r, q, -0.5);
-  const double p = fma(r * r, q, r);                // log1p(r)
-  const double k = (double)(24 - e);
-  double v = fma(k, LN2_HI, -lh) + (fma(k, LN2_LO, -ll) - p);  // -ln u1
   const uint32_t yi = (1u << 24) - m1;
-  if (yi < (1u << 15)) {
-    // u1 > 1 - 2^-9: -ln u1 cancels to |v| >= 2^-24 above; the series of
-    // -ln(1 - y), y = 1 - u1 exact, keeps it to an ulp (rare: a branch)
-    const double yy = (double)yi * 0x1p-24;
-    double z = fma(yy, 1.0 / 7.0, 1.0 / 6.0);
-    z = fma(yy, z, 1.0 / 5.0);
-    z = fma(yy, z, 1.0 / 4.0);
-    z = fma(yy, z, 1.0 / 3.0);
-    z = fma(yy, z, 0.5);
-    v = fma(yy * yy, z, yy);
+  float v;
+  if (yi < (1u << 16)) {
+    const float y = (float)yi * 0x1p-24f;
+    float z = y * C5 + 0.25f;
+    z = z * y + C3;
+    z = z * y + 0.5f;
+    z = z * y + 1.0f;
+    v = z * y;
+  } else {
+    const int e = 31 - __clz((int)m1);               // floor(log2 m1), 0..22
+    const uint32_t t = m1 << (31 - e);               // leading one at bit 31
+    const int i = (int)((t >> 24) & 127u);
+    const float delta = (float)((t >> 8) & 0xFFFFu) * 0x1p-23f;
+    const float* lg = tab + BM_TAB_LOG + 4 * i;      // (INV_C, LN_HI, LN_LO, 0)
+    const float r = delta * lg[0];
+    float p = r * -0.25f + C3;
+    p = p * r - 0.5f;
+    p = p * r + 1.0f;
+    p = p * r;                                       // log1p(r)
+    const float k = (float)(24 - e);
+    v = (k * LN2_HI - lg[1]) + ((k * LN2_LO - lg[2]) - p);
   }
-  const double x = 2.0 * v;
-  double y = __builtin_amdgcn_rsq(x);
-  const double hx = 0.5 * x;
-  double c = fma(-hx * y, y, 0.5);
-  y = fma(y, c, y);
-  c = fma(-hx * y, y, 0.5);
-  y = fma(y, c, y);
-  double R = x * y;
-  R = fma(fma(-R, R, x), 0.5 * y, R);
+  const float R = (float)sqrt((double)(2.0f * v));
   // ---- (cos, sin)(pi m2 2^-23), m2 = 2 (b >> 9) + 1
   const uint32_t m2 = ((b >> 9) << 1) | 1u;
-  const int ia = (int)(m2 >> 16);
-  const double ang = (double)(m2 & 0xFFFFu) * 0x1.921fb54442d18p-22;  // pi 2^-23 j
-  const double a2 = ang * ang;
-  double ps = fma(a2, -1.0 / 5040.0, 1.0 / 120.0);
-  ps = fma(a2, ps, -1.0 / 6.0);
-  const double sb = fma(ang * a2, ps, ang);
-  double pc = fma(a2, 1.0 / 40320.0, -1.0 / 720.0);
-  pc = fma(a2, pc, 1.0 / 24.0);
-  pc = fma(a2, pc, -0.5);
-  const double cb = fma(a2, pc, 1.0);
-  const double sa = tab[BM_TAB_SC + 2 * ia], ca = tab[BM_TAB_SC + 2 * ia + 1];
-  const double sn = fma(sa, cb, ca * sb);
-  const double cs = fma(ca, cb, -(sa * sb));
-  n0 = R * cs;
-  n1 = R * sn;
+  const float* sc = tab + BM_TAB_SC + 2 * (int)(m2 >> 16);
+  const float bb = (float)(m2 & 0xFFFFu) * PI_2M23;
+  const float b2 = bb * bb;
+  const float sb = bb - (bb * b2) * C6;
+  const float cb = 1.0f - b2 * (0.5f - b2 * C24);
+  const float sa = sc[0], ca = sc[1];
+  const float sn = sa * cb + ca * sb;
+  const float cs = ca * cb - sa * sb;
+  n0 = (double)(R * cs);
+  n1 = (double)(R * sn);
 }
 
 // ---- wave helpers (wave64) ---------------------------------------------------

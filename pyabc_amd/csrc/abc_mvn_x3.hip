@@ -773,7 +773,7 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
               const double* X, const double* w, int64_t N, const double* mu,
               const double* U, int r, double log_const, double log_norm,
               double* out, const int64_t* hint, void* ws, size_t ws_bytes,
-              hipStream_t s) {
+              hipStream_t s, int prof_channel) {
   if (r > MAX_R)
     return set_error(ABC_ERR_UNSUPPORTED, "mvn x3: rank %d > %d", r, MAX_R);
   PlanX3 p = make_plan_x3(M, N, r);
@@ -797,9 +797,9 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
                  p.KB, hdr, Bimg, p.MTpad, cflags, x3_Y(packed, N, r),
                  x3_lw(packed, N, r), N, hint, hint ? cand_o : (float*)nullptr, r + 6);
   ABC_LAUNCHED();
-  profile_start(s);
+  profile_start(s, prof_channel);
   int rc = dispatch_x3(p, Aimg, (const half8*)Bimg, r + 6, po, pl, hint == nullptr, s);
-  profile_stop(s);
+  profile_stop(s, prof_channel);
   if (rc) return rc;
   ABC_LAUNCHED();
   hipLaunchKernelGGL(x3_combine_kernel, dim3((unsigned)ceil_div(M, 256)), dim3(256),
@@ -829,7 +829,7 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
                          dim3(256), 0, s, rescue, (int64_t)nh, x, d, xs);
       ABC_LAUNCHED();
       const int rc2 = x3_logpdf(xs, nh, d, packed, X, w, N, mu, U, r, log_const, log_norm,
-                                outs, nullptr, ws2, need + 256, s);
+                                outs, nullptr, ws2, need + 256, s, ABC_PROF_RESCUE);
       if (rc2) return rc2;
       hipLaunchKernelGGL(x3_scatter_rescued, dim3((unsigned)ceil_div(nh, 256)), dim3(256), 0,
                          s, rescue, (int64_t)nh, outs, out);

@@ -3,20 +3,21 @@
 // kernel is launched on, directly around that one launch, per channel
 // (ABC_PROF_DENSITY: the transition-density GEMM + exp2 + sum launch;
 // ABC_PROF_CANDIDATES: the fused candidate round; ABC_PROF_REGEN: the
-// regeneration of kept rows).
+// regeneration of kept rows; ABC_PROF_RESCUE: the unhinted density re-run of
+// rescued candidates).
 #include <mutex>
 #include <vector>
 #include "abc_common.h"
 
 namespace {
 struct Pair { hipEvent_t a, b; };
-constexpr int NCH = 3;
+constexpr int NCH = 4;
 std::mutex g_mu;
 bool g_on = false;
 std::vector<Pair> g_pool[NCH];   // created once, reused
-size_t g_used[NCH] = {0, 0, 0};
-double g_ms[NCH] = {0, 0, 0};
-int64_t g_n[NCH] = {0, 0, 0};
+size_t g_used[NCH] = {0, 0, 0, 0};
+double g_ms[NCH] = {0, 0, 0, 0};
+int64_t g_n[NCH] = {0, 0, 0, 0};
 }  // namespace
 
 namespace abc {

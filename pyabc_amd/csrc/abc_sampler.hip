@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void simulate_lg_kernel(
     const double* __restrict__ sigma, uint64_t seed, uint32_t gen,
     int64_t idx0, double* __restrict__ x) {
   // one thread per (candidate, group of 4 stats): coalesced over k
-  __shared__ double sbmt[BM_TAB_SIZE];
+  __shared__ float sbmt[BM_TAB_SIZE];
   stage_bm_tab(sbmt);
   const int G = (S + 3) >> 2;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -270,31 +270,30 @@ def test_sampler_fused_equals_staged(dev, adaptive, local, max_fused, S):
 
 
 def test_box_muller_accuracy(dev):
-    """The table-driven fp64 Box-Muller transform (abc_common.h) against an
-    80-bit long-double evaluation of R cos / R sin, R = sqrt(-2 ln u1), on
-    4M draws (the simulator with a = 0, sigma = 1 returns the raw normals):
-    within 4 ulp of R (|n| <= R <= 5.8; the table sin/cos and their
-    combination carry ~2e-16 absolute, times R)."""
+    """The fp32 Box-Muller transform (abc_common.h): on 4M draws (the
+    simulator with a = 0, sigma = 1 returns the raw normals) the device
+    normals equal the oracle's float32 replay (oracle/philox.py
+    normal_pairs) BIT FOR BIT, and are within 4 fp32 ulp of R of an 80-bit
+    long-double evaluation of R cos / R sin, R = sqrt(-2 ln u1)."""
     from pyabc_amd import gpu
-    from oracle.philox import philox4x32_10
+    from oracle.philox import normal_pairs, philox4x32_10
     B, S = 1 << 20, 4
     th = torch.zeros((B, 1), dtype=torch.float64, device=dev)
     x = gpu.simulate_linear_gaussian(th, T(np.zeros(S), torch.int32), T(np.zeros(S)),
                                      T(np.ones(S)), 5, 6, 7).cpu().numpy()
     idx = np.arange(7, 7 + B, dtype=np.uint64)
-    r = philox4x32_10(idx, 0x40000000, 6, 5).astype(np.uint64)
+    r = philox4x32_10(idx, 0x40000000, 6, 5)
     ld = np.longdouble
-    out = np.empty((B, 4))
     for h in range(2):
-        m1 = ((r[:, 2 * h] >> np.uint64(9)) * 2 + 1).astype(ld)
-        m2 = ((r[:, 2 * h + 1] >> np.uint64(9)) * 2 + 1).astype(ld)
+        ref = np.stack(normal_pairs(r[:, 2 * h], r[:, 2 * h + 1]), 1)
+        np.testing.assert_array_equal(x[:, 2 * h:2 * h + 2], ref)
+        rr = r.astype(np.uint64)
+        m1 = ((rr[:, 2 * h] >> np.uint64(9)) * 2 + 1).astype(ld)
+        m2 = ((rr[:, 2 * h + 1] >> np.uint64(9)) * 2 + 1).astype(ld)
         R = np.sqrt(-2 * np.log(m1 * ld(2.0) ** -24))
         ang = ld("3.14159265358979323846264338327950288") * m2 * ld(2.0) ** -23
-        out[:, 2 * h] = (R * np.cos(ang)).astype(np.float64)
-        out[:, 2 * h + 1] = (R * np.sin(ang)).astype(np.float64)
-        Rm = R.astype(np.float64)
-        err = np.abs(x[:, 2 * h:2 * h + 2] - out[:, 2 * h:2 * h + 2])
-        ulp = err / np.spacing(Rm)[:, None]
-        w = np.unravel_index(np.argmax(ulp), ulp.shape)
-        assert ulp.max() <= 4, (ulp.max(), int(r[w[0], 2 * h]), int(r[w[0], 2 * h + 1]),
-                                float(Rm[w[0]]), float(err[w]))
+        exact = np.stack([(R * np.cos(ang)).astype(np.float64),
+                          (R * np.sin(ang)).astype(np.float64)], 1)
+        ulp = np.abs(x[:, 2 * h:2 * h + 2] - exact) / \
+            np.spacing(R.astype(np.float32)).astype(np.float64)[:, None]
+        assert ulp.max() <= 4, ulp.max()

@@ -6,14 +6,17 @@ against the reference's own samplers on identical work, in THIS container
         OMP_NUM_THREADS=1 python tools/calibrate_cpu_baseline.py
 
 Config: the 10-D conjugate model (c2 shape) at population 1000,
-QuantileEpsilon(0.5), PNormDistance, MultivariateNormalTransition, 3
-generations.  For each reference sampler (SingleCoreSampler,
+QuantileEpsilon(0.5), PNormDistance, MultivariateNormalTransition, 5
+generations (t = 1..3 compared: proposals from the transition and a density
+per accepted particle).  For each reference sampler (SingleCoreSampler,
 MulticoreEvalParallelSampler(n_procs=8)) the sample_until_n_accepted call of
 every generation is timed together with its evaluation count.  The port is
 timed on the same work: n_sim candidates (proposal, prior, simulation,
 distance; oracle/sampler.py) + n accepted transition densities against the
-population (oracle/transition.py), one core.  Writes
-profiles/r02_cpu_calibration.json.
+population (oracle/transition.py), one core.  At the c3 population (N =
+1e6, d = 10) the density dominates; one reference MultivariateNormalTransition
+.pdf call (smc.py:743 evaluates one per accepted particle) is timed against
+the port's density of one point.  Writes profiles/r02_cpu_calibration.json.
 """
 import json
 import os
@@ -30,7 +33,7 @@ import stub_env  # noqa: E402,F401  (before pyabc)
 import pyabc  # noqa: E402
 from pyabc.epsilon import QuantileEpsilon  # noqa: E402
 
-D, POP, GENS = 10, 1000, 3
+D, POP, GENS = 10, 1000, 5
 
 
 def run_reference(sampler):
@@ -94,8 +97,8 @@ def main():
     t_cand, t_pdf = port_rates(X, w)
     rows = []
     for g, (s, m) in enumerate(zip(single, multi)):
-        if g == 0:
-            continue   # calibration sample (prior, all accepted)
+        if g <= 1:
+            continue   # calibration sample and t = 0 (prior draws, no density)
         port_s = s["n_sim"] * t_cand + s["n"] * t_pdf
         rows.append(dict(generation=g - 1, n=s["n"], n_sim_single=s["n_sim"],
                          n_sim_multi=m["n_sim"],
@@ -106,8 +109,32 @@ def main():
     res["port_seconds_per_candidate"] = t_cand
     res["port_seconds_per_density_N1000"] = t_pdf
     res["generations"] = rows
+    # generations t >= 1 (proposal from the transition + density per accepted)
     res["ratio_single_over_port"] = float(np.median([r["single_over_port"] for r in rows]))
     res["ratio_multi8_over_port"] = float(np.median([r["multi8_over_port"] for r in rows]))
+    # c3-sized density: the reference's per-particle pdf vs the port's
+    import pandas as pd
+    import oracle
+    from pyabc.transition import MultivariateNormalTransition
+    rng = np.random.default_rng(3)
+    N = 1_000_000
+    Xb = rng.normal(0.8, 0.45, (N, D))
+    wb = np.full(N, 1.0 / N)
+    cols = [f"p{k}" for k in range(D)]
+    tr = MultivariateNormalTransition()
+    tr.fit(pd.DataFrame(Xb, columns=cols), wb.copy())
+    pt = pd.Series(Xb[0] + 0.1, index=cols)
+    tr.pdf(pt)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        tr.pdf(pt)
+    t_ref = (time.perf_counter() - t0) / 5
+    t0 = time.perf_counter()
+    for _ in range(5):
+        oracle.mvn_logpdf(Xb[:1] + 0.1, Xb, wb, tr.cov, block=1)
+    t_port = (time.perf_counter() - t0) / 5
+    res["density_N1e6"] = dict(reference_pdf_call_s=t_ref, port_density_s=t_port,
+                               reference_over_port=t_ref / t_port)
     out = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
