@@ -44,14 +44,16 @@ __device__ __forceinline__ double dist2(const double* __restrict__ X, int64_t j,
   return dist2v<D>(xj, xn);
 }
 
+// LU with partial pivoting (getrf order: pivot = first max |a[r][c]|,
+// multipliers l = a[r][c] * (1 / pivot)); returns det and keeps the factors
+// in a, the row permutation in perm.  The determinant and the inverse come
+// from the same factors, as la.det and la.inv (getrf + getri) do in the
+// reference: with two independently rounded factorisations a nearly
+// singular covariance could pass "det > 0" while its inverse is indefinite.
 template <int D>
-__device__ double det_lu(const double (&a_in)[D][D]) {
-  double a[D][D];
-#pragma unroll
-  for (int i = 0; i < D; ++i)
-#pragma unroll
-    for (int j = 0; j < D; ++j) a[i][j] = a_in[i][j];
+__device__ double lu_factor(double (&a)[D][D], int (&perm)[D]) {
   double det = 1.0;
+  for (int i = 0; i < D; ++i) perm[i] = i;
   for (int c = 0; c < D; ++c) {
     int p = c;
     double best = fabs(a[c][c]);
@@ -60,40 +62,39 @@ __device__ double det_lu(const double (&a_in)[D][D]) {
     if (a[p][c] == 0.0) return 0.0;
     if (p != c) {
       for (int j = 0; j < D; ++j) { double t = a[c][j]; a[c][j] = a[p][j]; a[p][j] = t; }
+      const int t = perm[c]; perm[c] = perm[p]; perm[p] = t;
       det = -det;
     }
     det *= a[c][c];
+    const double rp = 1.0 / a[c][c];
     for (int r = c + 1; r < D; ++r) {
-      double f = a[r][c] / a[c][c];
+      const double f = a[r][c] * rp;
+      a[r][c] = f;
       for (int j = c + 1; j < D; ++j) a[r][j] -= f * a[c][j];
     }
   }
   return det;
 }
 
+// inverse from the factors of lu_factor (det != 0): column j of A^-1 solves
+// L U x = P e_j
 template <int D>
-__device__ void inverse_gj(const double (&a_in)[D][D], double (&inv)[D][D]) {
-  double a[D][2 * D];
-  for (int i = 0; i < D; ++i)
-    for (int j = 0; j < D; ++j) { a[i][j] = a_in[i][j]; a[i][D + j] = (i == j) ? 1.0 : 0.0; }
-  for (int c = 0; c < D; ++c) {
-    int p = c;
-    double best = fabs(a[c][c]);
-    for (int r = c + 1; r < D; ++r)
-      if (fabs(a[r][c]) > best) { best = fabs(a[r][c]); p = r; }
-    if (p != c)
-      for (int j = 0; j < 2 * D; ++j) { double t = a[c][j]; a[c][j] = a[p][j]; a[p][j] = t; }
-    const double piv = a[c][c];
-    for (int j = 0; j < 2 * D; ++j) a[c][j] /= piv;
-    for (int r = 0; r < D; ++r) {
-      if (r == c) continue;
-      const double f = a[r][c];
-      if (f != 0.0)
-        for (int j = 0; j < 2 * D; ++j) a[r][j] -= f * a[c][j];
+__device__ void lu_inverse(const double (&lu)[D][D], const int (&perm)[D],
+                           double (&inv)[D][D]) {
+  for (int j = 0; j < D; ++j) {
+    double x[D];
+    for (int i = 0; i < D; ++i) {
+      double v = perm[i] == j ? 1.0 : 0.0;
+      for (int k = 0; k < i; ++k) v -= lu[i][k] * x[k];
+      x[i] = v;
     }
+    for (int i = D - 1; i >= 0; --i) {
+      double v = x[i];
+      for (int k = i + 1; k < D; ++k) v -= lu[i][k] * x[k];
+      x[i] = v / lu[i][i];
+    }
+    for (int i = 0; i < D; ++i) inv[i][j] = x[i];
   }
-  for (int i = 0; i < D; ++i)
-    for (int j = 0; j < D; ++j) inv[i][j] = a[i][D + j];
 }
 
 // Cholesky; on a non-positive pivot fall back to sqrt(|diag|) (the reference
@@ -552,13 +553,18 @@ __global__ __launch_bounds__(256) void local_finish_kernel(
     for (int a = 0; a < D; ++a) cov[a][a] = fabs(X[a]);  // X[0, a]
   for (int a = 0; a < D; ++a)
     for (int b = 0; b < D; ++b) cov[a][b] *= scaling;
-  double det = det_lu<D>(cov);
-  for (int it = 0; det <= 0.0 && it < 1000000; ++it) {
+  double lu[D][D];
+  int perm[D];
+  double det;
+  for (int it = 0;; ++it) {
+    for (int a = 0; a < D; ++a)
+      for (int b = 0; b < D; ++b) lu[a][b] = cov[a][b];
+    det = lu_factor<D>(lu, perm);
+    if (det > 0.0 || it >= 1000000) break;
     for (int a = 0; a < D; ++a) cov[a][a] += eps;
-    det = det_lu<D>(cov);
   }
   double inv[D][D], L[D][D];
-  inverse_gj<D>(cov, inv);
+  lu_inverse<D>(lu, perm, inv);
   cholesky<D>(cov, L);
   for (int a = 0; a < D; ++a)
     for (int b = 0; b < D; ++b) {

@@ -196,6 +196,36 @@ def test_local_golden(dev, tag, kw):
     np.testing.assert_allclose(pdf, gg["pdf"], rtol=1e-6)
 
 
+@pytest.mark.parametrize("d", [2, 3])
+def test_local_fit_singular_neighbourhoods(dev, d):
+    """d + 1 particles: every neighbour covariance is exactly singular and
+    local_transition.py:112-123 ("while det <= 0: cov += EPS I") runs on
+    rounding noise.  Whatever the noise decides, det and inverse must come
+    from one factorisation (la.det / la.inv share getrf in the reference):
+    a covariance kept with det > 0 has an inverse with a positive diagonal,
+    and the densities stay finite and below the largest kernel's peak."""
+    import pandas as pd
+    from pyabc_amd.transition import LocalTransition
+    rng = np.random.default_rng(77 + d)
+    cols = [f"p{k}" for k in range(d)]
+    for rep in range(150):
+        X = rng.random((d + 1, d))
+        t = LocalTransition()
+        t.fit(pd.DataFrame(X, columns=cols), np.ones(d + 1) / (d + 1))
+        dets = t._dev_dets.cpu().numpy()
+        inv = t._dev_inv.cpu().numpy()
+        assert (dets > 0).all()
+        assert (np.einsum("nii->ni", inv) > 0).all(), (rep, dets, inv)
+        ld = t.logpdf_device(gpu_as(rng.random((4, d)), dev)).cpu().numpy()
+        peak = (-0.5 * (d * np.log(2 * np.pi) + np.log(dets))).max()
+        assert np.all(ld <= peak + 1e-6 * abs(peak)), (rep, ld, peak)
+
+
+def gpu_as(a, dev):
+    from pyabc_amd import gpu
+    return gpu.as_dev(a, device=dev)
+
+
 @pytest.mark.parametrize("grid,N,d,k", [(None, 3000, 5, 50), (None, 3000, 5, 700),
                                          (7, 2000, 3, 50), (2, 1500, 3, 40),
                                          (None, 12000, 5, 3000), (None, 4096, 2, 10),
