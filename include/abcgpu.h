@@ -233,7 +233,18 @@ typedef struct abc_candidate_spec {
   double p;                    /*        p >= 1, +inf = max norm           */
   uint64_t seed;
   uint32_t generation;
+  const void* anc_table;       /* abc_ancestor_table of (X, cdf); required
+                                  with X (the guide field is then unused) */
 } abc_candidate_spec;
+/* Ancestor table of a population for the fused rounds: the rows X_j with
+ * their weight-scan value in 128-byte-aligned records, and a guide over
+ * 4 N scan bins (abc_candidate.h).  Same ancestors as the cdf / guide
+ * search (np.searchsorted(cdf, u * total, side="right"), smc.py:652 via
+ * multivariatenormal.py:90-94), fewer cache lines per draw.  table: device
+ * buffer of abc_ancestor_table_bytes(N, d) bytes, 128-byte aligned. */
+int64_t abc_ancestor_table_bytes(int64_t N, int d);
+int abc_ancestor_table(const double* X, const double* cdf, int64_t N, int d,
+                       void* table, size_t table_bytes, void* stream);
 /* One round of B candidates: writes the positions b (0 <= b < B, increasing)
  * of the first `cap` accepted candidates to idx and the number accepted in
  * the round (uncapped) to *count (device int64).  rec_x (nullable) receives

@@ -69,7 +69,8 @@ def normal_pairs(x0, x1):
     2 pi u2 with R = sqrt(-2 ln u1), u = uniform01.  Restates the device
     transform (pyabc_amd/csrc/abc_common.h box_muller) operation for
     operation in float32 -- table-driven log and sin/cos, every operation
-    correctly rounded, sqrt through float64 -- so the normals replay the
+    correctly rounded (the device's sqrt_rn is the correctly rounded fp32
+    sqrt, here float64 sqrt rounded once) -- so the normals replay the
     device BIT FOR BIT (tests/test_gpu_kernels.py).  Tables:
     oracle/bm_tables.npz (tools/gen_bm_tables.py)."""
     T = _bm_tables()

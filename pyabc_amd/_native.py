@@ -41,6 +41,8 @@ SIGNATURES = {
     "abc_mvn_logpdf_direct": (I32, [P, I64, P, P, I64, I32, P, I32, P, I32,
                                     D, D, P, P]),
     "abc_cdf_guide": (I32, [P, I64, P, P]),
+    "abc_ancestor_table_bytes": (I64, [I64, I32]),
+    "abc_ancestor_table": (I32, [P, P, I64, I32, P, SZ, P]),
     "abc_propose": (I32, [P, P, P, I64, I32, P, P, P, U64, U32, I64, I64, I32,
                           P, P, P, P, P]),
     "abc_prior_logpdf": (I32, [P, I64, I32, P, P, P, P]),
@@ -90,7 +92,7 @@ class CandidateSpec(C.Structure):
                 ("prior_kind", P), ("prior_params", P), ("max_attempts", C.c_int),
                 ("src", P), ("a", P), ("sigma", P),
                 ("x0", P), ("wf", P), ("p", D),
-                ("seed", U64), ("generation", U32)]
+                ("seed", U64), ("generation", U32), ("anc_table", P)]
 
 
 # C error codes (include/abcgpu.h)

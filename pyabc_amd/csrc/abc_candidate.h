@@ -246,6 +246,18 @@ __device__ __forceinline__ int64_t ancestor_finish(const double* __restrict__ cd
   return lo < N ? lo : N - 1;
 }
 
+// search of the ancestor table's bracket [lo, hi] (hi inclusive; hi == N:
+// past the last row), the scan read from the records (rec[i rs + d] = cdf_i)
+__device__ __forceinline__ int64_t table_finish(const double* __restrict__ rec, int rs, int d,
+                                                int64_t N, double target, AncestorBracket b) {
+  int64_t lo = b.lo, hi = b.hi;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (rec[mid * rs + d] > target) hi = mid; else lo = mid + 1;
+  }
+  return lo < N ? lo : N - 1;
+}
+
 // ---- exact support box ------------------------------------------------------
 // The support {x : prior_in_support1(kind, p, x)} of every kind is an
 // interval of doubles (y = (x - loc) / scale is monotone in x, and so is each
@@ -314,7 +326,37 @@ struct ProposalArgs {
   int max_attempts;
   uint64_t seed;
   uint32_t gen;
+  // ancestor table (abc_ancestor_table; rec == nullptr: X / cdf / guide)
+  const double* rec = nullptr;     // records [N x rs]: X_j, cdf_j, padding
+  const int32_t* bguide = nullptr; // exact-bin guide [G + 2]
+  int rs = 0;
+  int64_t G = 0;
 };
+
+// ---- ancestor table -----------------------------------------------------------
+// The ancestor draw reads, per candidate, a guide entry, the weight scan near
+// the answer and the answer's row: three random cache lines or more from the
+// Infinity Cache at c3 sizes (cdf 8 MB, X 80 MB), which bound the fused round
+// (tools/bench_fused.py --N: 3.1e10 candidates/s at N = 1e3, 1.9e10 at 1e6).
+// The table keeps each row in a 128-byte-aligned record with its scan value
+// (rs = 16 doubles for d <= 15), and a guide over G = 4 N bins of the scan,
+// bin(x) = min(floor(x * G / total), G), guide[k] = first i with
+// bin(cdf_i) >= k.  bin is monotone and both sides evaluate it identically,
+// so for target t with kt = bin(t), i* = first i with cdf_i > t lies in
+// [guide[kt], guide[kt + 1]] (i < guide[kt]: bin(cdf_i) < kt, so cdf_i < t;
+// bin(cdf_{guide[kt+1]}) > kt, so cdf > t): np.searchsorted's answer, with
+// no probe when the two entries agree (most bins at G = 4 N) and otherwise
+// probes that read the records holding the candidate rows themselves.
+constexpr int ANC_HDR = 256;  // table header bytes
+__host__ __device__ inline int anc_rs(int d) { return (d + 1 + 15) / 16 * 16; }
+__host__ __device__ inline int64_t anc_bins(int64_t N) {
+  const int64_t g = 4 * N;
+  return g < (int64_t)0x7FFFFFF0 ? g : (int64_t)0x7FFFFFF0;
+}
+__device__ __forceinline__ int64_t anc_bin(double x, double inv_step, int64_t G) {
+  const double b = x * inv_step;  // x >= 0
+  return b >= (double)G ? G : (int64_t)b;
+}
 
 // MODE: PROP_MVN (one shared L), PROP_LOCAL (per-particle L), PROP_PRIOR
 // (X == nullptr: draw from the prior).  Separate instantiations keep the
@@ -346,6 +388,7 @@ struct BlockConsts {
   double2 wx[SIM_SMAX];           // (wf_k, x0_k)
   int32_t src[SIM_SMAX];
   double total;                   // cdf[N - 1]
+  double inv_step;                // G / total (ancestor table)
 };
 
 // Fill C (every thread of the block calls it; synchronises).  BOX_FROM_SRC:
@@ -371,7 +414,11 @@ __device__ __forceinline__ void stage_block_consts(BlockConsts& C, const Proposa
       C.wx[k] = make_double2(M->wf[k], M->x0[k]);
       C.src[k] = M->src[k];
     }
-  if (t == 0) C.total = (MODE != PROP_PRIOR) ? A.cdf[A.N - 1] : 0.0;
+  if (t == 0) {
+    const double total = (MODE != PROP_PRIOR) ? A.cdf[A.N - 1] : 0.0;
+    C.total = total;
+    C.inv_step = (MODE != PROP_PRIOR && A.rec) ? (double)A.G / total : 0.0;
+  }
   __syncthreads();
 }
 
@@ -382,7 +429,7 @@ __device__ __forceinline__ void stage_block_consts(BlockConsts& C, const Proposa
 // starting from X_jk (one code copy of the transform).  Returns the attempts
 // used, max_attempts + 1 when every attempt fell outside the support (theta
 // then holds the last one).
-template <int D, int MODE>
+template <int D, int MODE, bool TABLE = false>
 __device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockConsts& C,
                                            uint64_t g, double* th, int64_t& j) {
   constexpr bool LT_LDS = MODE == PROP_MVN && D > 0 && D <= LT_DMAX;
@@ -409,13 +456,20 @@ __device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockCon
       // the search and the X_j row come after: theta_k = X_jk + (L n)_k
       u32x4 r = philox(g, s0 + SLOT_ANCESTOR, A.gen, A.seed);
       const double target = uniform53(r.x, r.y) * total;
-      AncestorBracket br = ancestor_bracket(A.guide, A.N, total, target);
+      AncestorBracket br;
+      if (TABLE) {
+        const int64_t kt = anc_bin(target, C.inv_step, A.G);
+        br = {A.bguide[kt], A.bguide[kt + 1]};  // answer in [lo, hi]
+      } else {
+        br = ancestor_bracket(A.guide, A.N, total, target);
+      }
 #pragma unroll
       for (int k = 0; k < (D > 0 ? D : d); ++k) th[k] = 0.0;
       const double* Lj = A.L;
       if (MODE == PROP_LOCAL) {
         // per-particle factor: needs j first
-        j = ancestor_finish(A.cdf, A.N, target, br);
+        j = TABLE ? table_finish(A.rec, A.rs, d, A.N, target, br)
+                  : ancestor_finish(A.cdf, A.N, target, br);
         Lj = A.L + j * d * d;
       }
 #pragma unroll 1
@@ -434,8 +488,10 @@ __device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockCon
           }
         }
       }
-      if (MODE != PROP_LOCAL) j = ancestor_finish(A.cdf, A.N, target, br);
-      const double* Xj = A.X + j * d;
+      if (MODE != PROP_LOCAL)
+        j = TABLE ? table_finish(A.rec, A.rs, d, A.N, target, br)
+                  : ancestor_finish(A.cdf, A.N, target, br);
+      const double* Xj = TABLE ? A.rec + j * A.rs : A.X + j * d;
 #pragma unroll
       for (int k = 0; k < (D > 0 ? D : d); ++k) th[k] = Xj[k] + th[k];
     }
@@ -451,11 +507,19 @@ __device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockCon
 __device__ __forceinline__ double pterm(double v, double p) {
   return (p == 1.0) ? v : (p == 2.0 ? v * v : pow(v, p));
 }
-// running p-norm state s (sum of |.|^p, or max for p = inf); order = k order
+// running p-norm state s (sum of |.|^p, or max for p = inf); order = k order.
+// PK = 2: p == 2 known at compile time (the same operations as the runtime
+// p == 2 branch, so the same bits); PK = 0: any p.  A kernel that can meet a
+// general p carries pow's constants in registers for its whole candidate loop
+// (~30 VGPRs), so the hot kernels are instantiated for p == 2 separately.
+template <int PK = 0>
 __device__ __forceinline__ double pnorm_acc(double s, double v, double p) {
+  if constexpr (PK == 2) return s + v * v;
   return isinf(p) ? fmax(s, v) : s + pterm(v, p);
 }
+template <int PK = 0>
 __device__ __forceinline__ double pnorm_finish(double s, double p) {
+  if constexpr (PK == 2) return sqrt(s);
   return isinf(p) ? s : ((p == 1.0) ? s : (p == 2.0 ? sqrt(s) : pow(s, 1.0 / p)));
 }
 // one simulated statistic (simulate_lg_kernel's formula)
@@ -466,9 +530,9 @@ __device__ __forceinline__ double lg_stat(double a, double sigma, double th_src,
 // Simulate statistics [q0, q1) (q0 even, q1 <= SIM_SMAX) of candidate g and
 // fold them into the p-norm state s in k order; x (nullable) receives the
 // row.  Statistic k uses normal k of the candidate's simulation stream (slot
-// SLOT_SIM + k/4).  theta_{src_k} is read from tsrc[src_k * tstride] (an LDS
-// column of the calling thread: a register array indexed by src_k would go
-// to scratch).
+// SLOT_SIM + k/4).  theta_{src_k} is read from tsrc[src_k * tstride] (a
+// theta row in memory; sim_pnorm_regs below for theta in registers).
+template <int PK = 0>
 __device__ __forceinline__ double sim_pnorm_range(const SimDistArgs& M, const BlockConsts& C,
                                                   const double* tsrc, int tstride,
                                                   uint64_t g, uint32_t gen,
@@ -488,7 +552,38 @@ __device__ __forceinline__ double sim_pnorm_range(const SimDistArgs& M, const Bl
         const double2 as = C.as[k], wx = C.wx[k];
         const double xv = lg_stat(as.x, as.y, tsrc[C.src[k] * tstride], n2[t]);
         if (x) x[k] = xv;
-        s = pnorm_acc(s, fabs(wx.x * (xv - wx.y)), M.p);
+        s = pnorm_acc<PK>(s, fabs(wx.x * (xv - wx.y)), M.p);
+      }
+    }
+  }
+  return s;
+}
+
+// sim_pnorm_range with theta in registers (D > 0): src_k is block-uniform, so
+// th[src_k] is a register-indexed read with an SGPR index (readfirstlane of
+// the LDS value) instead of an LDS slab of every thread's theta, which would
+// cost 8 D bytes of LDS per thread and halve the occupancy.
+template <int D, int PK = 0>
+__device__ __forceinline__ double sim_pnorm_regs(const SimDistArgs& M, const BlockConsts& C,
+                                                 const double (&th)[D], uint64_t g,
+                                                 uint32_t gen, uint64_t seed, int q0, int q1,
+                                                 double s, double* x) {
+  u32x4 r;
+  if (q0 < q1 && (q0 & 3)) r = philox(g, SLOT_SIM + (uint32_t)(q0 >> 2), gen, seed);
+#pragma unroll 1
+  for (int q = q0; q < q1; q += 2) {
+    if ((q & 3) == 0) r = philox(g, SLOT_SIM + (uint32_t)(q >> 2), gen, seed);
+    double n2[2];
+    box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n2[0], n2[1], C.bmt);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int k = q + t;
+      if (k < q1) {
+        const double2 as = C.as[k], wx = C.wx[k];
+        const int sk = __builtin_amdgcn_readfirstlane(C.src[k]);
+        const double xv = lg_stat(as.x, as.y, th[sk], n2[t]);
+        if (x) x[k] = xv;
+        s = pnorm_acc<PK>(s, fabs(wx.x * (xv - wx.y)), M.p);
       }
     }
   }

@@ -60,8 +60,9 @@ __device__ __forceinline__ u32x4 philox(uint64_t index, uint32_t slot,
   for (int r = 0; r < 10; ++r) {
     uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    // three-way xors as single v_bitop3_b32 (0x96 = a ^ b ^ c)
+    uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c1, k0, 0x96);
+    uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c3, k1, 0x96);
     c1 = (uint32_t)p1; c3 = (uint32_t)p0; c0 = n0; c2 = n2;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
@@ -77,6 +78,22 @@ __device__ __forceinline__ double uniform53(uint32_t a, uint32_t b) {
   return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) *
          (1.0 / 9007199254740992.0);
 }
+// Correctly rounded fp32 sqrt of a positive normal v: v_sqrt_f32 (within one
+// ulp) and the one-ulp fix-up by the signs of the fma residuals of its
+// neighbours (the sequence LLVM emits for IEEE sqrtf, without the denormal
+// and special-value scaling v never needs).  Checked against
+// (float)sqrt((double)v) on every fp32 in [2^-26, 128):
+// tools/probes/sqrt_check.hip.
+__device__ __forceinline__ float sqrt_rn(float v) {
+  const float s = __builtin_amdgcn_sqrtf(v);
+  const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+  const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+  const float em = __builtin_fmaf(-sm, s, v);
+  const float ep = __builtin_fmaf(-sp, s, v);
+  const float r = em <= 0.0f ? sm : s;
+  return ep > 0.0f ? sp : r;
+}
+
 // Copy of BM_TAB in LDS (every thread of the block calls it; synchronises).
 }  // namespace abc
 #include "abc_bm_tables.h"
@@ -89,8 +106,8 @@ __device__ __forceinline__ void stage_bm_tab(float* lds) {
 // Box-Muller: n0 = R cos(2 pi u2), n1 = R sin(2 pi u2), R = sqrt(-2 ln u1),
 // u = uniform01 (24 significant bits: u = m 2^-24, m odd).  The transform is
 // evaluated in fp32 -- the precision its 24-bit inputs carry -- with only
-// correctly rounded operations in a fixed order (no contraction; sqrt through
-// fp64, exact after the final rounding; 4 KB of tables), so that
+// correctly rounded operations in a fixed order (no contraction; sqrt_rn;
+// 4 KB of tables), so that
 // oracle/philox.py normal_pairs replays it bit for bit in numpy float32:
 //   ln: m = 2^e f, f = c_i + delta with c_i = 1 + i/128 for the top 7
 //     fraction bits i (delta exact); ln f = ln c_i + log1p(delta / c_i),
@@ -136,7 +153,7 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, double& n0,
     const float k = (float)(24 - e);
     v = (k * LN2_HI - lg[1]) + ((k * LN2_LO - lg[2]) - p);
   }
-  const float R = (float)sqrt((double)(2.0f * v));
+  const float R = sqrt_rn(2.0f * v);
   // ---- (cos, sin)(pi m2 2^-23), m2 = 2 (b >> 9) + 1
   const uint32_t m2 = ((b >> 9) << 1) | 1u;
   const float* sc = tab + BM_TAB_SC + 2 * (int)(m2 >> 16);

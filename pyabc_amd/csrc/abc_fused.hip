@@ -36,37 +36,26 @@ struct RoundArgs {
   const double* box;  // prior support [d x (lo, hi)] (support_box_kernel)
 };
 
-// theta of the calling thread as the simulator's source column: an LDS
-// slab [D][FR_T] for D > 0, the (scratch) array itself for runtime d
-template <int D>
-struct ThetaSlab {
-  static constexpr int ROWS = D > 0 ? D : 1;
-  double* base;
-  __device__ __forceinline__ const double* put(const double* th) const {
-    if (D == 0) return th;
-#pragma unroll
-    for (int k = 0; k < ROWS; ++k) base[k * FR_T + threadIdx.x] = th[k];
-    return base + threadIdx.x;
-  }
-  static constexpr int stride() { return D > 0 ? FR_T : 1; }
-};
-
 // Full evaluation of candidate g: proposal + simulation + distance.  Returns
 // the distance (+inf when the proposal gave up on the prior support), the
 // attempts and the ancestor through the references; x (nullable) gets the row.
-template <int D, int MODE>
+template <int D, int MODE, int PK>
 __device__ __forceinline__ double evaluate_full(const RoundArgs& A, const BlockConsts& C,
-                                                const ThetaSlab<D>& slab, uint64_t g,
+                                                uint64_t g,
                                                 double* th, int64_t& j, int& att, double* x) {
-  att = propose_one<D, MODE>(A.P, C, g, th, j);
-  const double* ts = slab.put(th);
-  const double s = sim_pnorm_range(A.M, C, ts, slab.stride(), g, A.P.gen, A.P.seed, 0,
-                                   A.M.S, 0.0, x);
-  const double dist = pnorm_finish(s, A.M.p);
+  att = propose_one<D, MODE, true>(A.P, C, g, th, j);
+  double s;
+  if constexpr (D > 0) {
+    s = sim_pnorm_regs<D, PK>(A.M, C, *reinterpret_cast<const double(*)[D]>(th), g, A.P.gen,
+                          A.P.seed, 0, A.M.S, 0.0, x);
+  } else {
+    s = sim_pnorm_range<PK>(A.M, C, th, 1, g, A.P.gen, A.P.seed, 0, A.M.S, 0.0, x);
+  }
+  const double dist = pnorm_finish<PK>(s, A.M.p);
   return att <= A.P.max_attempts ? dist : INFINITY;
 }
 
-template <int D, int MODE, bool FILTER>
+template <int D, int MODE, bool FILTER, int PK>
 __device__ __forceinline__ void round_body(
     RoundArgs A, int64_t idx0, int64_t B, double eps,
     uint64_t* __restrict__ bits, int64_t* __restrict__ tile_cnt,
@@ -78,8 +67,6 @@ __device__ __forceinline__ void round_body(
   __shared__ uint32_t tbits[FR_TILE / 32];
   __shared__ uint16_t queue[FR_TILE];
   __shared__ int qn;
-  __shared__ double thl[ThetaSlab<D>::ROWS * FR_T];
-  const ThetaSlab<D> slab{thl};
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int d = D > 0 ? D : A.P.d;
   const int64_t tile0 = (int64_t)blockIdx.x * FR_TILE;
@@ -97,11 +84,15 @@ __device__ __forceinline__ void round_body(
       const int64_t b = tile0 + loc;
       if (b < B) {
         const uint64_t g = (uint64_t)(idx0 + b);
-        att = propose_one<D, MODE>(A.P, C, g, th, j);
-        const double* ts = slab.put(th);
-        const double s = sim_pnorm_range(A.M, C, ts, slab.stride(), g, A.P.gen, A.P.seed, 0,
-                                         4, 0.0, nullptr);
-        if (att <= A.P.max_attempts && !(pnorm_finish(s, A.M.p) > eps)) {
+        att = propose_one<D, MODE, true>(A.P, C, g, th, j);
+        double s;
+        if constexpr (D > 0) {
+          s = sim_pnorm_regs<D, PK>(A.M, C, *reinterpret_cast<const double(*)[D]>(th), g,
+                                A.P.gen, A.P.seed, 0, 4, 0.0, nullptr);
+        } else {
+          s = sim_pnorm_range<PK>(A.M, C, th, 1, g, A.P.gen, A.P.seed, 0, 4, 0.0, nullptr);
+        }
+        if (att <= A.P.max_attempts && !(pnorm_finish<PK>(s, A.M.p) > eps)) {
           const int pos = atomicAdd(&qn, 1);
           queue[pos] = (uint16_t)loc;
         }
@@ -118,7 +109,7 @@ __device__ __forceinline__ void round_body(
     const int64_t b = tile0 + loc;
     if (b < B) {
       double* xr = rec_x ? rec_x + b * A.M.S : nullptr;
-      const double dist = evaluate_full<D, MODE>(A, C, slab, (uint64_t)(idx0 + b), th, j, att,
+      const double dist = evaluate_full<D, MODE, PK>(A, C, (uint64_t)(idx0 + b), th, j, att,
                                                   xr);
       if (dist <= eps) atomicOr(&tbits[loc >> 5], 1u << (loc & 31));
     }
@@ -140,20 +131,21 @@ __device__ __forceinline__ void round_body(
 }
 
 // the plain and the early-reject round as separate kernels (a runtime
-// switch would give both the register allocation of the larger one)
-template <int D, int MODE>
-__global__ __launch_bounds__(FR_T) void fused_round_plain(RoundArgs A, int64_t idx0, int64_t B,
-                                                          double eps, uint64_t* bits,
-                                                          int64_t* tile_cnt, double* rec_x) {
-  round_body<D, MODE, false>(A, idx0, B, eps, bits, tile_cnt, rec_x);
-}
-template <int D, int MODE>
-__global__ __launch_bounds__(FR_T) void fused_round_filter(RoundArgs A, int64_t idx0,
-                                                           int64_t B, double eps,
-                                                           uint64_t* bits, int64_t* tile_cnt,
-                                                           double* rec_x) {
-  round_body<D, MODE, true>(A, idx0, B, eps, bits, tile_cnt, nullptr);
-}
+// switch would give both the register allocation of the larger one), each
+// for p == 2 and for any p (pnorm_acc)
+#define ABC_ROUND_KERNEL(NAME, FILTER, PK)                                            \
+  template <int D, int MODE>                                                          \
+  __global__ __launch_bounds__(FR_T) void NAME(RoundArgs A, int64_t idx0, int64_t B,  \
+                                               double eps, uint64_t* bits,            \
+                                               int64_t* tile_cnt, double* rec_x) {    \
+    round_body<D, MODE, FILTER, PK>(A, idx0, B, eps, bits, tile_cnt,                  \
+                                    FILTER ? nullptr : rec_x);                        \
+  }
+ABC_ROUND_KERNEL(fused_round_plain, false, 0)
+ABC_ROUND_KERNEL(fused_round_plain_p2, false, 2)
+ABC_ROUND_KERNEL(fused_round_filter, true, 0)
+ABC_ROUND_KERNEL(fused_round_filter_p2, true, 2)
+#undef ABC_ROUND_KERNEL
 
 __global__ void support_box_kernel(const int32_t* __restrict__ kind,
                                    const double* __restrict__ params, int d,
@@ -263,17 +255,15 @@ __global__ __launch_bounds__(256) void fused_regen_kernel(
     double* __restrict__ theta, double* __restrict__ lp, int64_t* __restrict__ anc,
     double* __restrict__ x, double* __restrict__ dist) {
   constexpr int DM = D > 0 ? D : 64;
-  __shared__ double thl[ThetaSlab<D>::ROWS * FR_T];
   __shared__ BlockConsts C;
   stage_block_consts<D, MODE>(C, A.P, &A.M, nullptr);
-  const ThetaSlab<D> slab{thl};
   const int d = D > 0 ? D : A.P.d;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   double th[DM];
   int64_t j;
   int att;
-  const double dd = evaluate_full<D, MODE>(A, C, slab, (uint64_t)(idx0 + idx[i]), th, j, att,
+  const double dd = evaluate_full<D, MODE, 0>(A, C, (uint64_t)(idx0 + idx[i]), th, j, att,
                                           x + i * A.M.S);
 #pragma unroll
   for (int k = 0; k < (D > 0 ? D : d); ++k) theta[i * d + k] = th[k];
@@ -282,11 +272,55 @@ __global__ __launch_bounds__(256) void fused_regen_kernel(
   dist[i] = dd;
 }
 
+// ---- ancestor table (abc_candidate.h) ---------------------------------------
+__global__ __launch_bounds__(256) void anc_records_kernel(const double* __restrict__ X,
+                                                          const double* __restrict__ cdf,
+                                                          int64_t N, int d, int rs,
+                                                          double* __restrict__ rec) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= N * rs) return;
+  const int64_t i = e / rs;
+  const int k = (int)(e - i * rs);
+  rec[e] = k < d ? X[i * d + k] : (k == d ? cdf[i] : 0.0);
+}
+
+// guide[k] = first i with anc_bin(cdf_i) >= k (N if none), k = 0 .. G + 1
+__global__ __launch_bounds__(256) void anc_guide_kernel(const double* __restrict__ cdf,
+                                                        int64_t N, int64_t G,
+                                                        int32_t* __restrict__ guide) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k > G + 1) return;
+  const double inv_step = (double)G / cdf[N - 1];  // as stage_block_consts
+  int64_t lo = 0, hi = N;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (anc_bin(cdf[mid], inv_step, G) >= k) hi = mid; else lo = mid + 1;
+  }
+  guide[k] = (int32_t)lo;
+}
+
+struct AncTable { const double* rec; const int32_t* guide; int rs; int64_t G; };
+inline AncTable anc_table_view(const void* t, int64_t N, int d) {
+  AncTable v;
+  v.rs = anc_rs(d);
+  v.G = anc_bins(N);
+  v.rec = reinterpret_cast<const double*>(static_cast<const char*>(t) + ANC_HDR);
+  v.guide = reinterpret_cast<const int32_t*>(v.rec + N * v.rs);
+  return v;
+}
+
 RoundArgs round_args(const abc_candidate_spec* s, const double* box) {
   RoundArgs A;
   A.box = box;
   A.P = ProposalArgs{s->X, s->cdf, s->guide, s->N, s->L, s->prior_kind,
                      s->prior_params, s->d, s->max_attempts, s->seed, s->generation};
+  if (s->X && s->anc_table) {
+    const AncTable v = anc_table_view(s->anc_table, s->N, s->d);
+    A.P.rec = v.rec;
+    A.P.bguide = v.guide;
+    A.P.rs = v.rs;
+    A.P.G = v.G;
+  }
   A.M = SimDistArgs{s->src, s->a, s->sigma, s->x0, s->wf, s->p, s->S};
   return A;
 }
@@ -304,6 +338,7 @@ int check_spec(const abc_candidate_spec* s) {
   ABC_CHECK_ARG(s->X == nullptr || (s->cdf && s->L && s->N >= 1),
                 "candidates: population needs cdf, L, N");
   ABC_CHECK_ARG(s->p >= 1.0, "candidates: p < 1");
+  ABC_CHECK_ARG(s->X == nullptr || s->anc_table, "candidates: population needs anc_table");
   return ABC_OK;
 }
 
@@ -355,6 +390,32 @@ extern "C" size_t abc_candidates_workspace(int64_t B) {
   return off + 256;
 }
 
+extern "C" int64_t abc_ancestor_table_bytes(int64_t N, int d) {
+  if (N < 1 || d < 1) return 0;
+  return ANC_HDR + N * anc_rs(d) * (int64_t)sizeof(double) +
+         (anc_bins(N) + 2) * (int64_t)sizeof(int32_t);
+}
+
+extern "C" int abc_ancestor_table(const double* X, const double* cdf, int64_t N, int d,
+                                  void* table, size_t table_bytes, void* stream) {
+  ABC_CHECK_ARG(N >= 1 && N < (1ll << 31) && d >= 1 && d <= 64,
+                "ancestor_table: bad N/d");
+  ABC_CHECK_ARG(X && cdf && table, "ancestor_table: null pointer");
+  ABC_CHECK_ARG(((uintptr_t)table & 127) == 0, "ancestor_table: table not 128-B aligned");
+  if ((int64_t)table_bytes < abc_ancestor_table_bytes(N, d))
+    return set_error(ABC_ERR_WORKSPACE, "ancestor_table: buffer too small");
+  const AncTable v = anc_table_view(table, N, d);
+  hipStream_t s = as_stream(stream);
+  ABC_HIP(hipMemsetAsync(table, 0, ANC_HDR, s));
+  hipLaunchKernelGGL(anc_records_kernel, dim3((unsigned)ceil_div(N * v.rs, 256)), dim3(256), 0,
+                     s, X, cdf, N, d, v.rs, const_cast<double*>(v.rec));
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(anc_guide_kernel, dim3((unsigned)ceil_div(v.G + 2, 256)), dim3(256), 0, s,
+                     cdf, N, v.G, const_cast<int32_t*>(v.guide));
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
 extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0,
                                     int64_t B, double eps, int filter, int64_t cap,
                                     int64_t* idx, int64_t* count, double* rec_x,
@@ -389,9 +450,16 @@ extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0
   const RoundArgs A = round_args(spec, box);
   ABC_CHECK_ARG(nt < (1ll << 31), "candidates_round: too many tiles");
   profile_start(s, ABC_PROF_CANDIDATES);
-  if (filt)
+  const bool p2 = p == 2.0;
+  if (filt && p2)
+    ABC_FUSED_DISPATCH(fused_round_filter_p2, dim3((unsigned)nt), s, A, idx0, B, eps, bits,
+                       tcnt, rec_x);
+  else if (filt)
     ABC_FUSED_DISPATCH(fused_round_filter, dim3((unsigned)nt), s, A, idx0, B, eps, bits, tcnt,
                        rec_x);
+  else if (p2)
+    ABC_FUSED_DISPATCH(fused_round_plain_p2, dim3((unsigned)nt), s, A, idx0, B, eps, bits,
+                       tcnt, rec_x);
   else
     ABC_FUSED_DISPATCH(fused_round_plain, dim3((unsigned)nt), s, A, idx0, B, eps, bits, tcnt,
                        rec_x);

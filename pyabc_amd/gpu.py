@@ -207,6 +207,19 @@ def cdf_guide(cdf):
     return guide
 
 
+def ancestor_table(X, cdf):
+    """Ancestor table of a population (abc_ancestor_table): padded row
+    records with their scan value + exact-bin guide, for the fused rounds."""
+    N, d = X.shape
+    nb = nat.query("abc_ancestor_table_bytes", int(N), int(d))
+    t = torch.empty(int(nb), dtype=torch.uint8, device=X.device)
+    if t.data_ptr() % 128:
+        raise RuntimeError("ancestor_table: allocation not 128-byte aligned")
+    nat.call("abc_ancestor_table", p(X), p(cdf), int(N), int(d), p(t), t.numel(),
+             stream_ptr())
+    return t
+
+
 def propose(X, cdf, L, prior_kind, prior_params, seed, generation, idx0, B,
             max_attempts, d, per_particle_L=False, guide=None):
     dev = prior_params.device
@@ -276,9 +289,9 @@ class CandidateRound:
 
     def __init__(self, d, S, prior_kind, prior_params, src, a, sigma, x0, wf,
                  p, seed, generation, max_attempts, X=None, cdf=None,
-                 guide=None, L=None, per_particle_L=False):
+                 guide=None, L=None, per_particle_L=False, anc_table=None):
         self._keep = [t for t in (prior_kind, prior_params, src, a, sigma, x0,
-                                  wf, X, cdf, guide, L) if t is not None]
+                                  wf, X, cdf, guide, L, anc_table) if t is not None]
         for t in self._keep:
             assert t.is_contiguous() and t.is_cuda
         if src.dtype != torch.int32 or prior_kind.dtype != torch.int32:
@@ -296,6 +309,10 @@ class CandidateRound:
         s.x0, s.wf, s.p = _ptr(x0), _ptr(wf), float(p)
         s.seed = int(seed) & (2 ** 64 - 1)
         s.generation = int(generation) & 0xFFFFFFFF
+        if X is not None and anc_table is None:
+            anc_table = ancestor_table(X, cdf)
+            self._keep.append(anc_table)
+        s.anc_table = _ptr(anc_table) if X is not None else None
         self.device = prior_params.device
 
     def run(self, idx0, B, eps, cap, filter=True, rec_x=None, idx_out=None,

@@ -121,7 +121,7 @@ class BatchedGPUSampler(Sampler):
 
     def __init__(self, batch_size=None, max_batch_size=1 << 22, seed=None,
                  max_attempts=10000, check_max_eval=False, fused=True,
-                 max_fused_batch_size=1 << 31, filter_below=0.15,
+                 max_fused_batch_size=1 << 31, filter_below=0.0,
                  record_budget_bytes=1 << 31):
         super().__init__()
         self.check_max_eval = check_max_eval
@@ -135,7 +135,11 @@ class BatchedGPUSampler(Sampler):
         # the acceptor uniform and the transition an MVN / LocalTransition
         self.fused = fused
         self.max_fused_batch_size = max_fused_batch_size
-        self.filter_below = filter_below          # early-reject mode below this rate
+        # early-reject mode below this acceptance rate; off by default: with
+        # the proposal dominating the candidate's cost the plain round is
+        # faster at every rate (tools/bench_fused.py: 2.69e10 vs 2.52e10
+        # candidates/s at 1e-4)
+        self.filter_below = filter_below
         self.record_budget_bytes = record_budget_bytes  # rec rows per fused round
         # first m recorded candidates are all that is used
         # (ABCSMC.max_nr_recorded_particles, smc.py:998-1001)

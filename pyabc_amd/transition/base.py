@@ -76,6 +76,16 @@ class Transition(BaseEstimator, metaclass=TransitionMeta):
         self.cv_estimate_ = res
         return res.n_estimated
 
+    def _ancestor_table(self):
+        """abc_ancestor_table of the fitted population (built once per fit,
+        on first use by the fused candidate rounds)."""
+        from .. import gpu
+        t = getattr(self, "_dev_anc", None)
+        if t is None or t[0] is not self._dev_cdf:
+            t = (self._dev_cdf, gpu.ancestor_table(self._dev_X, self._dev_cdf))
+            self._dev_anc = t
+        return t[1]
+
     # device tensors are immutable after fit(): share them on deepcopy
     # (ABCSMC deep-copies transitions every generation, smc.py:979).
     _SHARED = ()

@@ -138,7 +138,8 @@ class LocalTransition(Transition):
         """Device arrays for the fused candidate kernel: per-particle
         Cholesky factors (local_transition.py:141-145)."""
         return dict(X=self._dev_X, cdf=self._dev_cdf, guide=self._dev_guide,
-                    L=self._dev_chol, per_particle_L=True)
+                    L=self._dev_chol, per_particle_L=True,
+                    anc_table=self._ancestor_table())
 
     def rvs_single(self):
         theta = self.propose_device(1)[0].cpu().numpy()[0]

@@ -226,7 +226,8 @@ class MultivariateNormalTransition(Transition):
         """Device arrays of the proposal for the fused candidate kernel
         (abc_candidate_spec): population, weight scan, guide, shared L."""
         return dict(X=self._dev_X, cdf=self._dev_cdf, guide=self._dev_guide,
-                    L=self._dev_L, per_particle_L=False)
+                    L=self._dev_L, per_particle_L=False,
+                    anc_table=self._ancestor_table())
 
     def rvs(self, size: int = None) -> Union[pd.Series, pd.DataFrame]:
         n = 1 if size is None else size

@@ -138,6 +138,40 @@ def test_fused_equals_staged(dev, mode, d, S, rate):
     assert n > 0
 
 
+@pytest.mark.parametrize("wkind", ["zeros", "heavy", "tiny", "n1", "n2", "n65"])
+def test_ancestor_table_edge_weights(dev, wkind):
+    """The fused rounds draw ancestors through abc_ancestor_table (padded
+    records + exact-bin guide); the staged kernels through the cdf guide.
+    Both must give np.searchsorted's ancestor: runs of zero weights (flat
+    scan, leading and trailing), one row with most of the weight (a row
+    spanning many bins), weights over 300 decades, N = 1, 2, 65."""
+    from pyabc_amd import gpu
+    N = {"n1": 1, "n2": 2, "n65": 65}.get(wkind, 4000)
+    c = _case(3, 3, N=N, seed=4)
+    rng = np.random.default_rng(8)
+    w = rng.uniform(size=N)
+    if wkind == "zeros":
+        w[rng.uniform(size=N) < 0.7] = 0.0
+        w[:5] = 0.0
+        w[-5:] = 0.0
+    elif wkind == "heavy":
+        w[N // 3] = 1e6
+    elif wkind == "tiny":
+        w = 10.0 ** rng.uniform(-300, 0, N)
+    cdf = gpu.inclusive_scan(T(w))
+    c.update(cdf=cdf, guide=gpu.cdf_guide(cdf))
+    lo, B = 99, 40_000
+    ref = _staged(c, lo, B, 1e300)
+    assert ref["n"] == B
+    n = _check_equal(c, _round(c), ref, lo, B, 1e300, False)
+    assert n == B
+    anc = ref["anc"].cpu().numpy()
+    if wkind == "zeros":    # zero-weight rows are never drawn
+        assert (w[anc] > 0).all()
+    if wkind == "heavy":
+        assert (anc == N // 3).mean() > 0.9
+
+
 @pytest.mark.parametrize("p", [1.0, np.inf, 3.0])
 def test_fused_pnorm_orders(dev, p):
     c = _case(6, 11, p=p, seed=5)

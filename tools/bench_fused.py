@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--S", type=int, default=None, help="statistics (default d)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--staged", action="store_true")
+    ap.add_argument("--modes", nargs="+", default=["plain", "filter"],
+                    choices=["plain", "filter"])
     a = ap.parse_args()
     import torch
     from pyabc_amd import gpu
@@ -54,7 +56,7 @@ def main():
     dist = gpu.pnorm(x, one, one, 2.0).cpu().numpy()
     for rate in a.rates:
         eps = float(np.quantile(dist, rate))
-        for filt in (False, True):
+        for filt in [m == "filter" for m in a.modes]:
             ts = []
             for r in range(a.reps + 1):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -67,7 +69,7 @@ def main():
             c = int(cnt.cpu())
             ms = float(np.median(ts))
             print(f"rate {rate:g} eps {eps:.4f} filter={filt}: B={a.B} {ms:.2f} ms "
-                  f"-> {a.B / ms / 1e6:.3e} candidates/s (accepted {c}, "
+                  f"-> {a.B / ms * 1e3:.3e} candidates/s (accepted {c}, "
                   f"{c / a.B:.2e})", flush=True)
         if a.staged:
             B = 1 << 22
@@ -83,7 +85,7 @@ def main():
                 e1.synchronize()
             ms = e0.elapsed_time(e1)
             print(f"  staged 4-kernel pipeline: B={B} {ms:.2f} ms -> "
-                  f"{B / ms / 1e6:.3e} candidates/s", flush=True)
+                  f"{B / ms * 1e3:.3e} candidates/s", flush=True)
 
 
 if __name__ == "__main__":
