@@ -147,7 +147,8 @@ int abc_mvn_logpdf_direct(const double* x, int64_t M, const double* X,
  * Candidate g (global index idx0 .. idx0+B-1) draws, from Philox4x32-10 keyed
  * by (seed, generation, g, slot), an ancestor j ~ Cat(w) by inverse CDF over
  * `cdf` (inclusive prefix of w) and theta = X_j + L n, n ~ N(0, I_d)
- * (L: any square root of Sigma, [d x d] row-major).  It re-draws while the
+ * (L: the lower-triangular square root of Sigma, L L^T = Sigma, [d x d]
+ * row-major; entries above the diagonal are not read).  It re-draws while the
  * prior density is 0 (smc.py:654-656; at most max_attempts), and writes
  * theta [B x d], prior log-density [B], ancestor [B] and attempts used [B]
  * (attempts > max_attempts means "gave up").  With X == NULL it samples the
@@ -220,7 +221,9 @@ typedef struct abc_candidate_spec {
   const double* cdf;           /* inclusive scan of the weights [N]        */
   const int32_t* guide;        /* abc_cdf_guide table [N] (nullable)        */
   int64_t N;
-  const double* L;             /* [d x d], or [N x d x d] per particle     */
+  const double* L;             /* [d x d], or [N x d x d] per particle:
+                                  lower-triangular factors (L L^T = cov;
+                                  entries above the diagonal are not read) */
   int per_particle_L;
   const int32_t* prior_kind;   /* [d] ABC_PRIOR_*                          */
   const double* prior_params;  /* [4 d]                                    */

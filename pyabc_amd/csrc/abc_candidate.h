@@ -472,22 +472,28 @@ __device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockCon
                   : ancestor_finish(A.cdf, A.N, target, br);
         Lj = A.L + j * d * d;
       }
-#pragma unroll 1
-      for (int q = 0; q < d; q += 2) {
+      // L is lower triangular (a Cholesky factor; the ABI contract), so
+      // column q only reaches rows k >= q: with D known the pair loop is
+      // unrolled and the upper triangle's multiply-adds vanish
+      auto pair = [&](int q) {
         if ((q & 3) == 0) r = philox(g, s0 + SLOT_PERTURB + (uint32_t)(q >> 2), A.gen, A.seed);
         double n0, n1;
         box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1, C.bmt);
         const bool two = q + 1 < d;
 #pragma unroll
         for (int k = 0; k < (D > 0 ? D : d); ++k) {
-          const double l0 = LT_LDS ? LT[q * d + k] : Lj[k * d + q];
-          th[k] = fma(l0, n0, th[k]);
-          if (two) {
+          if (k >= q) {
+            const double l0 = LT_LDS ? LT[q * d + k] : Lj[k * d + q];
+            th[k] = fma(l0, n0, th[k]);
+          }
+          if (two && k >= q + 1) {
             const double l1 = LT_LDS ? LT[(q + 1) * d + k] : Lj[k * d + q + 1];
             th[k] = fma(l1, n1, th[k]);
           }
         }
-      }
+      };
+#pragma unroll 1
+      for (int q = 0; q < d; q += 2) pair(q);
       if (MODE != PROP_LOCAL)
         j = TABLE ? table_finish(A.rec, A.rs, d, A.N, target, br)
                   : ancestor_finish(A.cdf, A.N, target, br);

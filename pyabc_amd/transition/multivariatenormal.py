@@ -48,7 +48,11 @@ def psd_whitening(cov):
                          "semidefinite.")
     keep = s > eps
     U = u[:, keep] / np.sqrt(s[keep])
-    L = u * np.sqrt(np.clip(s, 0, None))[None, :]
+    # sampling factor L L^T = cov, lower triangular (the proposal kernels
+    # skip the upper triangle): LQ of the eigen factor B = u sqrt(s), i.e.
+    # L = R^T of B^T = Q R, which exists for singular cov as well
+    B = u * np.sqrt(np.clip(s, 0, None))[None, :]
+    L = np.tril(np.linalg.qr(B.T, mode="r").T)
     return dict(U=U, V=u[:, ~keep], rank=int(keep.sum()),
                 log_pdet=float(np.sum(np.log(s[keep]))), tol=1e3 * eps, L=L)
 
