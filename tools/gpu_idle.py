@@ -4,8 +4,10 @@ dispatch, overall and inside a window (e.g. the bench's timed region, from
 the first candidate-round kernel of generation `--skip` on).
 
     python tools/gpu_idle.py gpurun_out/prof/run_results.db [--after-kernel fused_round --skip N]
+    python tools/gpu_idle.py gpurun_out/prof/run_kernel_trace.csv [...]   (csv output)
 """
 import argparse
+import csv
 import sqlite3
 
 
@@ -37,12 +39,18 @@ def main():
                     help="start the window at the --skip-th dispatch of this kernel")
     ap.add_argument("--skip", type=int, default=0)
     a = ap.parse_args()
-    con = sqlite3.connect(a.db)
-    kd, ks = table(con, "rocpd_kernel_dispatch"), table(con, "rocpd_info_kernel_symbol")
-    cols = [r[1] for r in con.execute(f"pragma table_info({ks})")]
-    nc = "display_name" if "display_name" in cols else "kernel_name"
-    rows = con.execute(f"select s.{nc}, d.start, d.end from {kd} d join {ks} s "
-                       f"on d.kernel_id = s.id order by d.start").fetchall()
+    if a.db.endswith(".csv"):
+        with open(a.db) as f:
+            rows = sorted((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                          for r in csv.DictReader(f))
+        rows.sort(key=lambda r: r[1])
+    else:
+        con = sqlite3.connect(a.db)
+        kd, ks = table(con, "rocpd_kernel_dispatch"), table(con, "rocpd_info_kernel_symbol")
+        cols = [r[1] for r in con.execute(f"pragma table_info({ks})")]
+        nc = "display_name" if "display_name" in cols else "kernel_name"
+        rows = con.execute(f"select s.{nc}, d.start, d.end from {kd} d join {ks} s "
+                           f"on d.kernel_id = s.id order by d.start").fetchall()
     t0 = rows[0][1]
     if a.after_kernel:
         hits = [r for r in rows if a.after_kernel in r[0]]
