@@ -331,6 +331,7 @@ struct ProposalArgs {
   const int32_t* bguide = nullptr; // exact-bin guide [G + 2]
   int rs = 0;
   int64_t G = 0;
+  const double* xmax = nullptr;    // max |X_jk| over the table (its header)
 };
 
 // ---- ancestor table -----------------------------------------------------------
@@ -389,6 +390,7 @@ struct BlockConsts {
   int32_t src[SIM_SMAX];
   double total;                   // cdf[N - 1]
   double inv_step;                // G / total (ancestor table)
+  int lazy;                       // early reject from theta_0..LAZY_KT-1 (lazy_filter_ok)
 };
 
 // Fill C (every thread of the block calls it; synchronises).  BOX_FROM_SRC:
@@ -508,6 +510,81 @@ __device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockCon
     if (ok) return att + 1;  // prior density > 0 (smc.py:654-656)
   }
   return A.max_attempts + 1;
+}
+
+// ---- the lazy early-reject head ---------------------------------------------
+// With a lower-triangular L, theta_k depends on normals 0..k only, so the
+// first LAZY_KT coordinates of attempt 0 need one perturbation Philox call
+// and two Box-Muller pairs instead of all d.  propose_head evaluates exactly
+// those coordinates with propose_one's operations in propose_one's order
+// (same streams, same fma chain, same X_j + (L n)_k), so they are the bits
+// propose_one produces whenever attempt 0 is the accepted proposal.
+constexpr int LAZY_KT = 4;
+
+// Attempt 0 is the accepted proposal for EVERY candidate whose first LAZY_KT
+// coordinates lie in the support, when the support box of every coordinate
+// k >= LAZY_KT contains the whole range theta_k can take:
+//   |theta_k| <= max_jk |X_jk| + 6 sum_q |L_kq|
+// (every Box-Muller normal has |n| <= sqrt(2 * 24 ln 2) < 5.77; a relative
+// margin covers the roundings).  Also the early-reject statistics 0..3 must
+// read theta_src with src < LAZY_KT.  Decided per block from its LDS
+// constants (thread 0; the caller synchronises before C.lazy is read).
+template <int D, int MODE>
+__device__ __forceinline__ bool lazy_filter_ok(const BlockConsts& C, const ProposalArgs& A,
+                                               const SimDistArgs& M) {
+  if constexpr (MODE != PROP_MVN || D <= LAZY_KT || D > LT_DMAX) {
+    return false;
+  } else {
+    if (A.xmax == nullptr || M.S <= 4) return false;
+    bool ok = true;
+    for (int k = 0; k < 4; ++k) ok = ok && C.src[k] >= 0 && C.src[k] < LAZY_KT;
+    const double xm = *A.xmax;
+    for (int k = LAZY_KT; k < D; ++k) {
+      double ls = 0.0;
+      for (int q = 0; q <= k; ++q) ls += fabs(C.LT[q * D + k]);
+      const double b = (xm + 6.0 * ls) * 1.000001 + 1e-300;
+      ok = ok && (C.box[2 * k] <= -b) && (b <= C.box[2 * k + 1]);  // NaN: false
+    }
+    return ok;
+  }
+}
+
+// theta_0..LAZY_KT-1 of attempt 0 (MVN, ancestor table); returns whether they
+// are inside the support box.  Mirrors propose_one line for line.
+template <int D>
+__device__ __forceinline__ bool propose_head(const ProposalArgs& A, const BlockConsts& C,
+                                             uint64_t g, double* th) {
+  constexpr int KT = LAZY_KT;
+  static_assert(D > KT, "propose_head: D > LAZY_KT");
+  int oz = 0;
+  asm volatile("" : "+s"(oz));
+  const double* LT = C.LT + oz;
+  const double* box = C.box + oz;
+  u32x4 r = philox(g, SLOT_ANCESTOR, A.gen, A.seed);
+  const double target = uniform53(r.x, r.y) * C.total;
+  const int64_t kt = anc_bin(target, C.inv_step, A.G);
+  const AncestorBracket br = {A.bguide[kt], A.bguide[kt + 1]};
+#pragma unroll
+  for (int k = 0; k < KT; ++k) th[k] = 0.0;
+  r = philox(g, SLOT_PERTURB, A.gen, A.seed);
+#pragma unroll
+  for (int q = 0; q < KT; q += 2) {
+    double n0, n1;
+    box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1, C.bmt);
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      if (k >= q) th[k] = fma(LT[q * D + k], n0, th[k]);
+      if (k >= q + 1) th[k] = fma(LT[(q + 1) * D + k], n1, th[k]);
+    }
+  }
+  const int64_t j = table_finish(A.rec, A.rs, D, A.N, target, br);
+  const double* Xj = A.rec + j * A.rs;
+#pragma unroll
+  for (int k = 0; k < KT; ++k) th[k] = Xj[k] + th[k];
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < KT; ++k) ok = ok & (box[2 * k] <= th[k]) & (th[k] <= box[2 * k + 1]);
+  return ok;
 }
 
 __device__ __forceinline__ double pterm(double v, double p) {

@@ -71,15 +71,44 @@ __device__ __forceinline__ void round_body(
   const int d = D > 0 ? D : A.P.d;
   const int64_t tile0 = (int64_t)blockIdx.x * FR_TILE;
   if (tid < FR_TILE / 32) tbits[tid] = 0u;
-  if (tid == 0) qn = 0;
+  if (tid == 0) {
+    qn = 0;
+    if (FILTER) C.lazy = lazy_filter_ok<D, MODE>(C, A.P, A.M) ? 1 : 0;
+  }
   __syncthreads();
   double th[DM];
   int64_t j;
   int att;
   if (FILTER) {
     // phase A: proposal + first group of 4 statistics; an exact early reject
+    bool lazy_done = false;
+    if constexpr (MODE == PROP_MVN && D > LAZY_KT && D <= LT_DMAX) {
+      if (C.lazy) {
+        // lazy head: theta_0..3 of attempt 0 and statistics 0..3 only; a
+        // head outside the support (attempt 0 may be re-drawn) survives
 #pragma unroll 1
-    for (int it = 0; it < FR_CPT; ++it) {
+        for (int it = 0; it < FR_CPT; ++it) {
+          const int loc = it * FR_T + tid;
+          const int64_t b = tile0 + loc;
+          if (b < B) {
+            const uint64_t g = (uint64_t)(idx0 + b);
+            bool keep = true;
+            if (propose_head<D>(A.P, C, g, th)) {
+              const double s = sim_pnorm_regs<D, PK>(A.M, C, *reinterpret_cast<const double(*)[D]>(th),
+                                                     g, A.P.gen, A.P.seed, 0, 4, 0.0, nullptr);
+              keep = !(pnorm_finish<PK>(s, A.M.p) > eps);
+            }
+            if (keep) {
+              const int pos = atomicAdd(&qn, 1);
+              queue[pos] = (uint16_t)loc;
+            }
+          }
+        }
+        lazy_done = true;
+      }
+    }
+#pragma unroll 1
+    for (int it = 0; it < (lazy_done ? 0 : FR_CPT); ++it) {
       const int loc = it * FR_T + tid;
       const int64_t b = tile0 + loc;
       if (b < B) {
@@ -276,12 +305,20 @@ __global__ __launch_bounds__(256) void fused_regen_kernel(
 __global__ __launch_bounds__(256) void anc_records_kernel(const double* __restrict__ X,
                                                           const double* __restrict__ cdf,
                                                           int64_t N, int d, int rs,
-                                                          double* __restrict__ rec) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= N * rs) return;
+                                                          double* __restrict__ rec,
+                                                          unsigned long long* __restrict__ xmax_bits) {
+  const int64_t e0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t e = e0 < N * rs ? e0 : N * rs - 1;  // whole waves reach the max
   const int64_t i = e / rs;
   const int k = (int)(e - i * rs);
-  rec[e] = k < d ? X[i * d + k] : (k == d ? cdf[i] : 0.0);
+  const double v = k < d ? X[i * d + k] : (k == d ? cdf[i] : 0.0);
+  if (e0 == e) rec[e] = v;
+  // max |X_jk| into the header (lazy_filter_ok): the bits of a non-negative
+  // double order like the value (a NaN sorts above +inf and disables it)
+  double a = k < d ? fabs(v) : 0.0;
+  a = wave_max(a);
+  if ((threadIdx.x & 63) == 0)
+    atomicMax(xmax_bits, (unsigned long long)__double_as_longlong(a));
 }
 
 // guide[k] = first i with anc_bin(cdf_i) >= k (N if none), k = 0 .. G + 1
@@ -299,9 +336,10 @@ __global__ __launch_bounds__(256) void anc_guide_kernel(const double* __restrict
   guide[k] = (int32_t)lo;
 }
 
-struct AncTable { const double* rec; const int32_t* guide; int rs; int64_t G; };
+struct AncTable { const double* rec; const int32_t* guide; int rs; int64_t G; const double* xmax; };
 inline AncTable anc_table_view(const void* t, int64_t N, int d) {
   AncTable v;
+  v.xmax = static_cast<const double*>(t);  // header word 0
   v.rs = anc_rs(d);
   v.G = anc_bins(N);
   v.rec = reinterpret_cast<const double*>(static_cast<const char*>(t) + ANC_HDR);
@@ -320,6 +358,7 @@ RoundArgs round_args(const abc_candidate_spec* s, const double* box) {
     A.P.bguide = v.guide;
     A.P.rs = v.rs;
     A.P.G = v.G;
+    A.P.xmax = v.xmax;
   }
   A.M = SimDistArgs{s->src, s->a, s->sigma, s->x0, s->wf, s->p, s->S};
   return A;
@@ -408,7 +447,8 @@ extern "C" int abc_ancestor_table(const double* X, const double* cdf, int64_t N,
   hipStream_t s = as_stream(stream);
   ABC_HIP(hipMemsetAsync(table, 0, ANC_HDR, s));
   hipLaunchKernelGGL(anc_records_kernel, dim3((unsigned)ceil_div(N * v.rs, 256)), dim3(256), 0,
-                     s, X, cdf, N, d, v.rs, const_cast<double*>(v.rec));
+                     s, X, cdf, N, d, v.rs, const_cast<double*>(v.rec),
+                     static_cast<unsigned long long*>(table));
   ABC_LAUNCHED();
   hipLaunchKernelGGL(anc_guide_kernel, dim3((unsigned)ceil_div(v.G + 2, 256)), dim3(256), 0, s,
                      cdf, N, v.G, const_cast<int32_t*>(v.guide));

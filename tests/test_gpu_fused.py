@@ -199,6 +199,7 @@ def test_fused_prior_kinds_and_gave_up(dev):
         ref = _staged(c, lo, B, 1e300, max_attempts=max_att)
         fr = _round(c, max_attempts=max_att)
         n = _check_equal(c, fr, ref, lo, B, 1e300, False)
+        assert _check_equal(c, fr, ref, lo, B, 1e300, True) == n
         if max_att == 2:
             assert 0 < n < B     # some gave up and were rejected
         assert torch.isfinite(fr.regen(lo, ref["idx"][:1000])[1]).all()
@@ -206,6 +207,40 @@ def test_fused_prior_kinds_and_gave_up(dev):
     c0 = _case(6, 6, mode="prior", kinds=kinds, params=params, seed=9)
     ref = _staged(c0, lo, B, 1e300)
     _check_equal(c0, _round(c0), ref, lo, B, 1e300, False)
+
+
+@pytest.mark.parametrize("variant", ["wide_uniform", "narrow_uniform", "src_late",
+                                     "huge_x", "d5_S6"])
+def test_fused_lazy_filter(dev, variant):
+    """The lazy early reject (filter mode, MVN, d > 4): theta_0..3 of attempt
+    0 and statistics 0..3 decide the rejection when every coordinate k >= 4
+    of any proposal lies in the support (lazy_filter_ok); otherwise the full
+    proposal runs first.  Both must give the staged pipeline's accept set
+    and rows bit for bit: bounded priors wide enough for the lazy head
+    (uniform(-50, 100)), narrow ones (the head is refused, attempt 0 may be
+    re-drawn), early-reject statistics reading theta_7 (refused), a
+    population far out (|X| ~ 1e6: refused by the bound), and d = 5."""
+    d, S = (5, 6) if variant == "d5_S6" else (8, 9)
+    kinds, params, src = None, None, None
+    if variant == "wide_uniform":
+        kinds, params = ["uniform"] * d, [[-50.0, 150.0, 0, 0]] * d
+    elif variant == "narrow_uniform":
+        kinds, params = ["uniform"] * d, [[-1.0, 3.0, 0, 0]] * d
+    elif variant == "src_late":
+        src = [7, 1, 2, 3, 4, 5, 6, 0, 1]
+    c = _case(d, S, kinds=kinds, params=params, src=src, seed=21)
+    if variant == "huge_x":
+        c["host"]["X"] = c["host"]["X"] + 1e6
+        c["X"] = T(c["host"]["X"])
+        c["x0"] = T(np.full(S, 1e6 + 1.0))
+    lo, B = 31, 120_000
+    fr = _round(c)
+    for rate in (0.2, 0.003):
+        eps = _eps_for(_staged(c, lo, B, np.inf)["dist"], rate)
+        ref = _staged(c, lo, B, eps)
+        assert ref["n"] > 0
+        for filt in (True, False):
+            _check_equal(c, fr, ref, lo, B, eps, filt)
 
 
 def test_fused_edges(dev):
