@@ -55,6 +55,8 @@ def parse():
                     help="worker processes of the CPU baseline (the box's CPU "
                          "share per GPU is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--filter-below", type=float, default=None,
+                    help="BatchedGPUSampler.filter_below (default: the sampler's)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: functional multi-rank runs on one GPU (tests)")
     return ap.parse_args()
@@ -131,7 +133,9 @@ def build_abc(args, rank, ws):
     abc = pa.ABCSMC(model, prior, pa.PNormDistance(p=2),
                     population_size=args.pop,
                     transitions=tr, eps=pa.QuantileEpsilon(alpha=0.5),
-                    sampler=pa.BatchedGPUSampler(seed=20251016))
+                    sampler=pa.BatchedGPUSampler(seed=20251016, **(
+                        {} if args.filter_below is None
+                        else {"filter_below": args.filter_below})))
     abc.new("sqlite://", {k: 1.0 for k in keys})
     return abc, tr
 

@@ -243,8 +243,10 @@ typedef struct abc_candidate_spec {
  * their weight-scan value in 128-byte-aligned records, and a guide over
  * 4 N scan bins (abc_candidate.h).  Same ancestors as the cdf / guide
  * search (np.searchsorted(cdf, u * total, side="right"), smc.py:652 via
- * multivariatenormal.py:90-94), fewer cache lines per draw.  table: device
- * buffer of abc_ancestor_table_bytes(N, d) bytes, 128-byte aligned. */
+ * multivariatenormal.py:90-94), fewer cache lines per draw.  The header's
+ * first double is max |X_jk| (the lazy early reject's support bound).
+ * table: device buffer of abc_ancestor_table_bytes(N, d) bytes, 128-byte
+ * aligned. */
 int64_t abc_ancestor_table_bytes(int64_t N, int d);
 int abc_ancestor_table(const double* X, const double* cdf, int64_t N, int d,
                        void* table, size_t table_bytes, void* stream);
@@ -253,7 +255,9 @@ int abc_ancestor_table(const double* X, const double* cdf, int64_t N, int d,
  * the round (uncapped) to *count (device int64).  rec_x (nullable) receives
  * the sum stats of every candidate [B x S] (record_rejected).  filter != 0
  * allows the exact early-rejection mode (first 4 statistics, p in {1,2,inf},
- * no rec_x): the same accept set at lower cost when few candidates pass. */
+ * no rec_x; for the shared-L transition with every coordinate beyond the
+ * 4th provably inside the support, only theta_0..3 of the first attempt):
+ * the same accept set at lower cost when few candidates pass. */
 size_t abc_candidates_workspace(int64_t B);
 int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0,
                          int64_t B, double eps, int filter, int64_t cap,

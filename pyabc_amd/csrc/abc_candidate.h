@@ -336,18 +336,22 @@ struct ProposalArgs {
 
 // ---- ancestor table -----------------------------------------------------------
 // The ancestor draw reads, per candidate, a guide entry, the weight scan near
-// the answer and the answer's row: three random cache lines or more from the
-// Infinity Cache at c3 sizes (cdf 8 MB, X 80 MB), which bound the fused round
-// (tools/bench_fused.py --N: 3.1e10 candidates/s at N = 1e3, 1.9e10 at 1e6).
-// The table keeps each row in a 128-byte-aligned record with its scan value
-// (rs = 16 doubles for d <= 15), and a guide over G = 4 N bins of the scan,
-// bin(x) = min(floor(x * G / total), G), guide[k] = first i with
-// bin(cdf_i) >= k.  bin is monotone and both sides evaluate it identically,
-// so for target t with kt = bin(t), i* = first i with cdf_i > t lies in
-// [guide[kt], guide[kt + 1]] (i < guide[kt]: bin(cdf_i) < kt, so cdf_i < t;
-// bin(cdf_{guide[kt+1]}) > kt, so cdf > t): np.searchsorted's answer, with
-// no probe when the two entries agree (most bins at G = 4 N) and otherwise
-// probes that read the records holding the candidate rows themselves.
+// the answer and the answer's row.  At c3 sizes (1e6 rows) those are random
+// accesses into the Infinity Cache, and the chip serves ~5.5e10 of them per
+// second whatever their size (8 B .. 128 B; a 2-MB table that stays in L2
+// serves 2.5e11: tools/probes/gather_cost.hip, profiles/r02_gather_probe.txt).
+// The table keeps
+//   * each row in a 128-byte-aligned record with its scan value (rs = 16
+//     doubles for d <= 15): the answer's row and the scan values the search
+//     probes are one access;
+//   * a guide over G = 4 N bins of the scan, bin(x) = min(floor(x G /
+//     total), G), guide[k] = first i with bin(cdf_i) >= k.  bin is monotone
+//     and both sides evaluate it identically, so for target t with kt =
+//     bin(t), i* = first i with cdf_i > t lies in [guide[kt], guide[kt + 1]]
+//     (i < guide[kt]: bin(cdf_i) < kt, so cdf_i < t; bin(cdf_{guide[kt+1]}) >
+//     kt, so cdf > t): np.searchsorted's answer, with no probe when the two
+//     entries agree (most bins at G = 4 N) and otherwise probes that read the
+//     records holding the candidate rows themselves.  Two accesses per draw.
 constexpr int ANC_HDR = 256;  // table header bytes
 __host__ __device__ inline int anc_rs(int d) { return (d + 1 + 15) / 16 * 16; }
 __host__ __device__ inline int64_t anc_bins(int64_t N) {
@@ -515,10 +519,11 @@ __device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockCon
 // ---- the lazy early-reject head ---------------------------------------------
 // With a lower-triangular L, theta_k depends on normals 0..k only, so the
 // first LAZY_KT coordinates of attempt 0 need one perturbation Philox call
-// and two Box-Muller pairs instead of all d.  propose_head evaluates exactly
-// those coordinates with propose_one's operations in propose_one's order
-// (same streams, same fma chain, same X_j + (L n)_k), so they are the bits
-// propose_one produces whenever attempt 0 is the accepted proposal.
+// and two Box-Muller pairs instead of all d.  lazy_head_group (below)
+// evaluates exactly those coordinates with propose_one's operations in
+// propose_one's order (same streams, same fma chain, same X_j + (L n)_k), so
+// they are the bits propose_one produces whenever attempt 0 is the accepted
+// proposal.
 constexpr int LAZY_KT = 4;
 
 // Attempt 0 is the accepted proposal for EVERY candidate whose first LAZY_KT
@@ -547,44 +552,6 @@ __device__ __forceinline__ bool lazy_filter_ok(const BlockConsts& C, const Propo
     }
     return ok;
   }
-}
-
-// theta_0..LAZY_KT-1 of attempt 0 (MVN, ancestor table); returns whether they
-// are inside the support box.  Mirrors propose_one line for line.
-template <int D>
-__device__ __forceinline__ bool propose_head(const ProposalArgs& A, const BlockConsts& C,
-                                             uint64_t g, double* th) {
-  constexpr int KT = LAZY_KT;
-  static_assert(D > KT, "propose_head: D > LAZY_KT");
-  int oz = 0;
-  asm volatile("" : "+s"(oz));
-  const double* LT = C.LT + oz;
-  const double* box = C.box + oz;
-  u32x4 r = philox(g, SLOT_ANCESTOR, A.gen, A.seed);
-  const double target = uniform53(r.x, r.y) * C.total;
-  const int64_t kt = anc_bin(target, C.inv_step, A.G);
-  const AncestorBracket br = {A.bguide[kt], A.bguide[kt + 1]};
-#pragma unroll
-  for (int k = 0; k < KT; ++k) th[k] = 0.0;
-  r = philox(g, SLOT_PERTURB, A.gen, A.seed);
-#pragma unroll
-  for (int q = 0; q < KT; q += 2) {
-    double n0, n1;
-    box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1, C.bmt);
-#pragma unroll
-    for (int k = 0; k < KT; ++k) {
-      if (k >= q) th[k] = fma(LT[q * D + k], n0, th[k]);
-      if (k >= q + 1) th[k] = fma(LT[(q + 1) * D + k], n1, th[k]);
-    }
-  }
-  const int64_t j = table_finish(A.rec, A.rs, D, A.N, target, br);
-  const double* Xj = A.rec + j * A.rs;
-#pragma unroll
-  for (int k = 0; k < KT; ++k) th[k] = Xj[k] + th[k];
-  bool ok = true;
-#pragma unroll
-  for (int k = 0; k < KT; ++k) ok = ok & (box[2 * k] <= th[k]) & (th[k] <= box[2 * k + 1]);
-  return ok;
 }
 
 __device__ __forceinline__ double pterm(double v, double p) {
@@ -671,6 +638,92 @@ __device__ __forceinline__ double sim_pnorm_regs(const SimDistArgs& M, const Blo
     }
   }
   return s;
+}
+
+// The lazy early reject for CG candidates at once: theta_0..LAZY_KT-1 of
+// attempt 0 (propose_one's operations in propose_one's order: same streams,
+// same fma chain, same X_j + (L n)_k) and statistics 0..3 (sim_pnorm_regs's
+// operations), in stages so that the memory accesses of the CG candidates
+// overlap with each other and with arithmetic: the guide loads of all CG
+// are issued, their perturbation normals computed (independent of the
+// ancestor), the searches finished and the X heads loaded (the record line
+// the search probes), the simulation normals computed, then theta, the
+// statistics and the partial p-norm.  keep[c]: candidate c may be accepted (its head left the
+// support, or its partial distance is <= eps).
+template <int D, int PK, int CG>
+__device__ __forceinline__ void lazy_head_group(const ProposalArgs& A, const SimDistArgs& M,
+                                                const BlockConsts& C, const uint64_t (&g)[CG],
+                                                double eps, bool (&keep)[CG]) {
+  constexpr int KT = LAZY_KT;
+  static_assert(D > KT, "lazy_head_group: D > LAZY_KT");
+  int oz = 0;
+  asm volatile("" : "+s"(oz));
+  const double* LT = C.LT + oz;
+  const double* box = C.box + oz;
+  double target[CG];
+  int32_t glo[CG], ghi[CG];
+#pragma unroll
+  for (int c = 0; c < CG; ++c) {
+    const u32x4 r = philox(g[c], SLOT_ANCESTOR, A.gen, A.seed);
+    target[c] = uniform53(r.x, r.y) * C.total;
+    const int64_t kt = anc_bin(target[c], C.inv_step, A.G);
+    glo[c] = A.bguide[kt];
+    ghi[c] = A.bguide[kt + 1];
+  }
+  double th[CG][KT];
+#pragma unroll
+  for (int c = 0; c < CG; ++c) {
+#pragma unroll
+    for (int k = 0; k < KT; ++k) th[c][k] = 0.0;
+    const u32x4 r = philox(g[c], SLOT_PERTURB, A.gen, A.seed);
+#pragma unroll
+    for (int q = 0; q < KT; q += 2) {
+      double n0, n1;
+      box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1, C.bmt);
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        if (k >= q) th[c][k] = fma(LT[q * D + k], n0, th[c][k]);
+        if (k >= q + 1) th[c][k] = fma(LT[(q + 1) * D + k], n1, th[c][k]);
+      }
+    }
+  }
+  const double* xh[CG];
+#pragma unroll
+  for (int c = 0; c < CG; ++c) {
+    const int64_t j = table_finish(A.rec, A.rs, D, A.N, target[c],
+                                   AncestorBracket{(int64_t)glo[c], (int64_t)ghi[c]});
+    xh[c] = A.rec + j * A.rs;
+  }
+  double xv4[CG][KT];
+#pragma unroll
+  for (int c = 0; c < CG; ++c)
+#pragma unroll
+    for (int k = 0; k < KT; ++k) xv4[c][k] = xh[c][k];
+  double e[CG][4];
+#pragma unroll
+  for (int c = 0; c < CG; ++c) {
+    const u32x4 r = philox(g[c], SLOT_SIM, A.gen, A.seed);
+    box_muller(r.x, r.y, e[c][0], e[c][1], C.bmt);
+    box_muller(r.z, r.w, e[c][2], e[c][3], C.bmt);
+  }
+#pragma unroll
+  for (int c = 0; c < CG; ++c) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      th[c][k] = xv4[c][k] + th[c][k];
+      ok = ok & (box[2 * k] <= th[c][k]) & (th[c][k] <= box[2 * k + 1]);
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double2 as = C.as[k], wx = C.wx[k];
+      const int sk = __builtin_amdgcn_readfirstlane(C.src[k]);
+      const double xv = lg_stat(as.x, as.y, th[c][sk], e[c][k]);
+      s = pnorm_acc<PK>(s, fabs(wx.x * (xv - wx.y)), M.p);
+    }
+    keep[c] = !ok || !(pnorm_finish<PK>(s, M.p) > eps);
+  }
 }
 
 }  // namespace abc

@@ -29,6 +29,10 @@ constexpr int FR_T = 256;                // threads per block
 constexpr int FR_CPT = 8;                // candidates per thread and tile
 constexpr int FR_TILE = FR_T * FR_CPT;   // candidates per block
 constexpr int FR_WORDS = FR_TILE / 64;   // 64-bit accept words per tile
+#ifndef ABC_FR_CG
+#define ABC_FR_CG 2
+#endif
+constexpr int FR_CG = ABC_FR_CG;         // lazy early reject: candidates in flight per thread
 
 struct RoundArgs {
   ProposalArgs P;
@@ -84,21 +88,20 @@ __device__ __forceinline__ void round_body(
     bool lazy_done = false;
     if constexpr (MODE == PROP_MVN && D > LAZY_KT && D <= LT_DMAX) {
       if (C.lazy) {
-        // lazy head: theta_0..3 of attempt 0 and statistics 0..3 only; a
-        // head outside the support (attempt 0 may be re-drawn) survives
+        // lazy head: theta_0..3 of attempt 0 and statistics 0..3 only, FR_CG
+        // candidates at a time (lazy_head_group); a head outside the
+        // support (attempt 0 may be re-drawn) survives
 #pragma unroll 1
-        for (int it = 0; it < FR_CPT; ++it) {
-          const int loc = it * FR_T + tid;
-          const int64_t b = tile0 + loc;
-          if (b < B) {
-            const uint64_t g = (uint64_t)(idx0 + b);
-            bool keep = true;
-            if (propose_head<D>(A.P, C, g, th)) {
-              const double s = sim_pnorm_regs<D, PK>(A.M, C, *reinterpret_cast<const double(*)[D]>(th),
-                                                     g, A.P.gen, A.P.seed, 0, 4, 0.0, nullptr);
-              keep = !(pnorm_finish<PK>(s, A.M.p) > eps);
-            }
-            if (keep) {
+        for (int it = 0; it < FR_CPT; it += FR_CG) {
+          uint64_t gs[FR_CG];
+          bool keep[FR_CG];
+#pragma unroll
+          for (int c = 0; c < FR_CG; ++c) gs[c] = (uint64_t)(idx0 + tile0 + (it + c) * FR_T + tid);
+          lazy_head_group<D, PK, FR_CG>(A.P, A.M, C, gs, eps, keep);
+#pragma unroll
+          for (int c = 0; c < FR_CG; ++c) {
+            const int loc = (it + c) * FR_T + tid;
+            if (keep[c] && tile0 + loc < B) {
               const int pos = atomicAdd(&qn, 1);
               queue[pos] = (uint16_t)loc;
             }
@@ -336,6 +339,7 @@ __global__ __launch_bounds__(256) void anc_guide_kernel(const double* __restrict
   guide[k] = (int32_t)lo;
 }
 
+// table layout: header (ANC_HDR) | records [N x rs] doubles | guide int32 [G + 2]
 struct AncTable { const double* rec; const int32_t* guide; int rs; int64_t G; const double* xmax; };
 inline AncTable anc_table_view(const void* t, int64_t N, int d) {
   AncTable v;

@@ -29,6 +29,7 @@ import math
 import numpy as np
 
 from .. import gpu
+from .._native import PRIOR_KINDS
 from ..distance.distance import SumStatMatrix
 from ..population import ColumnarParticles, Particle, Population
 from ..parameters import Parameter
@@ -122,7 +123,7 @@ class BatchedGPUSampler(Sampler):
     def __init__(self, batch_size=None, max_batch_size=1 << 22, seed=None,
                  max_attempts=10000, check_max_eval=False, fused=True,
                  max_fused_batch_size=1 << 31, filter_below=0.0,
-                 record_budget_bytes=1 << 31):
+                 filter_min_stats=5, record_budget_bytes=1 << 31):
         super().__init__()
         self.check_max_eval = check_max_eval
         self.batch_size = batch_size
@@ -135,11 +136,19 @@ class BatchedGPUSampler(Sampler):
         # the acceptor uniform and the transition an MVN / LocalTransition
         self.fused = fused
         self.max_fused_batch_size = max_fused_batch_size
-        # early-reject mode below this acceptance rate; off by default: with
-        # the proposal dominating the candidate's cost the plain round is
-        # faster at every rate (tools/bench_fused.py: 2.69e10 vs 2.52e10
-        # candidates/s at 1e-4)
+        # early-reject mode (the lazy head: theta_0..3 and 4 statistics
+        # decide most rejections) below this acceptance rate, for rounds
+        # where the lazy head applies (_lazy_capable) with at least
+        # filter_min_stats statistics.  Off by default: the round is bound
+        # by the ancestor table's random accesses (~2 Infinity-Cache misses
+        # per candidate, the same with or without the head) as much as by
+        # its arithmetic, and the head rejects few candidates when the 4
+        # statistics are a small part of the distance: c3 bench 4.54e6 vs
+        # 4.78e6 accepted/s; tools/bench_fused.py 1.4e10 vs 1.9e10
+        # candidates/s at S = 32 (profiles/r02_lazy_filter_ab.log,
+        # r02_lazy_filter_S.log)
         self.filter_below = filter_below
+        self.filter_min_stats = filter_min_stats
         self.record_budget_bytes = record_budget_bytes  # rec rows per fused round
         # first m recorded candidates are all that is used
         # (ABCSMC.max_nr_recorded_particles, smc.py:998-1001)
@@ -326,10 +335,30 @@ class BatchedGPUSampler(Sampler):
             prop = arrays()
         src, a, sigma = sim
         wf, pval = fp
-        return gpu.CandidateRound(len(spec.param_names), len(spec.sum_stat_keys),
-                                  spec.prior_kind, spec.prior_params, src, a,
-                                  sigma, spec.x0vec, wf, pval, seed, gen,
-                                  self.max_attempts, **prop)
+        fr = gpu.CandidateRound(len(spec.param_names), len(spec.sum_stat_keys),
+                                spec.prior_kind, spec.prior_params, src, a,
+                                sigma, spec.x0vec, wf, pval, seed, gen,
+                                self.max_attempts, **prop)
+        fr.src_host = getattr(spec.model, "src", None)   # host copy (_lazy_capable)
+        return fr
+
+    LAZY_KT = 4              # abc_candidate.h: the lazy head's coordinates
+
+    def _lazy_capable(self, spec, fr):
+        """Whether the fused round's early reject can take the lazy head
+        (abc_candidate.h lazy_filter_ok): shared Cholesky factor, d and S
+        beyond the head, p in {1, 2, inf}, the first 4 statistics reading
+        theta_0..3, and unbounded priors (norm, laplace), whose support
+        holds every proposal; the kernel re-checks the bound exactly."""
+        s = fr.spec
+        kinds = getattr(spec, "prior_kind_host", None)
+        src = getattr(fr, "src_host", None)
+        return (s.X is not None and not s.per_particle_L and s.d > self.LAZY_KT
+                and s.S >= max(5, self.filter_min_stats) and s.p in (1.0, 2.0, math.inf)
+                and kinds is not None
+                and all(k in (PRIOR_KINDS["norm"], PRIOR_KINDS["laplace"])
+                        for k in kinds)
+                and src is not None and all(0 <= int(v) < self.LAZY_KT for v in src[:4]))
 
     def _fused_size(self, need, ws, rate, measured, S, record):
         """Candidates per rank for the next fused round: need / rate, with a
@@ -399,7 +428,8 @@ class BatchedGPUSampler(Sampler):
             lo, _ = dd.rank_range(base, B, rank)
             rx = (torch.empty((B, S), dtype=gpu.F64, device=dev)
                   if record and rec_left > 0 else None)
-            filt = rate is not None and rate < self.filter_below and rx is None
+            filt = (rate is not None and rate < self.filter_below and rx is None
+                    and self._lazy_capable(spec, fr))
             filtered += int(filt)
             idx, cnt = fr.run(lo, B, spec.eps, cap=need, filter=filt, rec_x=rx)
             if ws == 1:

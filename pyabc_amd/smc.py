@@ -114,6 +114,7 @@ class GenerationSpec:
                               gpu.as_dev(spec[1], device=dev),
                               gpu.as_dev(x0, device=dev))
             self.prior_kind, self.prior_params, self.x0vec = cache[key]
+            self.prior_kind_host = tuple(int(k) for k in np.asarray(spec[0]).ravel())
 
     def __call__(self):
         if self._closure is None:

@@ -210,7 +210,8 @@ def test_fused_prior_kinds_and_gave_up(dev):
 
 
 @pytest.mark.parametrize("variant", ["wide_uniform", "narrow_uniform", "src_late",
-                                     "huge_x", "d5_S6"])
+                                     "huge_x", "d5_S6", "w_zeros", "w_heavy", "w_tiny",
+                                     "n65", "n1"])
 def test_fused_lazy_filter(dev, variant):
     """The lazy early reject (filter mode, MVN, d > 4): theta_0..3 of attempt
     0 and statistics 0..3 decide the rejection when every coordinate k >= 4
@@ -219,8 +220,13 @@ def test_fused_lazy_filter(dev, variant):
     and rows bit for bit: bounded priors wide enough for the lazy head
     (uniform(-50, 100)), narrow ones (the head is refused, attempt 0 may be
     re-drawn), early-reject statistics reading theta_7 (refused), a
-    population far out (|X| ~ 1e6: refused by the bound), and d = 5."""
+    population far out (|X| ~ 1e6: refused by the bound), and d = 5.  The
+    lazy head reads its ancestor from the head bins (one record per scan
+    bin with up to three candidate rows, abc_candidate.h): weights with runs
+    of zeros, one dominant row, weights over 300 decades, N = 65 and N = 1
+    exercise the bins holding more than three rows and the last rows."""
     d, S = (5, 6) if variant == "d5_S6" else (8, 9)
+    N = {"n65": 65, "n1": 1}.get(variant, 3000)
     kinds, params, src = None, None, None
     if variant == "wide_uniform":
         kinds, params = ["uniform"] * d, [[-50.0, 150.0, 0, 0]] * d
@@ -228,7 +234,21 @@ def test_fused_lazy_filter(dev, variant):
         kinds, params = ["uniform"] * d, [[-1.0, 3.0, 0, 0]] * d
     elif variant == "src_late":
         src = [7, 1, 2, 3, 4, 5, 6, 0, 1]
-    c = _case(d, S, kinds=kinds, params=params, src=src, seed=21)
+    c = _case(d, S, N=N, kinds=kinds, params=params, src=src, seed=21)
+    if variant.startswith("w_"):
+        from pyabc_amd import gpu
+        rng = np.random.default_rng(8)
+        w = rng.uniform(size=N)
+        if variant == "w_zeros":
+            w[rng.uniform(size=N) < 0.7] = 0.0
+            w[:5] = 0.0
+            w[-5:] = 0.0
+        elif variant == "w_heavy":
+            w[N // 3] = 1e4
+        else:
+            w = 10.0 ** rng.uniform(-300, 0, N)
+        cdf = gpu.inclusive_scan(T(w))
+        c.update(cdf=cdf, guide=gpu.cdf_guide(cdf))
     if variant == "huge_x":
         c["host"]["X"] = c["host"]["X"] + 1e6
         c["X"] = T(c["host"]["X"])
@@ -292,7 +312,8 @@ def test_fused_vs_oracle_replay(dev):
     np.testing.assert_allclose(lpg.cpu().numpy(), lp[sel], rtol=1e-12)
 
 
-def _abc(fused, adaptive=False, pop=4000, max_fused=1 << 31, local=False, S=10):
+def _abc(fused, adaptive=False, pop=4000, max_fused=1 << 31, local=False, S=10,
+         filter_below=0.01):
     import pyabc_amd as pa
     d = 4 if local else 10
     names = [f"p{k}" for k in range(d)]
@@ -305,7 +326,8 @@ def _abc(fused, adaptive=False, pop=4000, max_fused=1 << 31, local=False, S=10):
     dist = (pa.AdaptivePNormDistance(p=2) if adaptive else pa.PNormDistance(p=2))
     tr = pa.LocalTransition(k=50, k_fraction=None) if local else pa.MultivariateNormalTransition()
     sampler = pa.BatchedGPUSampler(seed=77, fused=fused,
-                                   max_fused_batch_size=max_fused)
+                                   max_fused_batch_size=max_fused,
+                                   filter_below=filter_below, filter_min_stats=5)
     np.random.seed(3)
     abc = pa.ABCSMC(model, prior, dist, population_size=pop, transitions=tr,
                     eps=pa.QuantileEpsilon(alpha=0.5), sampler=sampler)
@@ -313,22 +335,27 @@ def _abc(fused, adaptive=False, pop=4000, max_fused=1 << 31, local=False, S=10):
     return abc
 
 
-@pytest.mark.parametrize("adaptive,local,max_fused,S",
-                         [(False, False, 1 << 31, 10), (True, False, 1 << 31, 24),
-                          (False, False, 5000, 10), (False, True, 1 << 31, 6)])
-def test_sampler_fused_equals_staged(dev, adaptive, local, max_fused, S):
+@pytest.mark.parametrize("adaptive,local,max_fused,S,filt",
+                         [(False, False, 1 << 31, 10, 0.01), (True, False, 1 << 31, 24, 0.01),
+                          (False, False, 5000, 10, 0.01), (False, True, 1 << 31, 6, 0.01),
+                          (False, False, 1 << 31, 10, 1.0), (False, False, 20000, 10, 1.0)])
+def test_sampler_fused_equals_staged(dev, adaptive, local, max_fused, S, filt):
     """Whole generations: fused and staged samplers give the same populations,
     weights, epsilons and evaluation counts (several rounds per generation
-    with a small fused batch)."""
+    with a small fused batch; every round in early-reject mode with
+    filter_below = 1)."""
     runs = []
     for fused in (False, True):
-        abc = _abc(fused, adaptive=adaptive, max_fused=max_fused, local=local, S=S)
+        abc = _abc(fused, adaptive=adaptive, max_fused=max_fused, local=local, S=S,
+                   filter_below=filt)
         h = abc.run(max_nr_populations=4)
         pops = [h.get_population_device(t) for t in range(h.max_t + 1)]
         runs.append((abc, pops, [g["n_sim"] for g in abc.generation_log],
                      [g["eps"] for g in abc.generation_log]))
         if fused:
             assert abc.sampler.last_stats.get("fused")
+            if filt == 1.0:
+                assert abc.sampler.last_stats.get("filtered_rounds", 0) > 0
     (_, p0, n0, e0), (_, p1, n1, e1) = runs
     assert n0 == n1 and e0 == e1
     for a, b in zip(p0, p1):

@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--d", type=int, default=10)
     ap.add_argument("--S", type=int, default=None, help="statistics (default d)")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--wsigma", type=float, default=0.0,
+                    help="lognormal importance weights, ESS/N = exp(-wsigma^2) "
+                         "(c3's last generations: ~1e-2)")
     ap.add_argument("--staged", action="store_true")
     ap.add_argument("--modes", nargs="+", default=["plain", "filter"],
                     choices=["plain", "filter"])
@@ -36,7 +39,8 @@ def main():
     S = a.S or a.d
     g = torch.Generator(device="cpu").manual_seed(0)
     X = (0.8 + np.sqrt(0.2) * torch.randn(N, d, generator=g, dtype=torch.float64)).to(dev)
-    w = torch.ones(N, dtype=torch.float64, device=dev) / N
+    w = torch.exp(a.wsigma * torch.randn(N, generator=g, dtype=torch.float64)).to(dev)
+    w /= w.sum()
     bw = (4 / (2e4 * (d + 2))) ** (1 / (d + 4))
     L = torch.eye(d, dtype=torch.float64, device=dev) * (bw * np.sqrt(0.2))
     cdf = gpu.inclusive_scan(w)
