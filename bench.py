@@ -55,6 +55,9 @@ def parse():
                     help="worker processes of the CPU baseline (the box's CPU "
                          "share per GPU is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--collectives", default="torch", choices=["torch", "abc"],
+                    help="abc: the sampler's all-gathers through libabcgpu's RCCL "
+                         "wrappers (abc_comm_*) instead of torch.distributed")
     ap.add_argument("--filter-below", type=float, default=None,
                     help="BatchedGPUSampler.filter_below (default: the sampler's)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -243,6 +246,10 @@ def main():
     if ws != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {ws}", file=sys.stderr)
     import pyabc_amd as pa  # noqa: F401  (loads libabcgpu.so, fails loudly)
+    if ws > 1 and args.collectives == "abc":
+        from pyabc_amd.sampler import distributed as dd
+        from pyabc_amd.sampler.comm import RcclComm
+        dd.use_comm(RcclComm.from_process_group())
     abc, tr = build_abc(args, rank, ws)
     timer = KernelTimer(tr)
 

@@ -35,6 +35,7 @@ extern "C" {
 #define ABC_ERR_WORKSPACE (-3)
 #define ABC_ERR_NOT_ENOUGH_PARTICLES (-4)
 #define ABC_ERR_UNSUPPORTED (-5)
+#define ABC_ERR_COMM (-6)      /* RCCL missing or a collective failed */
 
 /* Precision of the transition-density kernel. */
 #define ABC_PREC_F64 0 /* f64 MFMA cross term: parity mode (default)   */
@@ -394,6 +395,35 @@ int abc_temper_sums(const double* dens, const double* lr,
                     const double* lr_sub, int64_t R, double pdf_norm, int scale_log, int mode, double beta,
                     double shift, double* out, void* ws, size_t ws_bytes,
                     void* stream);
+
+/* ---- multi-GPU collectives (RCCL over xGMI), SURVEY.md 8(b)/(e) -----------
+ * The reference has no collective: MulticoreEvalParallelSampler
+ * (multicore_evaluation_parallel.py:92-150) forks workers that share one
+ * evaluation counter and queue their particles to the parent.  Here one
+ * process drives one GPU and the ranks exchange, per generation, the accept
+ * counts (all-gather), the accepted rows (one packed all-gather) and, when
+ * the distance adapts, the recorded rows (pyabc_amd/sampler/distributed.py).
+ * These entry points give a binding without torch.distributed the same
+ * transport: RCCL is opened with dlopen on first use (librccl.so.1), so the
+ * library itself does not depend on it.  The caller moves the 128-byte
+ * unique id from rank 0 to the others by any channel (the Python binding
+ * uses torch.distributed's broadcast), then every rank calls
+ * abc_comm_init.  All calls are stream-ordered on `stream`. */
+#define ABC_COMM_ID_BYTES 128
+#define ABC_COMM_F64 0
+#define ABC_COMM_I64 1
+#define ABC_COMM_SUM 0
+#define ABC_COMM_MAX 1
+#define ABC_COMM_MIN 2
+int abc_comm_unique_id(void* id);
+int abc_comm_init(void** comm, int nranks, int rank, const void* id);
+int abc_comm_destroy(void* comm);
+/* recv[nranks * bytes] = the ranks' send[bytes] in rank order */
+int abc_comm_allgather(void* comm, const void* send, void* recv, size_t bytes,
+                       void* stream);
+int abc_comm_allreduce(void* comm, const void* send, void* recv, size_t count,
+                       int dtype, int op, void* stream);
+int abc_comm_broadcast(void* comm, void* buf, size_t bytes, int root, void* stream);
 
 #ifdef __cplusplus
 }

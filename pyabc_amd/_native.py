@@ -80,6 +80,12 @@ SIGNATURES = {
                                     P, P, P]),
     "abc_temper_workspace": (SZ, []),
     "abc_temper_sums": (I32, [P, P, P, I64, D, I32, I32, D, D, P, P, SZ, P]),
+    "abc_comm_unique_id": (I32, [P]),
+    "abc_comm_init": (I32, [P, I32, I32, P]),
+    "abc_comm_destroy": (I32, [P]),
+    "abc_comm_allgather": (I32, [P, P, P, SZ, P]),
+    "abc_comm_allreduce": (I32, [P, P, P, SZ, I32, I32, P]),
+    "abc_comm_broadcast": (I32, [P, P, SZ, I32, P]),
 }
 
 
@@ -102,6 +108,10 @@ ABC_ERR_HIP = -2
 ABC_ERR_WORKSPACE = -3
 ABC_ERR_NOT_ENOUGH_PARTICLES = -4
 ABC_ERR_UNSUPPORTED = -5
+ABC_ERR_COMM = -6
+ABC_COMM_ID_BYTES = 128
+ABC_COMM_F64, ABC_COMM_I64 = 0, 1
+ABC_COMM_SUM, ABC_COMM_MAX, ABC_COMM_MIN = 0, 1, 2
 ABC_PROF_DENSITY, ABC_PROF_CANDIDATES, ABC_PROF_REGEN, ABC_PROF_RESCUE = 0, 1, 2, 3
 ABC_PREC_F64 = 0
 ABC_PREC_F32 = 1

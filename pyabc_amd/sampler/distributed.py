@@ -138,11 +138,25 @@ def allgather_rows_ordered(tensors, keeps, device):
     return res
 
 
+_comm = None
+
+
+def use_comm(comm):
+    """Route the flat all-gathers of device tensors through `comm` (an
+    RcclComm over the C ABI's abc_comm_*) instead of torch.distributed;
+    None restores torch.distributed."""
+    global _comm
+    _comm = comm
+
+
 def all_gather_flat(out, t):
     """dist.all_gather_into_tensor(out, t) on every backend: RCCL (nccl)
     gathers device tensors directly; gloo, whose flat all-gather takes host
     tensors only, gets host copies (multi-rank runs on one GPU, CPU tests).
-    The caller's packing and cutting are the same code either way."""
+    The caller's packing and cutting are the same code either way.  With
+    use_comm(RcclComm) device tensors go through libabcgpu's RCCL wrappers."""
+    if _comm is not None and t.is_cuda:
+        return _comm.all_gather_into(out, t.contiguous())
     if t.is_cuda and dist.get_backend() == "gloo":
         host = torch.empty(out.shape, dtype=out.dtype)
         dist.all_gather_into_tensor(host, t.cpu())

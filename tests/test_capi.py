@@ -59,3 +59,19 @@ def test_store_library_exports_abcstore_h():
     h = ctypes.c_void_p()
     assert lib.abc_store_open(b"/nonexistent-dir/x.db", ctypes.byref(h)) != 0
     assert b"open" in lib.abc_store_last_error()
+
+
+def test_comm_unique_id_and_argument_checks():
+    """The RCCL wrappers (abc_comm_*): RCCL is opened on first use; a unique
+    id needs no GPU; bad ranks are rejected before RCCL is touched."""
+    import pytest
+    from pyabc_amd import _native as nat
+    a = ctypes.create_string_buffer(nat.ABC_COMM_ID_BYTES)
+    b = ctypes.create_string_buffer(nat.ABC_COMM_ID_BYTES)
+    nat.call("abc_comm_unique_id", a)
+    nat.call("abc_comm_unique_id", b)
+    assert a.raw != b.raw
+    h = ctypes.c_void_p()
+    with pytest.raises(ValueError):
+        nat.call("abc_comm_init", ctypes.addressof(h), 2, 2, a)
+    assert nat.load().abc_comm_destroy(None) == 0
