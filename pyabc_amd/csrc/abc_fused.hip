@@ -308,20 +308,40 @@ __global__ __launch_bounds__(256) void fused_regen_kernel(
 __global__ __launch_bounds__(256) void anc_records_kernel(const double* __restrict__ X,
                                                           const double* __restrict__ cdf,
                                                           int64_t N, int d, int rs,
-                                                          double* __restrict__ rec,
-                                                          unsigned long long* __restrict__ xmax_bits) {
-  const int64_t e0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t e = e0 < N * rs ? e0 : N * rs - 1;  // whole waves reach the max
+                                                          double* __restrict__ rec) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= N * rs) return;
   const int64_t i = e / rs;
   const int k = (int)(e - i * rs);
-  const double v = k < d ? X[i * d + k] : (k == d ? cdf[i] : 0.0);
-  if (e0 == e) rec[e] = v;
-  // max |X_jk| into the header (lazy_filter_ok): the bits of a non-negative
-  // double order like the value (a NaN sorts above +inf and disables it)
-  double a = k < d ? fabs(v) : 0.0;
-  a = wave_max(a);
-  if ((threadIdx.x & 63) == 0)
-    atomicMax(xmax_bits, (unsigned long long)__double_as_longlong(a));
+  rec[e] = k < d ? X[i * d + k] : (k == d ? cdf[i] : 0.0);
+}
+
+// max |X_jk| into the table header (lazy_filter_ok): a grid-stride pass
+// with one atomic per block (one per wave on a single address serialised
+// ~250k atomics per c3 table, ~3 ms); the bits of a non-negative double
+// order like the value (a NaN sorts above +inf and disables the lazy head)
+constexpr int XMAX_BLOCKS = 512;
+__global__ __launch_bounds__(256) void anc_xmax_kernel(const double* __restrict__ X,
+                                                       int64_t n,
+                                                       unsigned long long* __restrict__ xmax_bits) {
+  __shared__ unsigned long long wm[4];
+  unsigned long long a = 0ull;  // bits of |x|: order like the values, NaN on top
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(fabs(X[e]));
+    a = b > a ? b : a;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long b = __shfl_xor(a, o, 64);
+    a = b > a ? b : a;
+  }
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = 0ull;
+    for (int w = 0; w < 4; ++w) m = wm[w] > m ? wm[w] : m;
+    atomicMax(xmax_bits, m);
+  }
 }
 
 // guide[k] = first i with anc_bin(cdf_i) >= k (N if none), k = 0 .. G + 1
@@ -451,7 +471,11 @@ extern "C" int abc_ancestor_table(const double* X, const double* cdf, int64_t N,
   hipStream_t s = as_stream(stream);
   ABC_HIP(hipMemsetAsync(table, 0, ANC_HDR, s));
   hipLaunchKernelGGL(anc_records_kernel, dim3((unsigned)ceil_div(N * v.rs, 256)), dim3(256), 0,
-                     s, X, cdf, N, d, v.rs, const_cast<double*>(v.rec),
+                     s, X, cdf, N, d, v.rs, const_cast<double*>(v.rec));
+  ABC_LAUNCHED();
+  const int64_t nx = N * (int64_t)d;
+  const int64_t xb = ceil_div(nx, 256) < XMAX_BLOCKS ? ceil_div(nx, 256) : XMAX_BLOCKS;
+  hipLaunchKernelGGL(anc_xmax_kernel, dim3((unsigned)xb), dim3(256), 0, s, X, nx,
                      static_cast<unsigned long long*>(table));
   ABC_LAUNCHED();
   hipLaunchKernelGGL(anc_guide_kernel, dim3((unsigned)ceil_div(v.G + 2, 256)), dim3(256), 0, s,

@@ -7,22 +7,29 @@
 // per column of the recorded [R x S] matrix.  np.median: the middle order
 // statistic for odd R, the mean (a + b) / 2 of the two middle ones for even R.
 //
-// Layout: the row-major [R x S] fp64 matrix is transposed once (LDS tiles)
-// into column-major order-preserving u64 keys Kc[S][R].  One 1024-thread
-// workgroup per column then selects the rank-k key with 12-bit MSD digits:
-//   level 0: histogram of bits 63..52 over the column (LDS atomics), pick the
-//            bin holding rank k;
-//   level l: one pass over the surviving set that compacts the keys of the
-//            picked bin into scratch (in place from level 2 on, chunk-wise
-//            behind a barrier) and histograms their next digit.
-// The surviving set shrinks by ~the bin count per level.  Long columns are
-// first bracketed by a sorted sample (see BR_MARG): one streaming pass keeps
-// the ~12% of keys around the wanted rank, so a select costs ~1 full read of
-// the column instead of ~2.  For even R the (k+1)-th statistic is tracked along:
-// while it falls in the same bin it survives with rank k; once it falls in
-// the next non-empty bin it is the minimum of that bin, taken in the next
-// pass (LDS 64-bit atomic min).  Results are exact and bitwise deterministic
-// (the selection is order independent).
+// Layout: the recorded matrix stays row-major [R x S] fp64 (no transposed
+// copy).  Per pass (the median, then the median of |x - median|):
+//   col_sample_kernel   one workgroup per column sorts SMP evenly spaced
+//                       keys and brackets the wanted rank(s) by the sample
+//                       order statistics BR_MARG places either side;
+//   col_bracket_kernel  one streaming, coalesced read of the whole matrix
+//                       (each thread owns one column of a row band) counts
+//                       the keys below each column's window and compacts
+//                       the window (~12% of the column) into scratch;
+//   col_select_kernel   one 1024-thread workgroup per column selects the
+//                       rank-k key inside the window with 12-bit MSD digits:
+//     level 0: histogram of bits 63..52 (LDS atomics), pick the bin holding
+//              rank k;
+//     level l: one pass over the surviving set that compacts the keys of the
+//              picked bin in place (chunk-wise behind a barrier) and
+//              histograms their next digit.
+// When a column's rank is not inside its window (a sample that
+// misrepresents the column) the select runs over the whole column, read
+// strided from X.  For even R the (k+1)-th statistic is tracked along: while
+// it falls in the same bin it survives with rank k; once it falls in the
+// next non-empty bin it is the minimum of that bin, taken in the next pass
+// (LDS 64-bit atomic min).  Results are exact and bitwise deterministic (the
+// selection does not depend on the order of the compacted keys).
 #include "abc_common.h"
 
 namespace abc {
@@ -30,7 +37,6 @@ namespace {
 
 constexpr int SEL_T = 1024;
 constexpr int SEL_BITS = 12, SEL_BINS = 1 << SEL_BITS;
-constexpr int TP = 64;  // transpose tile
 
 __device__ __forceinline__ uint64_t f2key_s(double v) {
   if (v == 0.0) v = 0.0;  // -0.0 ties with +0.0
@@ -40,26 +46,6 @@ __device__ __forceinline__ uint64_t f2key_s(double v) {
 __device__ __forceinline__ double key2f_s(uint64_t k) {
   uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
   return __longlong_as_double((long long)b);
-}
-
-// X [R x S] row-major fp64 -> Kc [S][R] keys; 64 x 64 tiles through LDS
-__global__ __launch_bounds__(256) void transpose_keys_kernel(
-    const double* __restrict__ X, int64_t R, int S, uint64_t* __restrict__ Kc) {
-  __shared__ uint64_t tile[TP][TP + 1];
-  const int64_t r0 = (int64_t)blockIdx.x * TP;
-  const int c0 = blockIdx.y * TP;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
-  for (int i = ty; i < TP; i += 4) {
-    const int64_t r = r0 + i;
-    const int c = c0 + tx;
-    if (r < R && c < S) tile[i][tx] = f2key_s(X[r * S + c]);
-  }
-  __syncthreads();
-  for (int i = ty; i < TP; i += 4) {
-    const int c = c0 + i;
-    const int64_t r = r0 + tx;
-    if (r < R && c < S) Kc[(int64_t)c * R + r] = tile[tx][i];
-  }
 }
 
 // sample bracketing: columns with R >= BR_MIN first take SMP evenly spaced
@@ -131,79 +117,123 @@ __device__ void find_bins(SelShared& sh, int64_t k, bool want2) {
   __syncthreads();
 }
 
-// DEV: keys are f2key(|key2f(Kc) - med[c]|) (the MAD deviations)
+// key of element i of column c (DEV: of |x - med|, the MAD deviations)
+template <bool DEV>
+__device__ __forceinline__ uint64_t col_key(const double* __restrict__ X, int S, int c,
+                                            int64_t i, double m) {
+  const double v = X[i * S + c];
+  return DEV ? f2key_s(fabs(v - m)) : f2key_s(v);
+}
+// the rank(s) the median needs: k (and k + 1 for even R)
+__host__ __device__ inline int64_t med_rank(int64_t R) { return (R & 1) ? (R - 1) / 2 : R / 2 - 1; }
+
+// Per column: sample SMP keys, sort them and store the key window [lo, hi]
+// that brackets the wanted rank(s); columns shorter than BR_MIN get the
+// whole key range (their "window" is the column).
+template <bool DEV>
+__global__ __launch_bounds__(SEL_T) void col_sample_kernel(
+    const double* __restrict__ X, int64_t R, int S, const double* __restrict__ med,
+    uint64_t* __restrict__ win, unsigned long long* __restrict__ cnt) {
+  __shared__ SelShared sh;
+  const int c = blockIdx.x, t = threadIdx.x;
+  if (t == 0) { cnt[2 * c] = 0ull; cnt[2 * c + 1] = 0ull; }  // in window, below
+  if (R < BR_MIN) {
+    if (t == 0) { win[2 * c] = 0ull; win[2 * c + 1] = ~0ull; }
+    return;
+  }
+  const double m = DEV ? med[c] : 0.0;
+  for (int q = t; q < SMP; q += SEL_T)
+    sh.smp[q] = col_key<DEV>(X, S, c, ((2 * (int64_t)q + 1) * R) / (2 * SMP), m);
+  __syncthreads();
+  sort_sample(sh);
+  if (t == 0) {
+    const int64_t k = med_rank(R);
+    const int64_t j1 = (k * SMP) / R - BR_MARG;
+    const int64_t j2 = ((k + ((R & 1) ? 0 : 1)) * SMP) / R + BR_MARG;
+    win[2 * c] = j1 < 0 ? 0ull : sh.smp[j1];
+    win[2 * c + 1] = j2 >= SMP ? ~0ull : sh.smp[j2];
+  }
+}
+
+// One coalesced read of X: thread t of a block owns column c0 + t % CB of
+// the rows r = t / CB (mod RPI) of the block's row band; it counts the keys
+// below its column's window and stages the window's keys in LDS, BK_STAGE
+// at a time, before reserving room in the column's scratch segment (one
+// global atomic per BK_STAGE keys).  BK_U rows are in flight per thread.
+// (Two columns per thread with 16-byte loads measured 2x slower at c4: the
+// per-thread work doubles and the returning atomics serialise it.)  The
+// order of the compacted keys is not deterministic; the selection does not
+// depend on it.
+constexpr int BK_T = 256, BK_STAGE = 16, BK_U = 4;
+template <bool DEV>
+__global__ __launch_bounds__(BK_T) void col_bracket_kernel(
+    const double* __restrict__ X, int64_t R, int S, const double* __restrict__ med,
+    const uint64_t* __restrict__ win, int64_t rows_per_block,
+    unsigned long long* __restrict__ cnt, uint64_t* __restrict__ scratch) {
+  __shared__ uint64_t stage[BK_STAGE][BK_T];
+  const int t = threadIdx.x;
+  const int CB = S < BK_T ? S : BK_T;           // columns per block
+  const int RPI = BK_T / CB;                    // rows per iteration
+  const int c = blockIdx.y * CB + t % CB;
+  const int rsub = t / CB;
+  if (rsub >= RPI || c >= S) return;            // no barrier below
+  const double m = DEV ? med[c] : 0.0;
+  const uint64_t lo = win[2 * c], hi = win[2 * c + 1];
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < R ? r0 + rows_per_block : R;
+  uint64_t* sc = scratch + (int64_t)c * R;
+  unsigned long long below = 0;
+  int n = 0;
+  auto take = [&](uint64_t key) {
+    below += key < lo ? 1ull : 0ull;
+    if (key >= lo && key <= hi) {
+      stage[n++][t] = key;
+      if (n == BK_STAGE) {
+        const unsigned long long pos = atomicAdd(&cnt[2 * c], (unsigned long long)BK_STAGE);
+#pragma unroll
+        for (int e = 0; e < BK_STAGE; ++e) sc[pos + e] = stage[e][t];
+        n = 0;
+      }
+    }
+  };
+  int64_t r = r0 + rsub;
+  for (; r + (BK_U - 1) * RPI < r1; r += BK_U * RPI) {
+    uint64_t k4[BK_U];
+#pragma unroll
+    for (int u = 0; u < BK_U; ++u) k4[u] = col_key<DEV>(X, S, c, r + u * RPI, m);
+#pragma unroll
+    for (int u = 0; u < BK_U; ++u) take(k4[u]);
+  }
+  for (; r < r1; r += RPI) take(col_key<DEV>(X, S, c, r, m));
+  if (n) {
+    const unsigned long long pos = atomicAdd(&cnt[2 * c], (unsigned long long)n);
+    for (int e = 0; e < n; ++e) sc[pos + e] = stage[e][t];
+  }
+  if (below) atomicAdd(&cnt[2 * c + 1], below);
+}
+
+// Rank-k select of column c from its compacted window (cnt[2c] keys in
+// scratch, cnt[2c + 1] keys below it), or from the whole column when the
+// rank is outside the window.
 template <bool DEV>
 __global__ __launch_bounds__(SEL_T) void col_select_kernel(
-    const uint64_t* __restrict__ Kc, int64_t R, const double* __restrict__ med,
-    uint64_t* __restrict__ scratch, double* __restrict__ out) {
+    const double* __restrict__ X, int64_t R, int S, const double* __restrict__ med,
+    const unsigned long long* __restrict__ cnt, uint64_t* __restrict__ scratch,
+    double* __restrict__ out) {
   __shared__ SelShared sh;
   const int c = blockIdx.x;
   const int t = threadIdx.x;
-  const uint64_t* col = Kc + (int64_t)c * R;
   uint64_t* sc = scratch + (int64_t)c * R;
   const double m = DEV ? med[c] : 0.0;
-  auto keyof = [&](uint64_t k) -> uint64_t {
-    if (!DEV) return k;
-    return f2key_s(fabs(key2f_s(k) - m));
-  };
-  int64_t k = (R & 1) ? (R - 1) / 2 : R / 2 - 1;
+  auto colkey = [&](int64_t i) -> uint64_t { return col_key<DEV>(X, S, c, i, m); };
+  int64_t k = med_rank(R);
   bool want2 = (R & 1) == 0;     // still tracking rank k+1 inside the set
   bool have2 = false;            // rank k+1 resolved as a bin minimum
   uint64_t v2 = 0;
   int64_t n = R;
   bool in_scratch = false;
-  const int lane = t & 63;
-  if (R >= BR_MIN) {
-    // ---- sample bracketing (see BR_MARG): one pass instead of two
-    for (int q = t; q < SMP; q += SEL_T)
-      sh.smp[q] = keyof(col[((2 * (int64_t)q + 1) * R) / (2 * SMP)]);
-    if (t == 0) { sh.cnt = 0; sh.below = 0; }
-    __syncthreads();
-    sort_sample(sh);
-    if (t == 0) {
-      const int64_t j1 = (k * SMP) / R - BR_MARG;
-      const int64_t j2 = ((k + (want2 ? 1 : 0)) * SMP) / R + BR_MARG;
-      sh.lo = j1 < 0 ? 0ull : sh.smp[j1];
-      sh.hi = j2 >= SMP ? ~0ull : sh.smp[j2];
-    }
-    __syncthreads();
-    const uint64_t lo = sh.lo, hi = sh.hi;
-    uint64_t below = 0;
-    for (int64_t base = 0; base < R; base += (int64_t)SEL_T * BR_U) {
-      uint64_t kv[BR_U];
-      bool keep[BR_U];
-      uint64_t bal[BR_U];
-#pragma unroll
-      for (int u = 0; u < BR_U; ++u) {
-        const int64_t i = base + (int64_t)u * SEL_T + t;
-        kv[u] = i < R ? col[i] : 0;
-      }
-      uint32_t tot = 0;
-#pragma unroll
-      for (int u = 0; u < BR_U; ++u) {
-        const int64_t i = base + (int64_t)u * SEL_T + t;
-        const uint64_t key = keyof(kv[u]);
-        kv[u] = key;
-        below += (i < R && key < lo) ? 1 : 0;
-        keep[u] = i < R && key >= lo && key <= hi;
-        bal[u] = __ballot(keep[u]);
-        tot += (uint32_t)__popcll(bal[u]);
-      }
-      uint32_t wpos = 0;
-      if (lane == 0 && tot) wpos = atomicAdd(&sh.cnt, tot);
-      wpos = __shfl(wpos, 0, 64);
-      const uint64_t lt = (1ull << lane) - 1;
-#pragma unroll
-      for (int u = 0; u < BR_U; ++u) {
-        if (keep[u]) sc[wpos + __popcll(bal[u] & lt)] = kv[u];
-        wpos += (uint32_t)__popcll(bal[u]);
-      }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) below += __shfl_down(below, o, 64);
-    if (lane == 0 && below) atomicAdd(&sh.below, (unsigned long long)below);
-    __syncthreads();
-    const int64_t nin = sh.cnt, bel = (int64_t)sh.below;
+  {
+    const int64_t nin = (int64_t)cnt[2 * c], bel = (int64_t)cnt[2 * c + 1];
     if (bel <= k && k + (want2 ? 1 : 0) < bel + nin) {  // uniform
       k -= bel;
       n = nin;
@@ -221,14 +251,13 @@ __global__ __launch_bounds__(SEL_T) void col_select_kernel(
 #pragma unroll
     for (int u = 0; u < BR_U; ++u) {
       const int64_t i = base + (int64_t)u * SEL_T + t;
-      kv[u] = i < n ? (in_scratch ? sc[i] : col[i]) : 0;
+      kv[u] = i < n ? (in_scratch ? sc[i] : colkey(i)) : 0;
     }
 #pragma unroll
     for (int u = 0; u < BR_U; ++u) {
       const int64_t i = base + (int64_t)u * SEL_T + t;
       if (i < n) {
-        const uint64_t key = in_scratch ? kv[u] : keyof(kv[u]);
-        atomicAdd(&sh.hist[(key >> shift) & (SEL_BINS - 1)], 1u);
+        atomicAdd(&sh.hist[(kv[u] >> shift) & (SEL_BINS - 1)], 1u);
       }
     }
   }
@@ -256,7 +285,6 @@ __global__ __launch_bounds__(SEL_T) void col_select_kernel(
     __syncthreads();
     // compaction pass: keep the keys of bin b1, histogram their next digit;
     // in place (chunk-wise behind a barrier) once the set lives in scratch
-    const uint64_t* src = in_scratch ? sc : col;
     for (int64_t base = 0; base < n; base += SEL_T * 4) {
       uint64_t kv[4];
       bool keep[4];
@@ -265,7 +293,7 @@ __global__ __launch_bounds__(SEL_T) void col_select_kernel(
         const int64_t i = base + (int64_t)u * SEL_T + t;
         keep[u] = false;
         if (i < n) {
-          kv[u] = in_scratch ? src[i] : keyof(src[i]);
+          kv[u] = in_scratch ? sc[i] : colkey(i);
           const uint64_t hi = (kv[u] & pmask) ^ prefix;  // 0 iff in bin b1
           keep[u] = hi == 0;
           if (track_min && ((kv[u] >> shift) & (SEL_BINS - 1)) == (uint64_t)b2 &&
@@ -307,9 +335,10 @@ __global__ __launch_bounds__(SEL_T) void col_select_kernel(
 
 size_t select_ws_bytes(int64_t R, int S) {
   size_t off = 0;
-  size_only<uint64_t>(off, (size_t)R * S);  // keys
-  size_only<uint64_t>(off, (size_t)R * S);  // scratch
-  size_only<double>(off, (size_t)S);        // medians
+  size_only<uint64_t>(off, (size_t)R * S);             // window keys (worst case: all)
+  size_only<uint64_t>(off, (size_t)2 * S);             // windows [lo, hi]
+  size_only<unsigned long long>(off, (size_t)2 * S);   // in-window / below counts
+  size_only<double>(off, (size_t)S);                   // medians
   return off + 256;
 }
 
@@ -317,20 +346,48 @@ size_t select_ws_bytes(int64_t R, int S) {
 int column_mad_select(const double* X, int64_t R, int S, double* out, void* ws,
                       size_t ws_bytes, hipStream_t s) {
   Carver cv(ws, ws_bytes);
-  uint64_t* Kc = cv.take<uint64_t>((size_t)R * S);
   uint64_t* scratch = cv.take<uint64_t>((size_t)R * S);
+  uint64_t* win = cv.take<uint64_t>((size_t)2 * S);
+  unsigned long long* cnt = cv.take<unsigned long long>((size_t)2 * S);
   double* med = cv.take<double>((size_t)S);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "column_mad: workspace carve");
-  hipLaunchKernelGGL(transpose_keys_kernel,
-                     dim3((unsigned)ceil_div(R, TP), (unsigned)ceil_div(S, TP)),
-                     dim3(256), 0, s, X, R, S, Kc);
-  ABC_LAUNCHED();
-  hipLaunchKernelGGL(col_select_kernel<false>, dim3((unsigned)S), dim3(SEL_T), 0, s,
-                     (const uint64_t*)Kc, R, (const double*)nullptr, scratch, med);
-  ABC_LAUNCHED();
-  hipLaunchKernelGGL(col_select_kernel<true>, dim3((unsigned)S), dim3(SEL_T), 0, s,
-                     (const uint64_t*)Kc, R, (const double*)med, scratch, out);
-  ABC_LAUNCHED();
+  const int CB = S < BK_T ? S : BK_T;
+  const int ctiles = (int)ceil_div(S, CB);
+  const int rpi = BK_T / CB;
+  // ~1024 row bands in all (>= 4 waves per CU), at least BK_U rows per thread
+  int64_t bands = 1024 / ctiles;
+  bands = bands < 1 ? 1 : bands;
+  int64_t rpb = ceil_div(R, bands);
+  if (rpb < BK_U * rpi) rpb = BK_U * rpi;
+  const unsigned nb = (unsigned)ceil_div(R, rpb);
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool dev = pass == 1;
+    double* dst = dev ? out : med;
+    if (!dev) {
+      hipLaunchKernelGGL(col_sample_kernel<false>, dim3((unsigned)S), dim3(SEL_T), 0, s, X, R, S,
+                         (const double*)med, win, cnt);
+    } else {
+      hipLaunchKernelGGL(col_sample_kernel<true>, dim3((unsigned)S), dim3(SEL_T), 0, s, X, R, S,
+                         (const double*)med, win, cnt);
+    }
+    ABC_LAUNCHED();
+    if (!dev) {
+      hipLaunchKernelGGL(col_bracket_kernel<false>, dim3(nb, (unsigned)ctiles), dim3(BK_T), 0, s,
+                         X, R, S, (const double*)med, (const uint64_t*)win, rpb, cnt, scratch);
+    } else {
+      hipLaunchKernelGGL(col_bracket_kernel<true>, dim3(nb, (unsigned)ctiles), dim3(BK_T), 0, s,
+                         X, R, S, (const double*)med, (const uint64_t*)win, rpb, cnt, scratch);
+    }
+    ABC_LAUNCHED();
+    if (!dev) {
+      hipLaunchKernelGGL(col_select_kernel<false>, dim3((unsigned)S), dim3(SEL_T), 0, s, X, R, S,
+                         (const double*)med, (const unsigned long long*)cnt, scratch, dst);
+    } else {
+      hipLaunchKernelGGL(col_select_kernel<true>, dim3((unsigned)S), dim3(SEL_T), 0, s, X, R, S,
+                         (const double*)med, (const unsigned long long*)cnt, scratch, dst);
+    }
+    ABC_LAUNCHED();
+  }
   return ABC_OK;
 }
 
