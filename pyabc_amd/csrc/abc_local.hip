@@ -437,14 +437,24 @@ __global__ __launch_bounds__(256) void local_select_kernel(
 // (sum a, sum a^2, sum a d, upper triangle of sum a d d^T with a the
 // neighbour's weight) in the lane's registers.  The rows are split into RS
 // chunks (grid.y) for occupancy; the partial moments go to part[RS][NM][N]
-// and local_finish_kernel adds them in chunk order (deterministic).
-template <int D>
+// and local_finish_kernel adds them in chunk order (deterministic).  Above
+// d = 8 the NM moments no longer fit one lane's registers: the kernel is
+// instantiated per slice SL of MSLICE moments (the distance and membership
+// test are recomputed per slice; the same bits).
+constexpr int MSLICE = 48;
+template <int D> constexpr int local_nm() { return 2 + D + D * (D + 1) / 2; }
+template <int D> constexpr int local_nslices() { return (local_nm<D>() + MSLICE - 1) / MSLICE; }
+
+template <int D, int SL>
 __global__ __launch_bounds__(256) void local_moments_kernel(
     const double* __restrict__ X, const double* __restrict__ w, int64_t N,
     const unsigned long long* __restrict__ sel_v,
     const long long* __restrict__ sel_jcut,
     const long long* __restrict__ sel_rank0, double* __restrict__ part) {
-  constexpr int NM = 2 + D + D * (D + 1) / 2;
+  constexpr int NM = local_nm<D>();
+  constexpr int C0 = SL * MSLICE;
+  constexpr int C1 = C0 + MSLICE < NM ? C0 + MSLICE : NM;
+  constexpr int NS = C1 - C0;
   const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t ne = n < N ? n : N - 1;
   const int RS = gridDim.y;
@@ -454,9 +464,9 @@ __global__ __launch_bounds__(256) void local_moments_kernel(
   for (int q = 0; q < D; ++q) xp[q] = X[ne * D + q];
   const unsigned long long vs = sel_v[ne];
   const long long jcut = sel_jcut[ne], r0 = sel_rank0[ne];
-  double m[NM];
+  double m[NS];
 #pragma unroll
-  for (int t = 0; t < NM; ++t) m[t] = 0.0;
+  for (int t = 0; t < NS; ++t) m[t] = 0.0;
   auto row = [&](int64_t j, const double (&xj)[D]) {
     const unsigned long long key = (unsigned long long)__double_as_longlong(dist2v<D>(xj, xp));
     if ((key < vs || (key == vs && j < jcut)) && j != r0) {
@@ -464,19 +474,22 @@ __global__ __launch_bounds__(256) void local_moments_kernel(
       double dj[D];
 #pragma unroll
       for (int q = 0; q < D; ++q) dj[q] = xj[q] - xp[q];
-      m[0] += lw;
-      m[1] += lw * lw;
+      if (0 >= C0 && 0 < C1) m[0 - C0] += lw;
+      if (1 >= C0 && 1 < C1) m[1 - C0] += lw * lw;
       int c = 2 + D;
 #pragma unroll
       for (int a = 0; a < D; ++a) {
-        m[2 + a] += lw * dj[a];
+        if (2 + a >= C0 && 2 + a < C1) m[2 + a - C0] += lw * dj[a];
 #pragma unroll
-        for (int b = a; b < D; ++b) m[c++] += lw * dj[a] * dj[b];
+        for (int b = a; b < D; ++b) {
+          if (c >= C0 && c < C1) m[c - C0] += lw * dj[a] * dj[b];
+          ++c;
+        }
       }
     }
   };
   // 8 rows per step: their (scalar) loads issue together, then the pairs
-  constexpr int RU = 8;
+  constexpr int RU = D <= 8 ? 8 : 4;
   int64_t j = j0;
   for (; j + RU <= j1; j += RU) {
     double xa[RU][D];
@@ -495,7 +508,7 @@ __global__ __launch_bounds__(256) void local_moments_kernel(
   }
   if (n < N) {
 #pragma unroll
-    for (int t = 0; t < NM; ++t) part[((int64_t)blockIdx.y * NM + t) * N + n] = m[t];
+    for (int t = 0; t < NS; ++t) part[((int64_t)blockIdx.y * NM + C0 + t) * N + n] = m[t];
   }
 }
 
@@ -507,8 +520,7 @@ __global__ __launch_bounds__(256) void local_finish_kernel(
     const double* __restrict__ part, int RS, double* __restrict__ covs,
     double* __restrict__ invs, double* __restrict__ dets,
     double* __restrict__ chol, double* __restrict__ lnorm) {
-  constexpr int NT = D * (D + 1) / 2;
-  constexpr int NM = 2 + D + NT;
+  constexpr int NM = local_nm<D>();
   const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
   double cov[D][D];
@@ -586,7 +598,18 @@ inline int moments_chunks(int64_t N) {
   return (int)(rs < 1 ? 1 : rs);
 }
 
-constexpr int SEL_PB = 8;  // particles per selection block (in registers)
+// particles per selection block (their coordinates in registers)
+template <int D> constexpr int sel_pb() { return D <= 8 ? 8 : 4; }
+
+template <int D, int SL>
+void launch_moments(const double* X, const double* w, int64_t N, const unsigned long long* sel_v,
+                    const long long* sel_ties, const long long* sel_rank0, double* part, int RS,
+                    hipStream_t s) {
+  hipLaunchKernelGGL((local_moments_kernel<D, SL>), dim3((unsigned)ceil_div(N, 256), (unsigned)RS),
+                     dim3(256), 0, s, X, w, N, sel_v, sel_ties, sel_rank0, part);
+  if constexpr (SL + 1 < local_nslices<D>())
+    launch_moments<D, SL + 1>(X, w, N, sel_v, sel_ties, sel_rank0, part, RS, s);
+}
 
 template <int D>
 int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
@@ -599,18 +622,16 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   long long* sel_rank0 = cv.take<long long>((size_t)N);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
   if (N > 1) {
-    hipLaunchKernelGGL((local_select_kernel<D, SEL_PB>), dim3((unsigned)ceil_div(N, SEL_PB)),
+    hipLaunchKernelGGL((local_select_kernel<D, sel_pb<D>()>), dim3((unsigned)ceil_div(N, sel_pb<D>())),
                        dim3(256), 0, s, X, N, nq, sel_v, sel_ties, sel_rank0);
     ABC_LAUNCHED();
   }
-  constexpr int NM = 2 + D + D * (D + 1) / 2;
+  constexpr int NM = local_nm<D>();
   const int RS = N > 1 ? moments_chunks(N) : 1;
   double* part = cv.take<double>((size_t)RS * NM * (size_t)N);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
   if (N > 1) {
-    hipLaunchKernelGGL((local_moments_kernel<D>), dim3((unsigned)ceil_div(N, 256), (unsigned)RS),
-                       dim3(256), 0, s, X, w, N, (const unsigned long long*)sel_v,
-                       (const long long*)sel_ties, (const long long*)sel_rank0, part);
+    launch_moments<D, 0>(X, w, N, sel_v, sel_ties, sel_rank0, part, RS, s);
     ABC_LAUNCHED();
   }
   hipLaunchKernelGGL((local_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256),
@@ -638,7 +659,7 @@ template <int D>
 struct LocalFeat {
   static constexpr int K0 = D * (D + 1) / 2 + D + 1;
   static constexpr int KB = (K0 + 3) / 4;          // MFMA k-blocks of 4
-  static constexpr int NT = KB <= 6 ? 4 : 2;       // candidate tiles per wave
+  static constexpr int NT = KB <= 6 ? 4 : (KB <= 16 ? 2 : 1);  // candidate tiles per wave
 };
 
 // feature k of centred candidate y (order: a <= b pairs, linear, constant)
@@ -888,7 +909,7 @@ extern "C" int abc_local_fit(const double* X, const double* w, int64_t N,
                              double* covs, double* inv_covs, double* dets,
                              double* chol, double* log_norm, void* ws,
                              size_t ws_bytes, void* stream) {
-  ABC_CHECK_ARG(N >= 1 && d >= 1 && d <= 8 && k >= 1, "local_fit: bad N/d/k (d <= 8)");
+  ABC_CHECK_ARG(N >= 1 && d >= 1 && d <= 16 && k >= 1, "local_fit: bad N/d/k (d <= 16)");
   ABC_CHECK_ARG(ws && ws_bytes >= abc_local_fit_workspace(N, d), "local_fit: workspace");
   ABC_CHECK_ARG(X && w && covs && inv_covs && dets && chol && log_norm, "local_fit: null pointer");
   const int64_t nq = (k + 1) < N ? (k + 1) : N;
@@ -896,6 +917,7 @@ extern "C" int abc_local_fit(const double* X, const double* w, int64_t N,
   switch (d) {
 #define ABC_D(n) case n: return launch_fit<n>(X, w, N, nq, scaling, eps, covs, inv_covs, dets, chol, log_norm, ws, ws_bytes, s);
     ABC_D(1) ABC_D(2) ABC_D(3) ABC_D(4) ABC_D(5) ABC_D(6) ABC_D(7) ABC_D(8)
+    ABC_D(9) ABC_D(10) ABC_D(11) ABC_D(12) ABC_D(13) ABC_D(14) ABC_D(15) ABC_D(16)
 #undef ABC_D
   }
   return set_error(ABC_ERR_UNSUPPORTED, "local_fit: d=%d", d);
@@ -905,6 +927,7 @@ extern "C" size_t abc_local_logpdf_workspace(int64_t M, int64_t N, int d) {
   switch (d) {
 #define ABC_D(n) case n: return pdf_workspace<n>(M, N, nullptr);
     ABC_D(1) ABC_D(2) ABC_D(3) ABC_D(4) ABC_D(5) ABC_D(6) ABC_D(7) ABC_D(8)
+    ABC_D(9) ABC_D(10) ABC_D(11) ABC_D(12) ABC_D(13) ABC_D(14) ABC_D(15) ABC_D(16)
 #undef ABC_D
   }
   return 256;
@@ -915,13 +938,14 @@ extern "C" int abc_local_logpdf(const double* x, int64_t M, const double* X,
                                 const double* inv_covs,
                                 const double* log_norm, double* out,
                                 void* ws, size_t ws_bytes, void* stream) {
-  ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= 8, "local_logpdf: bad M/N/d");
+  ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= 16, "local_logpdf: bad M/N/d (d <= 16)");
   if (M == 0) return ABC_OK;
   ABC_CHECK_ARG(x && X && w && inv_covs && log_norm && out && ws, "local_logpdf: null pointer");
   hipStream_t s = as_stream(stream);
   switch (d) {
 #define ABC_D(n) case n: return launch_pdf<n>(x, M, X, w, N, inv_covs, log_norm, out, ws, ws_bytes, s);
     ABC_D(1) ABC_D(2) ABC_D(3) ABC_D(4) ABC_D(5) ABC_D(6) ABC_D(7) ABC_D(8)
+    ABC_D(9) ABC_D(10) ABC_D(11) ABC_D(12) ABC_D(13) ABC_D(14) ABC_D(15) ABC_D(16)
 #undef ABC_D
   }
   return set_error(ABC_ERR_UNSUPPORTED, "local_logpdf: d=%d", d);

@@ -21,7 +21,7 @@ from .exceptions import NotEnoughParticles
 class LocalTransition(Transition):
     EPS = 1e-3
     MIN_K = 10
-    MAX_DIM = 8
+    MAX_DIM = 16
 
     def __init__(self, k=None, k_fraction=1 / 4, scaling=1):
         if k_fraction is not None:

@@ -313,9 +313,9 @@ def test_fused_vs_oracle_replay(dev):
 
 
 def _abc(fused, adaptive=False, pop=4000, max_fused=1 << 31, local=False, S=10,
-         filter_below=0.01):
+         filter_below=0.01, dim=None):
     import pyabc_amd as pa
-    d = 4 if local else 10
+    d = dim or (4 if local else 10)
     names = [f"p{k}" for k in range(d)]
     keys = [f"y{k}" for k in range(S)]
     rng = np.random.default_rng(1234)
@@ -335,19 +335,23 @@ def _abc(fused, adaptive=False, pop=4000, max_fused=1 << 31, local=False, S=10,
     return abc
 
 
-@pytest.mark.parametrize("adaptive,local,max_fused,S,filt",
-                         [(False, False, 1 << 31, 10, 0.01), (True, False, 1 << 31, 24, 0.01),
-                          (False, False, 5000, 10, 0.01), (False, True, 1 << 31, 6, 0.01),
-                          (False, False, 1 << 31, 10, 1.0), (False, False, 20000, 10, 1.0)])
-def test_sampler_fused_equals_staged(dev, adaptive, local, max_fused, S, filt):
+@pytest.mark.parametrize("adaptive,local,max_fused,S,filt,dim",
+                         [(False, False, 1 << 31, 10, 0.01, None),
+                          (True, False, 1 << 31, 24, 0.01, None),
+                          (False, False, 5000, 10, 0.01, None),
+                          (False, True, 1 << 31, 6, 0.01, None),
+                          (False, False, 1 << 31, 10, 1.0, None),
+                          (False, False, 20000, 10, 1.0, None),
+                          (False, True, 1 << 31, 12, 0.01, 12)])
+def test_sampler_fused_equals_staged(dev, adaptive, local, max_fused, S, filt, dim):
     """Whole generations: fused and staged samplers give the same populations,
     weights, epsilons and evaluation counts (several rounds per generation
     with a small fused batch; every round in early-reject mode with
-    filter_below = 1)."""
+    filter_below = 1; LocalTransition at d = 12)."""
     runs = []
     for fused in (False, True):
         abc = _abc(fused, adaptive=adaptive, max_fused=max_fused, local=local, S=S,
-                   filter_below=filt)
+                   filter_below=filt, dim=dim)
         h = abc.run(max_nr_populations=4)
         pops = [h.get_population_device(t) for t in range(h.max_t + 1)]
         runs.append((abc, pops, [g["n_sim"] for g in abc.generation_log],

@@ -229,11 +229,15 @@ def gpu_as(a, dev):
 @pytest.mark.parametrize("grid,N,d,k", [(None, 3000, 5, 50), (None, 3000, 5, 700),
                                          (7, 2000, 3, 50), (2, 1500, 3, 40),
                                          (None, 12000, 5, 3000), (None, 4096, 2, 10),
-                                         (3, 5000, 4, 200)])
+                                         (3, 5000, 4, 200), (None, 3000, 10, 50),
+                                         (None, 2500, 16, 300), (3, 3000, 9, 100),
+                                         (None, 9000, 13, 2500)])
 def test_local_fit_selection_paths_vs_oracle(dev, grid, N, d, k):
     """k-NN selection: the sample-bracketed path (N >= 2048), the LDS bucket
     path (small and large k) and the radix-pass fallback (a {0,1}^3 grid: buckets of hundreds of exact ties,
-    taken by index) against the oracle's (distance, index) order."""
+    taken by index) against the oracle's (distance, index) order.  d = 9..16
+    run the 4-particle selection blocks and the sliced moments (several
+    kernels over one moment list each)."""
     from pyabc_amd import gpu
     rng = np.random.default_rng(N + k)
     if grid is None:
@@ -251,7 +255,9 @@ def test_local_fit_selection_paths_vs_oracle(dev, grid, N, d, k):
 
 
 @pytest.mark.parametrize("d,N,M,offset", [(5, 3001, 777, 0.0), (2, 17, 5, 40.0),
-                                            (8, 1000, 130, 5.0), (1, 64, 64, 0.0)])
+                                            (8, 1000, 130, 5.0), (1, 64, 64, 0.0),
+                                            (10, 700, 130, 2.0), (13, 333, 65, 1.0),
+                                            (16, 500, 70, 0.0)])
 def test_local_logpdf_mfma_vs_oracle(dev, d, N, M, offset):
     """fp64-MFMA quadratic-feature GEMM vs the fp64 oracle: ragged N / M
     (tiles of 16 rows, 64-candidate waves), a population far from the origin
