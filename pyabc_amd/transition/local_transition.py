@@ -8,7 +8,7 @@ Reference: pyabc/transition/local_transition.py:13-145.
   pdf      :98-110  np.average(exp(-d^T inv_j d / 2) / norm_j, weights=w)
   rvs      :141-145 j ~ Cat(w), theta ~ N(X_j, cov_j)
 Device kernels: abc_local_fit (exact radix-select k-NN + moments + small
-fp64 linear algebra), abc_local_logpdf, abc_local_propose.  d <= 8.
+fp64 linear algebra), abc_local_logpdf, abc_local_propose.  d <= 16.
 """
 import numpy as np
 import pandas as pd
