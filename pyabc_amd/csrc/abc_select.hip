@@ -156,60 +156,83 @@ __global__ __launch_bounds__(SEL_T) void col_sample_kernel(
 }
 
 // One coalesced read of X: thread t of a block owns column c0 + t % CB of
-// the rows r = t / CB (mod RPI) of the block's row band; it counts the keys
-// below its column's window and stages the window's keys in LDS, BK_STAGE
-// at a time, before reserving room in the column's scratch segment (one
-// global atomic per BK_STAGE keys).  BK_U rows are in flight per thread.
-// (Two columns per thread with 16-byte loads measured 2x slower at c4: the
-// per-thread work doubles and the returning atomics serialise it.)  The
-// order of the compacted keys is not deterministic; the selection does not
-// depend on it.
-constexpr int BK_T = 256, BK_STAGE = 16, BK_U = 4;
+// the rows r = t / CB (mod RPI) of the block's band of BK_ROWS rows.  Keys
+// below a column's window are counted in registers; keys inside it go to an
+// LDS pool of (key, column) pairs (LDS atomics only).  After the band, one
+// global atomic per column reserves room in the column's scratch segment and
+// the pool is scattered there.  A band whose window keys overflow the pool
+// (heavy ties: a constant column is all window) sends the rest straight to
+// scratch, one returning global atomic per key.  The order of the compacted
+// keys is not deterministic; the selection does not depend on it.
+#ifndef ABC_BK_U
+#define ABC_BK_U 8
+#endif
+#ifndef ABC_BK_ROWS
+#define ABC_BK_ROWS 96
+#endif
+constexpr int BK_T = 256, BK_U = ABC_BK_U, BK_ROWS = ABC_BK_ROWS, BK_CAP = 4096;
 template <bool DEV>
 __global__ __launch_bounds__(BK_T) void col_bracket_kernel(
     const double* __restrict__ X, int64_t R, int S, const double* __restrict__ med,
     const uint64_t* __restrict__ win, int64_t rows_per_block,
     unsigned long long* __restrict__ cnt, uint64_t* __restrict__ scratch) {
-  __shared__ uint64_t stage[BK_STAGE][BK_T];
+  __shared__ uint64_t pool[BK_CAP];
+  __shared__ uint16_t pool_c[BK_CAP];
+  __shared__ uint32_t pool_n;
+  __shared__ uint32_t col_n[BK_T];                 // pool keys per local column
+  __shared__ unsigned long long col_base[BK_T];    // their scratch offsets
   const int t = threadIdx.x;
-  const int CB = S < BK_T ? S : BK_T;           // columns per block
-  const int RPI = BK_T / CB;                    // rows per iteration
-  const int c = blockIdx.y * CB + t % CB;
+  const int CB = S < BK_T ? S : BK_T;              // columns per block
+  const int RPI = BK_T / CB;                       // rows per iteration
+  const int cl = t % CB;
+  const int c = blockIdx.y * CB + cl;
   const int rsub = t / CB;
-  if (rsub >= RPI || c >= S) return;            // no barrier below
-  const double m = DEV ? med[c] : 0.0;
-  const uint64_t lo = win[2 * c], hi = win[2 * c + 1];
+  const bool active = rsub < RPI && c < S;
+  if (t == 0) pool_n = 0;
+  col_n[t] = 0;
+  __syncthreads();
+  const double m = (DEV && active) ? med[c] : 0.0;
+  const uint64_t lo = active ? win[2 * c] : 0ull, hi = active ? win[2 * c + 1] : 0ull;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = r0 + rows_per_block < R ? r0 + rows_per_block : R;
   uint64_t* sc = scratch + (int64_t)c * R;
   unsigned long long below = 0;
-  int n = 0;
   auto take = [&](uint64_t key) {
     below += key < lo ? 1ull : 0ull;
     if (key >= lo && key <= hi) {
-      stage[n++][t] = key;
-      if (n == BK_STAGE) {
-        const unsigned long long pos = atomicAdd(&cnt[2 * c], (unsigned long long)BK_STAGE);
-#pragma unroll
-        for (int e = 0; e < BK_STAGE; ++e) sc[pos + e] = stage[e][t];
-        n = 0;
+      const uint32_t pos = atomicAdd(&pool_n, 1u);
+      if (pos < (uint32_t)BK_CAP) {
+        pool[pos] = key;
+        pool_c[pos] = (uint16_t)cl;
+        atomicAdd(&col_n[cl], 1u);
+      } else {  // overflow: straight to scratch
+        sc[atomicAdd(&cnt[2 * c], 1ull)] = key;
       }
     }
   };
-  int64_t r = r0 + rsub;
-  for (; r + (BK_U - 1) * RPI < r1; r += BK_U * RPI) {
-    uint64_t k4[BK_U];
+  if (active) {
+    int64_t r = r0 + rsub;
+    for (; r + (BK_U - 1) * RPI < r1; r += BK_U * RPI) {
+      uint64_t k4[BK_U];
 #pragma unroll
-    for (int u = 0; u < BK_U; ++u) k4[u] = col_key<DEV>(X, S, c, r + u * RPI, m);
+      for (int u = 0; u < BK_U; ++u) k4[u] = col_key<DEV>(X, S, c, r + u * RPI, m);
 #pragma unroll
-    for (int u = 0; u < BK_U; ++u) take(k4[u]);
+      for (int u = 0; u < BK_U; ++u) take(k4[u]);
+    }
+    for (; r < r1; r += RPI) take(col_key<DEV>(X, S, c, r, m));
+    if (below) atomicAdd(&cnt[2 * c + 1], below);
   }
-  for (; r < r1; r += RPI) take(col_key<DEV>(X, S, c, r, m));
-  if (n) {
-    const unsigned long long pos = atomicAdd(&cnt[2 * c], (unsigned long long)n);
-    for (int e = 0; e < n; ++e) sc[pos + e] = stage[e][t];
+  __syncthreads();
+  // one reservation per column, then the pool in place (col_n counts down)
+  if (t < CB && blockIdx.y * CB + t < S && col_n[t])
+    col_base[t] = atomicAdd(&cnt[2 * (blockIdx.y * CB + t)], (unsigned long long)col_n[t]);
+  __syncthreads();
+  const uint32_t np = pool_n < (uint32_t)BK_CAP ? pool_n : (uint32_t)BK_CAP;
+  for (uint32_t e = t; e < np; e += BK_T) {
+    const int q = pool_c[e];
+    const uint32_t slot = atomicSub(&col_n[q], 1u) - 1u;
+    scratch[(int64_t)(blockIdx.y * CB + q) * R + col_base[q] + slot] = pool[e];
   }
-  if (below) atomicAdd(&cnt[2 * c + 1], below);
 }
 
 // Rank-k select of column c from its compacted window (cnt[2c] keys in
@@ -353,12 +376,9 @@ int column_mad_select(const double* X, int64_t R, int S, double* out, void* ws,
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "column_mad: workspace carve");
   const int CB = S < BK_T ? S : BK_T;
   const int ctiles = (int)ceil_div(S, CB);
-  const int rpi = BK_T / CB;
-  // ~1024 row bands in all (>= 4 waves per CU), at least BK_U rows per thread
-  int64_t bands = 1024 / ctiles;
-  bands = bands < 1 ? 1 : bands;
-  int64_t rpb = ceil_div(R, bands);
-  if (rpb < BK_U * rpi) rpb = BK_U * rpi;
+  // expected window keys per band ~12.5% x 96 x 256 = 3072 < BK_CAP (measured
+  // at c4: 96 rows 1.17 ms per MAD, 64 rows 1.44, 128 rows 1.17-1.28)
+  const int64_t rpb = BK_ROWS;
   const unsigned nb = (unsigned)ceil_div(R, rpb);
   for (int pass = 0; pass < 2; ++pass) {
     const bool dev = pass == 1;
