@@ -1,0 +1,55 @@
+"""Host-side decisions of the batched sampler (no GPU): when a fused round
+may take the lazy early reject (BatchedGPUSampler._lazy_capable mirrors the
+device-side lazy_filter_ok preconditions of abc_candidate.h; the kernel
+re-checks the support bound exactly), and the round sizing."""
+import math
+import types
+
+import pytest
+
+from pyabc_amd._native import PRIOR_KINDS
+from pyabc_amd.sampler.batched import BatchedGPUSampler
+
+
+def _fr(d=10, S=10, p=2.0, X=1, ppl=0, src=None):
+    spec = types.SimpleNamespace(X=X, per_particle_L=ppl, d=d, S=S, p=p)
+    return types.SimpleNamespace(spec=spec, src_host=list(range(S)) if src is None else src)
+
+
+def _gen(kinds=("norm",) * 10):
+    return types.SimpleNamespace(prior_kind_host=tuple(PRIOR_KINDS[k] for k in kinds))
+
+
+@pytest.mark.parametrize("case,ok", [
+    (dict(), True),
+    (dict(p=1.0), True),
+    (dict(p=math.inf), True),
+    (dict(p=3.0), False),                 # partial p-norm not monotone-exact
+    (dict(X=None), False),                # t = 0: prior proposals
+    (dict(ppl=1), False),                 # LocalTransition factors
+    (dict(d=4, S=10), False),             # the head is the whole theta
+    (dict(S=4), False),                   # the 4 statistics are all of them
+    (dict(src=[7, 1, 2, 3, 4, 5, 6, 8, 9, 0]), False),   # stat 0 reads theta_7
+])
+def test_lazy_capable(case, ok):
+    s = BatchedGPUSampler(seed=1, filter_min_stats=5)
+    assert s._lazy_capable(_gen(), _fr(**case)) is ok
+
+
+def test_lazy_capable_priors_and_min_stats():
+    s = BatchedGPUSampler(seed=1, filter_min_stats=5)
+    assert s._lazy_capable(_gen(("laplace",) * 10), _fr())
+    assert not s._lazy_capable(_gen(("uniform",) + ("norm",) * 9), _fr())
+    assert not s._lazy_capable(types.SimpleNamespace(), _fr())   # no host kinds
+    assert not BatchedGPUSampler(seed=1, filter_min_stats=16)._lazy_capable(_gen(), _fr())
+    assert BatchedGPUSampler(seed=1).filter_below == 0.0        # off by default
+
+
+def test_fused_round_sizing():
+    s = BatchedGPUSampler(seed=1)
+    # need / rate (+6% once measured) / ranks + 4096, capped by the launch budget
+    assert s._fused_size(1000, 1, 0.01, False, 10, False) == 1000 * 100 + 4096
+    assert s._fused_size(1000, 2, 0.01, True, 10, False) == int(1000 * 100 * 1.06 / 2 + 4096)
+    assert s._fused_size(10 ** 9, 1, 1e-6, True, 10, False) == s.max_fused_batch_size
+    # record_rejected: rows of S doubles within record_budget_bytes
+    assert s._fused_size(10 ** 6, 1, 1e-3, True, 256, True) == s.record_budget_bytes // (8 * 256)
