@@ -241,8 +241,8 @@ __global__ __launch_bounds__(BK_T) void col_bracket_kernel(
 template <bool DEV>
 __global__ __launch_bounds__(SEL_T) void col_select_kernel(
     const double* __restrict__ X, int64_t R, int S, const double* __restrict__ med,
-    const unsigned long long* __restrict__ cnt, uint64_t* __restrict__ scratch,
-    double* __restrict__ out) {
+    const unsigned long long* __restrict__ cnt, const uint64_t* __restrict__ win,
+    uint64_t* __restrict__ scratch, double* __restrict__ out) {
   __shared__ SelShared sh;
   const int c = blockIdx.x;
   const int t = threadIdx.x;
@@ -255,20 +255,26 @@ __global__ __launch_bounds__(SEL_T) void col_select_kernel(
   uint64_t v2 = 0;
   int64_t n = R;
   bool in_scratch = false;
+  int top = 64;                  // bits below which the candidate keys differ
   {
     const int64_t nin = (int64_t)cnt[2 * c], bel = (int64_t)cnt[2 * c + 1];
     if (bel <= k && k + (want2 ? 1 : 0) < bel + nin) {  // uniform
       k -= bel;
       n = nin;
       in_scratch = true;
+      // every window key lies in [lo, hi], so shares their common high bits:
+      // the digits start below them (no pass over a constant digit)
+      const uint64_t d = win[2 * c] ^ win[2 * c + 1];
+      top = d ? 64 - __clzll((long long)d) : 0;
     }
     // else: the full select below, from the column
   }
+  const uint64_t low = top >= 64 ? ~0ull : ((1ull << top) - 1);
   // ---- level 0: histogram of the top digit over the (bracketed) set
   for (int i = t; i < SEL_BINS; i += SEL_T) sh.hist[i] = 0;
   if (t == 0) sh.b2 = -1;
   __syncthreads();
-  int shift = 64 - SEL_BITS;
+  int shift = top > SEL_BITS ? top - SEL_BITS : 0;
   for (int64_t base = 0; base < n; base += (int64_t)SEL_T * BR_U) {
     uint64_t kv[BR_U];
 #pragma unroll
@@ -286,7 +292,7 @@ __global__ __launch_bounds__(SEL_T) void col_select_kernel(
   }
   __syncthreads();
   find_bins(sh, k, want2);
-  uint64_t prefix = 0, pmask = 0;
+  uint64_t pmask = ~low, prefix = in_scratch ? (win[2 * c] & pmask) : 0ull;
   while (true) {
     const int b1 = sh.b1, b2 = sh.b2;
     k -= sh.below1;
@@ -401,10 +407,12 @@ int column_mad_select(const double* X, int64_t R, int S, double* out, void* ws,
     ABC_LAUNCHED();
     if (!dev) {
       hipLaunchKernelGGL(col_select_kernel<false>, dim3((unsigned)S), dim3(SEL_T), 0, s, X, R, S,
-                         (const double*)med, (const unsigned long long*)cnt, scratch, dst);
+                         (const double*)med, (const unsigned long long*)cnt, (const uint64_t*)win,
+                         scratch, dst);
     } else {
       hipLaunchKernelGGL(col_select_kernel<true>, dim3((unsigned)S), dim3(SEL_T), 0, s, X, R, S,
-                         (const double*)med, (const unsigned long long*)cnt, scratch, dst);
+                         (const double*)med, (const unsigned long long*)cnt, (const uint64_t*)win,
+                         scratch, dst);
     }
     ABC_LAUNCHED();
   }
