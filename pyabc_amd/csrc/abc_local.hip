@@ -44,6 +44,84 @@ __device__ __forceinline__ double dist2(const double* __restrict__ X, int64_t j,
   return dist2v<D>(xj, xn);
 }
 
+// ---- fp32 prefilter of the fp64 squared distances ---------------------------
+// The moments sweep compares s = |x_j - x_n|^2 (the fp64 fma chain of
+// dist2v) with the particle's k-th key v*.  The same chain in fp32 on fp32
+// copies of X, s32, decides most comparisons at twice the fp64 rate (k = 50
+// at c5: 7.1 -> 3.3 ms; in the selection sweeps the extra registers cost
+// more occupancy than the fp32 arithmetic saved, 15.9 -> 31.5 ms, so they
+// stay fp64): with u = 2^-24, M = max |x| over the population and the exact
+// s (and every fp32/fp64 rounding of the copies, the differences and the
+// fma chain accounted for)
+//   |s32 - s64| <= B(s) = 1.01 (4 u M sqrt(D s) + (D + 2) u s
+//                               + D u^2 (2 M + sqrt(s))^2) + 2^-1000,
+// B increasing and s - B(s) increasing above the tiny floor handled below,
+// so s32 < V - B(V) implies s64 < V and s32 > V + B(V) implies s64 > V.
+// Pairs between the two cuts, and s32 == 0 (exact duplicates, the rank-0
+// index), take the fp64 path.  The cuts are rounded outward to fp32.
+template <int D>
+__device__ __forceinline__ float dist2f(const float (&xj)[D], const float (&xn)[D]) {
+  float s = 0.0f;
+#pragma unroll
+  for (int q = 0; q < D; ++q) { const float t = xj[q] - xn[q]; s = __builtin_fmaf(t, t, s); }
+  return s;
+}
+template <int D>
+__device__ __forceinline__ double f32_bound(double V, double M) {
+  constexpr double u = 5.9604644775390625e-08;  // 2^-24
+  const double r = sqrt(V);
+  return 1.01 * (4.0 * u * M * sqrt((double)D) * r + (D + 2) * u * V +
+                 D * u * u * (2.0 * M + r) * (2.0 * M + r)) + 1e-300;
+}
+// fp32 c with c <= V - B(V) (-1 when that is not positive: no fast "below")
+template <int D>
+__device__ __forceinline__ float f32_cut_below(double V, double M) {
+  const double t = V - f32_bound<D>(V, M);
+  if (!(t > 0.0)) return -1.0f;
+  float c = (float)t;
+  if ((double)c > t) c = __uint_as_float(__float_as_uint(c) - 1u);  // c > t > 0
+  return c;
+}
+// fp32 c with c >= V + B(V) (+inf when V is not finite)
+template <int D>
+__device__ __forceinline__ float f32_cut_above(double V, double M) {
+  const double t = V + f32_bound<D>(V, M);
+  if (!(t < 3.0e38)) return INFINITY;
+  float c = (float)t;
+  if ((double)c < t) c = __uint_as_float(__float_as_uint(c) + 1u);  // 0 < c < t
+  return c;
+}
+__device__ __forceinline__ double key_val(unsigned long long k) {
+  return __longlong_as_double((long long)k);
+}
+
+// X32 = (float)X and M = max |X| (bits of a non-negative double, block-reduced
+// atomic max; a NaN orders above +inf and disables every fast path)
+__global__ __launch_bounds__(256) void local_prep_kernel(const double* __restrict__ X, int64_t n,
+                                                         float* __restrict__ X32,
+                                                         unsigned long long* __restrict__ mbits) {
+  __shared__ unsigned long long wm[4];
+  unsigned long long a = 0ull;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    const double v = X[e];
+    X32[e] = (float)v;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(fabs(v));
+    a = b > a ? b : a;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long b = __shfl_xor(a, o, 64);
+    a = b > a ? b : a;
+  }
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = 0ull;
+    for (int w = 0; w < 4; ++w) m = wm[w] > m ? wm[w] : m;
+    atomicMax(mbits, m);
+  }
+}
+
 // LU with partial pivoting (getrf order: pivot = first max |a[r][c]|,
 // multipliers l = a[r][c] * (1 / pivot)); returns det and keeps the factors
 // in a, the row permutation in perm.  The determinant and the inverse come
@@ -447,7 +525,8 @@ template <int D> constexpr int local_nslices() { return (local_nm<D>() + MSLICE 
 
 template <int D, int SL>
 __global__ __launch_bounds__(256) void local_moments_kernel(
-    const double* __restrict__ X, const double* __restrict__ w, int64_t N,
+    const double* __restrict__ X, const float* __restrict__ X32,
+    const double* __restrict__ Mp, const double* __restrict__ w, int64_t N,
     const unsigned long long* __restrict__ sel_v,
     const long long* __restrict__ sel_jcut,
     const long long* __restrict__ sel_rank0, double* __restrict__ part) {
@@ -464,12 +543,30 @@ __global__ __launch_bounds__(256) void local_moments_kernel(
   for (int q = 0; q < D; ++q) xp[q] = X[ne * D + q];
   const unsigned long long vs = sel_v[ne];
   const long long jcut = sel_jcut[ne], r0 = sel_rank0[ne];
+  float xp32[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) xp32[q] = X32[ne * D + q];
+  // fp32 prefilter of the membership test key <= v* (see f32_bound)
+  const double M = *Mp;
+  const float cut_in = f32_cut_below<D>(key_val(vs), M);   // s32 < cut_in: member
+  const float cut_out = f32_cut_above<D>(key_val(vs), M);  // s32 > cut_out: not one
   double m[NS];
 #pragma unroll
   for (int t = 0; t < NS; ++t) m[t] = 0.0;
-  auto row = [&](int64_t j, const double (&xj)[D]) {
-    const unsigned long long key = (unsigned long long)__double_as_longlong(dist2v<D>(xj, xp));
-    if ((key < vs || (key == vs && j < jcut)) && j != r0) {
+  auto row = [&](int64_t j, const float (&xj32)[D]) {
+    const float s32 = dist2f<D>(xj32, xp32);
+    if (s32 > cut_out) return;
+    bool member;
+    double xj[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
+    if (s32 < cut_in && s32 > 0.0f) {
+      member = true;
+    } else {
+      const unsigned long long key = (unsigned long long)__double_as_longlong(dist2v<D>(xj, xp));
+      member = key < vs || (key == vs && j < jcut);
+    }
+    if (member && j != r0) {
       const double lw = w[j];
       double dj[D];
 #pragma unroll
@@ -488,22 +585,23 @@ __global__ __launch_bounds__(256) void local_moments_kernel(
       }
     }
   };
-  // 8 rows per step: their (scalar) loads issue together, then the pairs
+  // 8 rows per step: their (scalar) fp32 loads issue together, then the
+  // pairs; the fp64 row is loaded only for pairs the prefilter leaves open
   constexpr int RU = D <= 8 ? 8 : 4;
   int64_t j = j0;
   for (; j + RU <= j1; j += RU) {
-    double xa[RU][D];
+    float xa[RU][D];
 #pragma unroll
     for (int u = 0; u < RU; ++u)
 #pragma unroll
-      for (int q = 0; q < D; ++q) xa[u][q] = X[(j + u) * D + q];
+      for (int q = 0; q < D; ++q) xa[u][q] = X32[(j + u) * D + q];
 #pragma unroll
     for (int u = 0; u < RU; ++u) row(j + u, xa[u]);
   }
   for (; j < j1; ++j) {
-    double xj[D];
+    float xj[D];
 #pragma unroll
-    for (int q = 0; q < D; ++q) xj[q] = X[j * D + q];
+    for (int q = 0; q < D; ++q) xj[q] = X32[j * D + q];
     row(j, xj);
   }
   if (n < N) {
@@ -602,13 +700,13 @@ inline int moments_chunks(int64_t N) {
 template <int D> constexpr int sel_pb() { return D <= 8 ? 8 : 4; }
 
 template <int D, int SL>
-void launch_moments(const double* X, const double* w, int64_t N, const unsigned long long* sel_v,
-                    const long long* sel_ties, const long long* sel_rank0, double* part, int RS,
-                    hipStream_t s) {
+void launch_moments(const double* X, const float* X32, const double* M, const double* w,
+                    int64_t N, const unsigned long long* sel_v, const long long* sel_ties,
+                    const long long* sel_rank0, double* part, int RS, hipStream_t s) {
   hipLaunchKernelGGL((local_moments_kernel<D, SL>), dim3((unsigned)ceil_div(N, 256), (unsigned)RS),
-                     dim3(256), 0, s, X, w, N, sel_v, sel_ties, sel_rank0, part);
+                     dim3(256), 0, s, X, X32, M, w, N, sel_v, sel_ties, sel_rank0, part);
   if constexpr (SL + 1 < local_nslices<D>())
-    launch_moments<D, SL + 1>(X, w, N, sel_v, sel_ties, sel_rank0, part, RS, s);
+    launch_moments<D, SL + 1>(X, X32, M, w, N, sel_v, sel_ties, sel_rank0, part, RS, s);
 }
 
 template <int D>
@@ -620,7 +718,17 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   unsigned long long* sel_v = cv.take<unsigned long long>((size_t)N);
   long long* sel_ties = cv.take<long long>((size_t)N);  // index cutoff of the ties
   long long* sel_rank0 = cv.take<long long>((size_t)N);
+  float* X32 = cv.take<float>((size_t)N * D);              // fp32 prefilter copy
+  double* Mx = cv.take<double>(1);                          // max |X|
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
+  ABC_HIP(hipMemsetAsync(Mx, 0, sizeof(double), s));
+  {
+    const int64_t nx = N * D;
+    const int64_t pb = ceil_div(nx, 256) < 512 ? ceil_div(nx, 256) : 512;
+    hipLaunchKernelGGL(local_prep_kernel, dim3((unsigned)pb), dim3(256), 0, s, X, nx, X32,
+                       reinterpret_cast<unsigned long long*>(Mx));
+    ABC_LAUNCHED();
+  }
   if (N > 1) {
     hipLaunchKernelGGL((local_select_kernel<D, sel_pb<D>()>), dim3((unsigned)ceil_div(N, sel_pb<D>())),
                        dim3(256), 0, s, X, N, nq, sel_v, sel_ties, sel_rank0);
@@ -631,7 +739,7 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   double* part = cv.take<double>((size_t)RS * NM * (size_t)N);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
   if (N > 1) {
-    launch_moments<D, 0>(X, w, N, sel_v, sel_ties, sel_rank0, part, RS, s);
+    launch_moments<D, 0>(X, X32, Mx, w, N, sel_v, sel_ties, sel_rank0, part, RS, s);
     ABC_LAUNCHED();
   }
   hipLaunchKernelGGL((local_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256),
@@ -898,6 +1006,8 @@ using namespace abc;
 extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
   size_t off = 0;
   for (int i = 0; i < 3; ++i) size_only<int64_t>(off, (size_t)(N > 0 ? N : 1));
+  size_only<float>(off, (size_t)(N > 0 ? N : 1) * (size_t)d);   // X32
+  size_only<double>(off, 1);                                     // max |X|
   // partial moments of the row chunks (local_moments_kernel)
   const size_t nm = 2 + (size_t)d + (size_t)d * (d + 1) / 2;
   size_only<double>(off, (size_t)moments_chunks(N > 1 ? N : 1) * nm * (size_t)(N > 0 ? N : 1));
