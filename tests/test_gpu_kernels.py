@@ -254,6 +254,26 @@ def test_local_fit_selection_paths_vs_oracle(dev, grid, N, d, k):
     np.testing.assert_allclose(dets.cpu().numpy(), ref["dets"], rtol=1e-8)
 
 
+@pytest.mark.parametrize("offset,spread,k", [(1e3, 0.01, 50), (1e3, 0.01, 700),
+                                             (-3e5, 1.0, 50), (0.0, 1e-6, 50)])
+def test_local_fit_fp32_prefilter_stress(dev, offset, spread, k):
+    """The moments sweep decides membership in fp32 where a rigorous bound
+    allows it (abc_local.hip f32_bound).  Populations far from the origin
+    relative to their spread (fp32 keeps ~1e-3 of the distances' bits, so
+    most pairs fall between the cuts) and tiny spreads must still give the
+    oracle's exact neighbourhoods."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(int(abs(offset)) + k)
+    N, d = 4000, 5
+    X = offset + spread * rng.normal(size=(N, d))
+    w = np.exp(0.3 * rng.standard_normal(N))
+    w /= w.sum()
+    ref = oracle.local_fit(X, w, k=k, k_fraction=None)
+    covs, inv, dets, chol, lnorm = gpu.local_fit(gpu.as_dev(X), gpu.as_dev(w), k, 1.0, 1e-3)
+    np.testing.assert_allclose(covs.cpu().numpy(), ref["covs"], rtol=1e-8,
+                               atol=1e-12 * spread ** 2)
+
+
 @pytest.mark.parametrize("d,N,M,offset", [(5, 3001, 777, 0.0), (2, 17, 5, 40.0),
                                             (8, 1000, 130, 5.0), (1, 64, 64, 0.0),
                                             (10, 700, 130, 2.0), (13, 333, 65, 1.0),
