@@ -49,8 +49,10 @@ __device__ __forceinline__ double dist2(const double* __restrict__ X, int64_t j,
 // dist2v) with the particle's k-th key v*.  The same chain in fp32 on fp32
 // copies of X, s32, decides most comparisons at twice the fp64 rate (k = 50
 // at c5: 7.1 -> 3.3 ms; in the selection sweeps the extra registers cost
-// more occupancy than the fp32 arithmetic saved, 15.9 -> 31.5 ms, so they
-// stay fp64): with u = 2^-24, M = max |x| over the population and the exact
+// more occupancy and branching than the fp32 arithmetic saved: 15.9 ms
+// fp64 vs 31.1 ms prefiltered with 8 particles per block, 23.5 ms with 4,
+// so they stay fp64): with u = 2^-24, M = max |x| over the population and
+// the exact
 // s (and every fp32/fp64 rounding of the copies, the differences and the
 // fma chain accounted for)
 //   |s32 - s64| <= B(s) = 1.01 (4 u M sqrt(D s) + (D + 2) u s
