@@ -581,13 +581,14 @@ __device__ __forceinline__ double lg_stat(double a, double sigma, double th_src,
 // fold them into the p-norm state s in k order; x (nullable) receives the
 // row.  Statistic k uses normal k of the candidate's simulation stream (slot
 // SLOT_SIM + k/4).  theta_{src_k} is read from tsrc[src_k * tstride] (a
-// theta row in memory; sim_pnorm_regs below for theta in registers).
+// theta row in memory; sim_pnorm_regs below for theta in registers); x[k -
+// xoff] receives statistic k.
 template <int PK = 0>
 __device__ __forceinline__ double sim_pnorm_range(const SimDistArgs& M, const BlockConsts& C,
                                                   const double* tsrc, int tstride,
                                                   uint64_t g, uint32_t gen,
                                                   uint64_t seed, int q0, int q1,
-                                                  double s, double* x) {
+                                                  double s, double* x, int xoff = 0) {
   u32x4 r;
   if (q0 < q1 && (q0 & 3)) r = philox(g, SLOT_SIM + (uint32_t)(q0 >> 2), gen, seed);
 #pragma unroll 1
@@ -601,7 +602,7 @@ __device__ __forceinline__ double sim_pnorm_range(const SimDistArgs& M, const Bl
       if (k < q1) {
         const double2 as = C.as[k], wx = C.wx[k];
         const double xv = lg_stat(as.x, as.y, tsrc[C.src[k] * tstride], n2[t]);
-        if (x) x[k] = xv;
+        if (x) x[k - xoff] = xv;
         s = pnorm_acc<PK>(s, fabs(wx.x * (xv - wx.y)), M.p);
       }
     }
@@ -617,7 +618,7 @@ template <int D, int PK = 0>
 __device__ __forceinline__ double sim_pnorm_regs(const SimDistArgs& M, const BlockConsts& C,
                                                  const double (&th)[D], uint64_t g,
                                                  uint32_t gen, uint64_t seed, int q0, int q1,
-                                                 double s, double* x) {
+                                                 double s, double* x, int xoff = 0) {
   u32x4 r;
   if (q0 < q1 && (q0 & 3)) r = philox(g, SLOT_SIM + (uint32_t)(q0 >> 2), gen, seed);
 #pragma unroll 1
@@ -632,7 +633,7 @@ __device__ __forceinline__ double sim_pnorm_regs(const SimDistArgs& M, const Blo
         const double2 as = C.as[k], wx = C.wx[k];
         const int sk = __builtin_amdgcn_readfirstlane(C.src[k]);
         const double xv = lg_stat(as.x, as.y, th[sk], n2[t]);
-        if (x) x[k] = xv;
+        if (x) x[k - xoff] = xv;
         s = pnorm_acc<PK>(s, fabs(wx.x * (xv - wx.y)), M.p);
       }
     }

@@ -59,6 +59,49 @@ __device__ __forceinline__ double evaluate_full(const RoundArgs& A, const BlockC
   return att <= A.P.max_attempts ? dist : INFINITY;
 }
 
+// Rows written through LDS: one group = FR_T candidates (one per thread)
+// whose sum-stat rows are out[0 .. nvalid) (S doubles each, consecutive).
+// Each chunk of XCH statistics goes to an LDS tile [FR_T][XCH + 1] and then
+// leaves the block as row segments, XCH consecutive doubles per row, instead
+// of one 8-byte store per thread and statistic into FR_T different rows.
+// The p-norm state runs through the chunks in k order (the same bits as one
+// pass).  Used by the regeneration of kept rows (c4, S = 256: 565 -> 480 us
+// per call); in the round's record_rejected path the barriers and the LDS
+// cost more than the stores save (1.03 -> 1.59 ms per round at c4).
+// Every thread of the block calls it (barriers inside); `valid` false only
+// keeps the thread in step.  Returns the distance as evaluate_full.
+constexpr int XCH = 16;  // multiple of 4: chunks start on a Philox slot
+template <int D, int MODE, int PK>
+__device__ __forceinline__ double evaluate_staged(const RoundArgs& A, const BlockConsts& C,
+                                                  uint64_t g, bool valid, double* th,
+                                                  int64_t& j, int& att, double* out,
+                                                  int nvalid, double (*stage)[XCH + 1]) {
+  const int t = threadIdx.x;
+  const int S = A.M.S;
+  att = valid ? propose_one<D, MODE, true>(A.P, C, g, th, j) : A.P.max_attempts + 1;
+  double s = 0.0;
+  for (int k0 = 0; k0 < S; k0 += XCH) {
+    const int k1 = k0 + XCH < S ? k0 + XCH : S;
+    if (valid) {
+      if constexpr (D > 0) {
+        s = sim_pnorm_regs<D, PK>(A.M, C, *reinterpret_cast<const double(*)[D]>(th), g,
+                                  A.P.gen, A.P.seed, k0, k1, s, stage[t], k0);
+      } else {
+        s = sim_pnorm_range<PK>(A.M, C, th, 1, g, A.P.gen, A.P.seed, k0, k1, s, stage[t], k0);
+      }
+    }
+    __syncthreads();
+    const int w = k1 - k0;
+    for (int e = t; e < FR_T * w; e += FR_T) {
+      const int r = e / w, c = e - r * w;
+      if (r < nvalid) out[(int64_t)r * S + k0 + c] = stage[r][c];
+    }
+    __syncthreads();
+  }
+  const double dist = pnorm_finish<PK>(s, A.M.p);
+  return att <= A.P.max_attempts ? dist : INFINITY;
+}
+
 template <int D, int MODE, bool FILTER, int PK>
 __device__ __forceinline__ void round_body(
     RoundArgs A, int64_t idx0, int64_t B, double eps,
@@ -165,18 +208,18 @@ __device__ __forceinline__ void round_body(
 // the plain and the early-reject round as separate kernels (a runtime
 // switch would give both the register allocation of the larger one), each
 // for p == 2 and for any p (pnorm_acc)
-#define ABC_ROUND_KERNEL(NAME, FILTER, PK)                                            \
+#define ABC_ROUND_KERNEL(NAME, FILTER, PK, REC)                                       \
   template <int D, int MODE>                                                          \
   __global__ __launch_bounds__(FR_T) void NAME(RoundArgs A, int64_t idx0, int64_t B,  \
                                                double eps, uint64_t* bits,            \
                                                int64_t* tile_cnt, double* rec_x) {    \
     round_body<D, MODE, FILTER, PK>(A, idx0, B, eps, bits, tile_cnt,                  \
-                                    FILTER ? nullptr : rec_x);                        \
+                                    REC ? rec_x : nullptr);                           \
   }
-ABC_ROUND_KERNEL(fused_round_plain, false, 0)
-ABC_ROUND_KERNEL(fused_round_plain_p2, false, 2)
-ABC_ROUND_KERNEL(fused_round_filter, true, 0)
-ABC_ROUND_KERNEL(fused_round_filter_p2, true, 2)
+ABC_ROUND_KERNEL(fused_round_plain, false, 0, true)
+ABC_ROUND_KERNEL(fused_round_plain_p2, false, 2, true)
+ABC_ROUND_KERNEL(fused_round_filter, true, 0, false)
+ABC_ROUND_KERNEL(fused_round_filter_p2, true, 2, false)
 #undef ABC_ROUND_KERNEL
 
 __global__ void support_box_kernel(const int32_t* __restrict__ kind,
@@ -288,15 +331,20 @@ __global__ __launch_bounds__(256) void fused_regen_kernel(
     double* __restrict__ x, double* __restrict__ dist) {
   constexpr int DM = D > 0 ? D : 64;
   __shared__ BlockConsts C;
+  __shared__ double stage[FR_T][XCH + 1];
   stage_block_consts<D, MODE>(C, A.P, &A.M, nullptr);
   const int d = D > 0 ? D : A.P.d;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  const int64_t i0 = (int64_t)blockIdx.x * FR_T;
+  const int64_t i = i0 + threadIdx.x;
+  const bool valid = i < n;
+  const int nvalid = n - i0 < FR_T ? (int)(n - i0) : FR_T;
   double th[DM];
-  int64_t j;
+  int64_t j = -1;
   int att;
-  const double dd = evaluate_full<D, MODE, 0>(A, C, (uint64_t)(idx0 + idx[i]), th, j, att,
-                                          x + i * A.M.S);
+  // the kept rows x[i] (consecutive) leave through LDS (evaluate_staged)
+  const double dd = evaluate_staged<D, MODE, 0>(A, C, valid ? (uint64_t)(idx0 + idx[i]) : 0ull,
+                                                valid, th, j, att, x + i0 * A.M.S, nvalid, stage);
+  if (!valid) return;
 #pragma unroll
   for (int k = 0; k < (D > 0 ? D : d); ++k) theta[i * d + k] = th[k];
   lp[i] = att <= A.P.max_attempts ? prior_logpdf(A.P.kind, A.P.params, d, th) : -INFINITY;

@@ -185,33 +185,30 @@ class AdaptivePNormDistance(PNormDistance):
         return np.asarray(scales, dtype=np.float64)
 
     def _update(self, t, all_sum_stats):
+        # distance.py:263-348 with the per-key loops as array operations (the
+        # same IEEE operations per key: 1 / scale, / mean, the ratio bound;
+        # ~1 ms of host time per generation at S = 256 otherwise)
         keys = list(self.x_0.keys())
-        scales = self._scales(all_sum_stats, keys)
-        w = {}
-        for key, scale in zip(keys, scales):
-            w[key] = 0 if np.isclose(scale, 0) else 1 / scale
+        scales = np.asarray(self._scales(all_sum_stats, keys), dtype=np.float64)
+        zero = np.isclose(scales, 0)
+        with np.errstate(divide="ignore"):
+            w = np.where(zero, 0.0, 1.0 / np.where(zero, 1.0, scales))
         w = self._normalize_weights(w)
         w = self._bound_weights(w)
-        self.weights[t] = w
+        self.weights[t] = dict(zip(keys, w.tolist()))
         self.log(t)
 
     def _normalize_weights(self, w):
         if not self.normalize_weights:
             return w
-        mean_weight = np.mean(list(w.values()))
-        for key in w:
-            w[key] /= mean_weight
-        return w
+        return w / np.mean(w)
 
     def _bound_weights(self, w):
         if self.max_weight_ratio is None:
             return w
-        w_arr = np.array(list(w.values()))
-        min_abs_weight = np.min(np.abs(w_arr[w_arr != 0]))
-        for key, value in w.items():
-            if abs(value) / min_abs_weight > self.max_weight_ratio:
-                w[key] = np.sign(value) * self.max_weight_ratio * min_abs_weight
-        return w
+        min_abs_weight = np.min(np.abs(w[w != 0]))
+        over = np.abs(w) / min_abs_weight > self.max_weight_ratio
+        return np.where(over, np.sign(w) * self.max_weight_ratio * min_abs_weight, w)
 
     def get_config(self) -> dict:
         return {"name": self.__class__.__name__, "p": self.p,

@@ -333,17 +333,25 @@ class CandidateRound:
                  p(ws), ws.numel(), stream_ptr())
         return idx, cnt
 
-    def regen(self, idx0, idx):
+    def regen(self, idx0, idx, out=None):
         """Rows of the candidates idx0 + idx[i] (abc_candidates_regen):
-        theta [n, d], prior log-density [n], ancestor [n], x [n, S], dist [n]."""
+        theta [n, d], prior log-density [n], ancestor [n], x [n, S], dist [n];
+        out: these five tensors (contiguous) to write into."""
         import ctypes as C
         n = int(idx.numel())
         dev = self.device
-        theta = torch.empty((n, self.d), dtype=F64, device=dev)
-        lp = torch.empty(n, dtype=F64, device=dev)
-        anc = torch.empty(n, dtype=I64, device=dev)
-        x = torch.empty((n, self.S), dtype=F64, device=dev)
-        dist = torch.empty(n, dtype=F64, device=dev)
+        if out is not None:
+            theta, lp, anc, x, dist = out
+            if not (tuple(theta.shape) == (n, self.d) and lp.numel() == n and anc.numel() == n
+                    and tuple(x.shape) == (n, self.S) and dist.numel() == n
+                    and anc.dtype == I64 and all(t.is_contiguous() for t in out)):
+                raise ValueError("CandidateRound.regen: out does not match the rows")
+        else:
+            theta = torch.empty((n, self.d), dtype=F64, device=dev)
+            lp = torch.empty(n, dtype=F64, device=dev)
+            anc = torch.empty(n, dtype=I64, device=dev)
+            x = torch.empty((n, self.S), dtype=F64, device=dev)
+            dist = torch.empty(n, dtype=F64, device=dev)
         if n:
             nat.call("abc_candidates_regen", C.addressof(self.spec), int(idx0),
                      p(idx.contiguous()), n, p(theta), p(lp), p(anc), p(x), p(dist),

@@ -412,6 +412,8 @@ class BatchedGPUSampler(Sampler):
         S = len(spec.sum_stat_keys)
         cols = {k: [] for k in ("theta", "lp", "dist", "x", "anc")}
         rec_x, rec_keeps, keeps = [], [], []
+        arena, arena_off = None, 0
+        kept, kept_off = None, 0
         rec_left = self._record_limit(S)
         n_acc = n_eval = base = rounds = 0
         ok = True
@@ -426,8 +428,15 @@ class BatchedGPUSampler(Sampler):
             B = self._limit_to_max_eval(self._fused_size(need, ws, rate, measured, S, record),
                                         max_eval, n_eval, ws)
             lo, _ = dd.rank_range(base, B, rank)
-            rx = (torch.empty((B, S), dtype=gpu.F64, device=dev)
-                  if record and rec_left > 0 else None)
+            rx = None
+            if record and rec_left > 0:
+                # recorded rows of consecutive rounds land back to back in one
+                # arena (the next round starts after the rows this one keeps),
+                # so the generation's matrix is a view, not a concatenation
+                if arena is None or arena_off + B > arena.shape[0]:
+                    arena = torch.empty((int(B * 1.25) + 4096, S), dtype=gpu.F64, device=dev)
+                    arena_off = 0
+                rx = arena[arena_off:arena_off + B]
             filt = (rate is not None and rate < self.filter_below and rx is None
                     and self._lazy_capable(spec, fr))
             filtered += int(filt)
@@ -457,7 +466,19 @@ class BatchedGPUSampler(Sampler):
             else:
                 evaluated = ws * B
             if k_mine:
-                th, lp, anc, x, dist = fr.regen(lo, idx[:k_mine])
+                # kept rows regenerated straight into one per-generation
+                # buffer (rows of later rounds follow): no concatenation
+                if kept is None or kept_off + k_mine > kept[0].shape[0]:
+                    cap = max(n - n_acc, k_mine)
+                    kept = (torch.empty((cap, fr.d), dtype=gpu.F64, device=dev),
+                            torch.empty(cap, dtype=gpu.F64, device=dev),
+                            torch.empty(cap, dtype=torch.int64, device=dev),
+                            torch.empty((cap, S), dtype=gpu.F64, device=dev),
+                            torch.empty(cap, dtype=gpu.F64, device=dev))
+                    kept_off = 0
+                th, lp, anc, x, dist = fr.regen(
+                    lo, idx[:k_mine], out=tuple(a[kept_off:kept_off + k_mine] for a in kept))
+                kept_off += k_mine
                 for k, v in zip(("theta", "lp", "dist", "x", "anc"),
                                 (th, lp, dist, x, anc)):
                     cols[k].append(v)
@@ -467,7 +488,8 @@ class BatchedGPUSampler(Sampler):
                 rec_all, rec_left = self._cap_records(rec_all, rec_left)
                 rr = int(rec_all[rank])
                 if rx is not None:
-                    rec_x.append(rx[:rr].clone() if rr < B // 2 else rx[:rr])
+                    rec_x.append(rx[:rr])
+                    arena_off += rr
                 rec_keeps.append(rec_all)
             keeps.append(keep)
             n_acc += total_keep
@@ -502,10 +524,26 @@ class BatchedGPUSampler(Sampler):
         all-gather them back into global candidate-index order."""
         if not pieces:
             return None
-        out = gpu.torch.cat(pieces, 0) if len(pieces) > 1 else pieces[0]
+        out = pieces[0] if len(pieces) == 1 else self._join_rows(pieces)
         if ws > 1:
             out = dd.allgather_rows_ordered([out.contiguous()], rec_keeps, dev)[0]
         return out.contiguous()
+
+    @staticmethod
+    def _join_rows(pieces):
+        """Row blocks -> one [sum rows x S] tensor: a view when they lie back
+        to back in one buffer (the fused rounds' record arena), else a copy."""
+        torch = gpu.torch
+        a = pieces[0]
+        adjacent = all(
+            p.dim() == 2 and p.is_contiguous() and p.shape[1] == a.shape[1]
+            and p.untyped_storage().data_ptr() == a.untyped_storage().data_ptr()
+            and p.data_ptr() == q.data_ptr() + q.numel() * q.element_size()
+            for q, p in zip(pieces[:-1], pieces[1:]))
+        if adjacent and a.is_contiguous():
+            n = sum(p.shape[0] for p in pieces)
+            return a.as_strided((n, a.shape[1]), a.stride())
+        return torch.cat(pieces, 0)
 
     @staticmethod
     def _local_cutoff_pos(idx, k):
@@ -567,7 +605,11 @@ class BatchedGPUSampler(Sampler):
         rank, ws = dd.world()
         torch = gpu.torch
         def cat(lst):
-            return lst[0] if len(lst) == 1 else torch.cat(lst, 0)
+            if len(lst) == 1:
+                return lst[0]
+            if lst[0].dim() == 2:
+                return self._join_rows(lst)
+            return self._join_rows([t.view(-1, 1) for t in lst]).view(-1)
         if acc_theta:
             theta, lp, dist, x = cat(acc_theta), cat(acc_lp), cat(acc_d), cat(acc_x)
         else:

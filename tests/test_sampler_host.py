@@ -53,3 +53,18 @@ def test_fused_round_sizing():
     assert s._fused_size(10 ** 9, 1, 1e-6, True, 10, False) == s.max_fused_batch_size
     # record_rejected: rows of S doubles within record_budget_bytes
     assert s._fused_size(10 ** 6, 1, 1e-3, True, 256, True) == s.record_budget_bytes // (8 * 256)
+
+
+def test_join_rows_view_or_copy():
+    """Recorded rows of consecutive fused rounds sit back to back in one
+    arena: joined as a view (no copy); anything else is concatenated."""
+    torch = pytest.importorskip("torch")
+    arena = torch.arange(60, dtype=torch.float64).reshape(20, 3)
+    a, b, c = arena[0:5], arena[5:12], arena[12:13]
+    j = BatchedGPUSampler._join_rows([a, b, c])
+    assert j.data_ptr() == arena.data_ptr() and torch.equal(j, arena[:13])
+    gap = BatchedGPUSampler._join_rows([arena[0:5], arena[6:8]])
+    assert gap.data_ptr() != arena.data_ptr()
+    assert torch.equal(gap, torch.cat([arena[0:5], arena[6:8]]))
+    other = torch.zeros(2, 3, dtype=torch.float64)
+    assert torch.equal(BatchedGPUSampler._join_rows([a, other]), torch.cat([a, other]))
