@@ -307,7 +307,13 @@ def e2e(reps):
     import time
     import torch
     import pyabc_amd as pa
-    # c1
+    # c1 (after one untimed run: the first kernel launches of a process load
+    # libabcgpu's code objects, a one-time cost of ~0.1 s)
+    w = pa.ABCSMC(pa.LinearGaussianModel(["x"], ["y"], src=[0], sigma=[0.5]),
+                  pa.Distribution(x=pa.RV("norm", 0, 1)), pa.PNormDistance(),
+                  population_size=1000, sampler=pa.BatchedGPUSampler(seed=9))
+    w.new("sqlite://", {"y": 2.0})
+    w.run(max_nr_populations=2)
     np.random.seed(0)
     abc = pa.ABCSMC(pa.LinearGaussianModel(["x"], ["y"], src=[0], sigma=[0.5]),
                     pa.Distribution(x=pa.RV("norm", 0, 1)), pa.PNormDistance(),
