@@ -272,8 +272,19 @@ __device__ __forceinline__ double dval(uint64_t k) {
   const uint64_t u = (k >> 63) ? (k & ~(1ull << 63)) : ~k;
   return __longlong_as_double((long long)u);
 }
-__device__ __forceinline__ void support_bounds(int kind, const double* p, double* lo_hi) {
-  double c;  // a point inside the support
+// The bisection runs with the 64 lanes of a wave probing together: each
+// step evaluates the predicate at 64 evenly spaced keys of the open bracket
+// and keeps the sub-bracket where it turns (the predicate is monotone in
+// the key on each side of an interior point c), so a 64-bit bracket closes
+// in ~11 steps instead of ~63 dependent ones.  Every lane of the wave must
+// call it (uniform arguments); lane 0 writes lo_hi = [lowest, highest
+// member] (inf, -inf for an empty support).
+__device__ __forceinline__ void support_bounds_wave(int kind, const double* pg, double* lo_hi) {
+  const int lane = threadIdx.x & 63;
+  double p[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) p[i] = pg[i];
+  double c;
   switch (kind) {
     case ABC_PRIOR_UNIFORM: c = p[0] + 0.5 * p[1]; break;
     case ABC_PRIOR_EXPON: c = p[0] + p[1]; break;
@@ -282,35 +293,40 @@ __device__ __forceinline__ void support_bounds(int kind, const double* p, double
     case ABC_PRIOR_NORM: case ABC_PRIOR_LAPLACE: c = p[0]; break;
     default: c = 0.0;
   }
-  if (!prior_in_support1(kind, p, c)) {  // empty (degenerate parameters)
-    lo_hi[0] = INFINITY;
-    lo_hi[1] = -INFINITY;
+  if (!prior_in_support1(kind, p, c)) {
+    if (lane == 0) { lo_hi[0] = INFINITY; lo_hi[1] = -INFINITY; }
     return;
   }
+  // first key in (lo, hi] where pred(key) == up (pred(lo) != up, pred(hi) == up)
+  auto turn = [&](uint64_t lo, uint64_t hi, bool up) {
+    while (hi - lo > 1) {
+      const uint64_t span = hi - lo;            // > 1
+      const uint64_t step = span / 65 > 0 ? span / 65 : 1;
+      const uint64_t m = lo + step * (uint64_t)(lane + 1);
+      const bool inside = m < hi;
+      const bool pr = inside ? (prior_in_support1(kind, p, dval(m)) == up) : true;
+      const unsigned long long bal = __ballot(pr);   // lanes past hi count as "turned"
+      if (bal == 0ull) {                             // the turn lies past the last probe
+        lo = lo + step * 64ull;
+        continue;
+      }
+      const int f = __ffsll((long long)bal) - 1;     // first turned probe (or a pad)
+      const uint64_t mf = lo + step * (uint64_t)(f + 1);
+      const uint64_t new_hi = mf < hi ? mf : hi;
+      const uint64_t new_lo = f == 0 ? lo : lo + step * (uint64_t)f;
+      lo = new_lo;
+      hi = new_hi;
+    }
+    return hi;
+  };
   const uint64_t kc = dkey(c);
-  // lowest member: P(hi) true, P(lo) false
-  uint64_t lo = dkey(-INFINITY), hi = kc;
-  if (prior_in_support1(kind, p, -INFINITY)) {
-    hi = lo;
-  } else {
-    while (hi - lo > 1) {
-      const uint64_t m = lo + (hi - lo) / 2;
-      if (prior_in_support1(kind, p, dval(m))) hi = m; else lo = m;
-    }
-  }
-  lo_hi[0] = dval(hi);
-  // highest member: P(lo) true, P(hi) false
-  lo = kc;
-  hi = dkey(INFINITY);
-  if (prior_in_support1(kind, p, INFINITY)) {
-    lo = hi;
-  } else {
-    while (hi - lo > 1) {
-      const uint64_t m = lo + (hi - lo) / 2;
-      if (prior_in_support1(kind, p, dval(m))) lo = m; else hi = m;
-    }
-  }
-  lo_hi[1] = dval(lo);
+  uint64_t lo_key;
+  if (prior_in_support1(kind, p, -INFINITY)) lo_key = dkey(-INFINITY);
+  else lo_key = turn(dkey(-INFINITY), kc, true);       // lowest member
+  uint64_t hi_key;
+  if (prior_in_support1(kind, p, INFINITY)) hi_key = dkey(INFINITY);
+  else hi_key = turn(kc, dkey(INFINITY), false) - 1;   // one below the first non-member
+  if (lane == 0) { lo_hi[0] = dval(lo_key); lo_hi[1] = dval(hi_key); }
 }
 
 // ---- one proposal ----------------------------------------------------------
@@ -399,7 +415,7 @@ struct BlockConsts {
 
 // Fill C (every thread of the block calls it; synchronises).  BOX_FROM_SRC:
 // copy the precomputed support box box_src, else bisect here
-// (support_bounds).
+// (support_bounds_wave; the block size is a multiple of 64).
 template <int D, int MODE, bool BOX_FROM_SRC = false>
 __device__ __forceinline__ void stage_block_consts(BlockConsts& C, const ProposalArgs& A,
                                                    const SimDistArgs* M,
@@ -411,8 +427,10 @@ __device__ __forceinline__ void stage_block_consts(BlockConsts& C, const Proposa
     for (int e = t; e < d * d; e += nt) C.LT[(e % d) * d + e / d] = A.L[e];
   if (BOX_FROM_SRC) {
     for (int k = t; k < 2 * d; k += nt) C.box[k] = box_src[k];
-  } else if (t < d) {
-    support_bounds(A.kind[t], A.params + 4 * t, C.box + 2 * t);
+  } else {
+    // one wave per dimension (support_bounds_wave)
+    for (int k = t >> 6; k < d; k += nt >> 6)
+      support_bounds_wave(A.kind[k], A.params + 4 * k, C.box + 2 * k);
   }
   if (M)
     for (int k = t; k < M->S && k < SIM_SMAX; k += nt) {

@@ -222,11 +222,13 @@ ABC_ROUND_KERNEL(fused_round_filter, true, 0, false)
 ABC_ROUND_KERNEL(fused_round_filter_p2, true, 2, false)
 #undef ABC_ROUND_KERNEL
 
-__global__ void support_box_kernel(const int32_t* __restrict__ kind,
-                                   const double* __restrict__ params, int d,
-                                   double* __restrict__ box) {
-  const int k = threadIdx.x;
-  if (k < d) support_bounds(kind[k], params + 4 * k, box + 2 * k);
+// one wave per dimension (support_bounds_wave): ~1 us instead of the ~40 us
+// of one thread's 126 dependent bisection steps
+__global__ __launch_bounds__(64) void support_box_kernel(const int32_t* __restrict__ kind,
+                                                         const double* __restrict__ params,
+                                                         int d, double* __restrict__ box) {
+  const int k = blockIdx.x;
+  if (k < d) support_bounds_wave(kind[k], params + 4 * k, box + 2 * k);
 }
 
 // ---- order-preserving compaction of the accept bits -----------------------
@@ -560,8 +562,8 @@ extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0
   double* box = c.take<double>(128);
   int64_t* bsum = c.take<int64_t>((size_t)ceil_div(nt, SC_N));
   if (!c.ok) return set_error(ABC_ERR_WORKSPACE, "candidates_round: workspace");
-  hipLaunchKernelGGL(support_box_kernel, dim3(1), dim3(64), 0, s, spec->prior_kind,
-                     spec->prior_params, spec->d, box);
+  hipLaunchKernelGGL(support_box_kernel, dim3((unsigned)spec->d), dim3(64), 0, s,
+                     spec->prior_kind, spec->prior_params, spec->d, box);
   ABC_LAUNCHED();
   const RoundArgs A = round_args(spec, box);
   ABC_CHECK_ARG(nt < (1ll << 31), "candidates_round: too many tiles");
