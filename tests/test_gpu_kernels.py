@@ -231,13 +231,16 @@ def gpu_as(a, dev):
                                          (None, 12000, 5, 3000), (None, 4096, 2, 10),
                                          (3, 5000, 4, 200), (None, 3000, 10, 50),
                                          (None, 2500, 16, 300), (3, 3000, 9, 100),
-                                         (None, 9000, 13, 2500)])
+                                         (None, 9000, 13, 2500), (2, 1500, 3, 400),
+                                         (3, 3000, 4, 1000), (None, 2048, 1, 600),
+                                         (None, 1000, 8, 999), (None, 70, 6, 20)])
 def test_local_fit_selection_paths_vs_oracle(dev, grid, N, d, k):
     """k-NN selection: the sample-bracketed path (N >= 2048), the LDS bucket
     path (small and large k) and the radix-pass fallback (a {0,1}^3 grid: buckets of hundreds of exact ties,
     taken by index) against the oracle's (distance, index) order.  d = 9..16
     run the 4-particle selection blocks and the sliced moments (several
-    kernels over one moment list each)."""
+    kernels over one moment list each).  k > N / 16 takes the moments GEMM
+    (local_moments_mfma_kernel), including grids of ties and k = N - 1."""
     from pyabc_amd import gpu
     rng = np.random.default_rng(N + k)
     if grid is None:
