@@ -302,7 +302,7 @@ def main():
     avg_ms = k_ms / k_n if k_n else float("nan")
     achieved = k_flops / (k_ms * 1e-3) / 1e12 if k_n else float("nan")
     peak = F64_MFMA_PEAK_TFLOPS if args.precision == "f64" else F32_MFMA_PEAK_TFLOPS
-    kpad = {"x3": 32 * (math.ceil((args.dim + 4) / 32)
+    kpad = {"x3": 32 * (math.ceil((args.dim + 7) / 32)
                         + math.ceil((5 * args.dim + 4) / 32)),
             "f64": 4 * math.ceil((args.dim + 1) / 4),
             "f32": 4 * math.ceil((args.dim + 1) / 4)}[args.precision]
@@ -395,7 +395,12 @@ def main():
                          "flop_per_pair": 2 * args.dim,
                          "note": ("achieved = algorithmic 2*d FLOP per (candidate, "
                                   "population) pair / HIP-event time of the GEMM "
-                                  "launch; peak = fp32 MFMA (x3/f32) or fp64 MFMA"),
+                                  "launch; peak = fp32 MFMA (x3/f32) or fp64 MFMA. "
+                                  "x3 runs f16 MFMA on 3-limb operands, so frac can "
+                                  "exceed 1 (fp32-grade results above the fp32 MFMA "
+                                  "roofline); its own bound is the MFMA + exp2 + add "
+                                  "issue rate per 16x16 tile, and executed_frac is "
+                                  "the f16 MFMA pipe's share"),
                          "pairs_per_s": k_pairs / (k_ms * 1e-3) if k_n else None,
                          "executed_mfma_tflops": executed,
                          "executed_mfma_peak": exec_peak,
