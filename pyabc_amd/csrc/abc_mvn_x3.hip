@@ -59,7 +59,6 @@ namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr double LOG2E = 1.4426950408889634074;
 constexpr double SQRT_LOG2E = 1.2011224087864498;  // sqrt(log2 e)
@@ -391,13 +390,10 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
   // population fragments (prefetch distance 2).  Work runs as a stream of
   // (tile, c) units: the MFMA chain of unit u is issued next to the
   // exp2/sum of unit u-1, so one wave keeps the MFMA and VALU pipes busy.
-  // per-lane f32 partial sums as pairs: the four exp2 of a tile enter with
-  // two packed adds (v_pk_add_f32) instead of four scalar ones -- the loop
-  // is issue-bound (MFMA + exp2 + adds), so this is 8 of its 72 cycles
   double l64[CT];
-  f32x2 ls[CT];
+  float ls[CT];
 #pragma unroll
-  for (int c = 0; c < CT; ++c) { l64[c] = 0.0; ls[c] = f32x2{0.f, 0.f}; }
+  for (int c = 0; c < CT; ++c) { l64[c] = 0.0; ls[c] = 0.f; }
   half8 a0[KB], a1[KB];
   if (t_begin < t_end) {
 #pragma unroll
@@ -413,9 +409,9 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
       r = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[kb], b[c][kb], r, 0, 0, 0);
     return r;
   };
-  auto expsum = [&](f32x2& acc, const f32x4& v) {
-    acc += f32x2{__builtin_amdgcn_exp2f(v[0]), __builtin_amdgcn_exp2f(v[1])};
-    acc += f32x2{__builtin_amdgcn_exp2f(v[2]), __builtin_amdgcn_exp2f(v[3])};
+  auto expsum = [&](const f32x4& v) {
+    return (__builtin_amdgcn_exp2f(v[0]) + __builtin_amdgcn_exp2f(v[1])) +
+           (__builtin_amdgcn_exp2f(v[2]) + __builtin_amdgcn_exp2f(v[3]));
   };
   // one tile: units (t, 0..CT-1); the exp2/sum of unit c - 1 is issued under
   // the MFMA chain of unit c.  Every candidate slot c sums the same tiles in
@@ -426,10 +422,10 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
 #pragma unroll
     for (int c = 1; c < CT; ++c) {
       const f32x4 cur = chain(a, c);
-      expsum(ls[c - 1], prev);
+      ls[c - 1] += expsum(prev);
       prev = cur;
     }
-    expsum(ls[CT - 1], prev);
+    ls[CT - 1] += expsum(prev);
   };
   int nflush = 0;
   for (int64_t t = t_begin; t < t_end; t += 2) {
@@ -441,19 +437,15 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) a1[kb] = Al[(tile(t + 3) + kb) * 64];
     }
-    // f32 partial sums over at most 16 tiles (32 terms per pair element),
-    // then fp64
+    // f32 partial sums over at most 16 tiles (64 terms per lane), then fp64
     if (++nflush == 8) {
       nflush = 0;
 #pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        l64[c] += (double)ls[c][0] + (double)ls[c][1];
-        ls[c] = f32x2{0.f, 0.f};
-      }
+      for (int c = 0; c < CT; ++c) { l64[c] += (double)ls[c]; ls[c] = 0.f; }
     }
   }
 #pragma unroll
-  for (int c = 0; c < CT; ++c) l64[c] += (double)ls[c][0] + (double)ls[c][1];
+  for (int c = 0; c < CT; ++c) l64[c] += (double)ls[c];
   // lanes l, l^16, l^32, l^48 hold the same candidate column (same o)
 #pragma unroll
   for (int c = 0; c < CT; ++c) {
