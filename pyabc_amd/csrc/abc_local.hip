@@ -698,6 +698,339 @@ inline int moments_chunks(int64_t N) {
   return (int)(rs < 1 ? 1 : rs);
 }
 
+// ---- dense neighbourhoods: the moments on f16 MFMA with exact limbs --------
+// At k a sizeable fraction of N (the default k = N/4) a quarter of all pairs
+// are members and local_moments_kernel runs its fp64 update for every row
+// (some lane of the wave is always a member).  Here the raw sums
+//   S_n,f = sum_j m_nj F_j,f,  F_j = [w, w^2, w Y_a, w Y_a Y_b (a <= b)],
+//   Y = X - X_0,  m the 0/1 membership of local_moments_kernel (same fp32
+//   prefilter and exact fp64 test)
+// are a [particles x rows] x [rows x features] product.  Each feature column
+// f is split into ML_NL = 5 limbs of 11 bits on a block exponent e_f (|F_f| <
+// 2^e_f from the population's max w and max |Y_a|): F = sum_l L_l 2^(e_f -
+// 11 (l + 1)), L_l integers with |L_l| <= 2048, exact f16.  Products m L are
+// exact and f32 sums of at most 8192 of them stay below 2^24, so the MFMA's
+// f32 accumulation is exact; every 256 steps (8192 rows) the sums are added
+// into fp64 partials (integers, exact).  The only rounding is the last
+// limb's (2^(e_f - 56) per term) and the fp64 re-centring at X_n
+// (mm_finish_kernel), whose error bound is checked per particle against the
+// local variance: a particle that fails it sends the whole fit back to the
+// VALU kernel (a device flag read by the host; never seen on the tests'
+// populations).
+#ifndef ABC_LOCAL_MOMENTS_VALU
+#define ABC_LOCAL_MOMENTS_VALU 0   // build-time A/B: 1 keeps the VALU kernel for all k
+#endif
+constexpr int ML_NL = 5;
+template <int D> constexpr int mm_nc() { return local_nm<D>() * ML_NL; }
+template <int D> constexpr int mm_nt() { return (mm_nc<D>() + 15) / 16; }
+constexpr double MM_EPS = 2.220446049250313e-16;  // fp64 epsilon
+constexpr int MM_FLUSH = 256;   // 32-row steps between fp64 flushes (8192 rows)
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// feature f of a row with weight lw and offsets y (local_nm order)
+template <int D>
+__device__ __forceinline__ double mm_feature(int f, double lw, const double (&y)[D]) {
+  if (f == 0) return lw;
+  if (f == 1) return lw * lw;
+  if (f < 2 + D) return lw * y[f - 2];
+  int c = 2 + D;
+#pragma unroll
+  for (int a = 0; a < D; ++a)
+#pragma unroll
+    for (int b = a; b < D; ++b) {
+      if (c == f) return lw * y[a] * y[b];
+      ++c;
+    }
+  return 0.0;
+}
+
+// block exponent of feature f: |F_f| <= bound < 2^e (bnd = [max w, max |Y_a|])
+template <int D>
+__device__ __forceinline__ int mm_fexp(int f, const double* bnd) {
+  double y[D];
+#pragma unroll
+  for (int a = 0; a < D; ++a) y[a] = bnd[1 + a];
+  const double b = mm_feature<D>(f, bnd[0], y);
+  if (!(b > 0.0)) return 0;
+  int e;
+  frexp(b, &e);
+  return e;
+}
+
+// limb l of v on the block exponent e (integer-valued, |.| <= 2048)
+__device__ __forceinline__ double mm_limb(double v, int e, int l) {
+  double r = ldexp(v, 11 - e);
+  double L = rint(r);
+  for (int q = 0; q < l; ++q) {
+    r = ldexp(r - L, 11);
+    L = rint(r);
+  }
+  return L;
+}
+
+// bnd[0] = max w, bnd[1 + a] = max |X_a - X_0a| (bit patterns of non-negative
+// doubles are monotone: atomicMax on them; bnd zeroed by the caller)
+template <int D>
+__global__ __launch_bounds__(256) void mm_bounds_kernel(const double* __restrict__ X,
+                                                        const double* __restrict__ w,
+                                                        int64_t N,
+                                                        unsigned long long* __restrict__ bnd) {
+  double m[1 + D];
+#pragma unroll
+  for (int a = 0; a <= D; ++a) m[a] = 0.0;
+  for (int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x; j < N;
+       j += (int64_t)gridDim.x * 256) {
+    m[0] = fmax(m[0], fabs(w[j]));
+#pragma unroll
+    for (int a = 0; a < D; ++a) m[1 + a] = fmax(m[1 + a], fabs(X[j * D + a] - X[a]));
+  }
+#pragma unroll
+  for (int a = 0; a <= D; ++a) {
+    const double v = wave_max(m[a]);
+    if ((threadIdx.x & 63) == 0 && v > 0.0)
+      atomicMax(bnd + a, (unsigned long long)__double_as_longlong(v));
+  }
+}
+
+// B operand image [step][tile][lane][8 halves]: lane l of tile t holds rows
+// 32 s + 8 (l >> 4) + 0..7 of column 16 t + (l & 15) = f * ML_NL + limb
+template <int D>
+__global__ __launch_bounds__(256) void mm_bimg_kernel(const double* __restrict__ X,
+                                                      const double* __restrict__ w,
+                                                      int64_t N, int64_t nsteps,
+                                                      const double* __restrict__ bnd,
+                                                      half8* __restrict__ img) {
+  constexpr int NT = mm_nt<D>(), NC = mm_nc<D>();
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= nsteps * NT * 64) return;
+  const int lane = (int)(g & 63);
+  const int64_t st = g >> 6;
+  const int t = (int)(st % NT);
+  const int64_t s = st / NT;
+  const int c = 16 * t + (lane & 15);
+  half8 h;
+  if (c >= NC) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) h[u] = (_Float16)0.0f;
+  } else {
+    const int f = c / ML_NL, l = c % ML_NL;
+    const int e = mm_fexp<D>(f, bnd);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t j = 32 * s + 8 * (lane >> 4) + u;
+      double v = 0.0;
+      if (j < N) {
+        double y[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) y[a] = X[j * D + a] - X[a];
+        v = mm_limb(mm_feature<D>(f, w[j], y), e, l);
+      }
+      h[u] = (_Float16)(float)v;
+    }
+  }
+  img[g] = h;
+}
+
+// Block = 8 waves x MM_G particle tiles of 16 (256 particles); a wave's tiles
+// share each B fragment, and the block stages MM_SB steps of the B image and
+// of the rows' fp32 coordinates in LDS (the image is ~14x the bytes of the
+// rows: every particle group re-reads it).  grid (ceil(N / 256), RS row
+// chunks of whole 32-row steps); part [RS][16 NT][N] (exact integer sums).
+constexpr int MM_G = 2, MM_W = 8, MM_SB = 4;
+constexpr int MM_PB = MM_W * MM_G * 16;   // particles per block
+template <int D>
+__global__ __launch_bounds__(512) void mm_moments_kernel(
+    const double* __restrict__ X, const float* __restrict__ X32,
+    const double* __restrict__ Mp, const half8* __restrict__ img, int64_t N,
+    int64_t nsteps, const unsigned long long* __restrict__ sel_v,
+    const long long* __restrict__ sel_jcut, const long long* __restrict__ sel_rank0,
+    double* __restrict__ part) {
+  constexpr int NT = mm_nt<D>(), NCP = 16 * NT;
+  __shared__ half8 bs[MM_SB * NT * 64];
+  __shared__ float xs[MM_SB * 32 * D];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int RS = gridDim.y;
+  const int64_t s0 = (nsteps * (int64_t)blockIdx.y) / RS;
+  const int64_t s1 = (nsteps * ((int64_t)blockIdx.y + 1)) / RS;
+  const int64_t p0 = ((int64_t)blockIdx.x * MM_W + wv) * (MM_G * 16);
+  const int kq = lane >> 4;
+  const double M = *Mp;
+  float xp32[MM_G][D];
+  unsigned long long vs[MM_G];
+  long long jcut[MM_G], r0[MM_G];
+  float cut_in[MM_G], cut_out[MM_G];
+#pragma unroll
+  for (int g = 0; g < MM_G; ++g) {
+    const int64_t pn = p0 + 16 * g + (lane & 15);
+    const int64_t pe = pn < N ? pn : N - 1;
+#pragma unroll
+    for (int q = 0; q < D; ++q) xp32[g][q] = X32[pe * D + q];
+    vs[g] = sel_v[pe];
+    jcut[g] = sel_jcut[pe];
+    r0[g] = sel_rank0[pe];
+    cut_in[g] = f32_cut_below<D>(key_val(vs[g]), M);
+    cut_out[g] = f32_cut_above<D>(key_val(vs[g]), M);
+  }
+  f32x4 acc[MM_G][NT];
+#pragma unroll
+  for (int g = 0; g < MM_G; ++g)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool first = true;
+  int since = 0;
+  auto flush = [&]() {
+#pragma unroll
+    for (int g = 0; g < MM_G; ++g)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int c = 16 * t + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t n = p0 + 16 * g + 4 * kq + r;
+          if (n < N) {
+            double* dst = part + ((int64_t)blockIdx.y * NCP + c) * N + n;
+            *dst = (first ? 0.0 : *dst) + (double)acc[g][t][r];
+          }
+        }
+        acc[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    first = false;
+    since = 0;
+  };
+  for (int64_t sb = s0; sb < s1; sb += MM_SB) {
+    const int nk = (int)((s1 - sb) < MM_SB ? (s1 - sb) : MM_SB);
+    __syncthreads();
+    {
+      const int64_t jb = 32 * sb;
+      const int64_t cnt = ((N - jb) < MM_SB * 32 ? (N - jb) : MM_SB * 32) * D;
+      for (int e = threadIdx.x; e < MM_SB * 32 * D; e += 512)
+        xs[e] = e < cnt ? X32[jb * D + e] : 0.0f;
+      const half8* src = img + sb * NT * 64;
+      for (int e = threadIdx.x; e < nk * NT * 64; e += 512) bs[e] = src[e];
+    }
+    __syncthreads();
+    for (int k = 0; k < nk; ++k) {
+      // fp32 prefilter of the 8 x MM_G pairs without branches; pairs between
+      // the cuts (and distance 0: duplicates, the particle itself) go to the
+      // exact fp64 test below, entered when any lane of the wave has one
+      // (rows past N have zero features, so their bits do not matter; the
+      // excluded rank-0 row has distance 0 and always takes the exact test)
+      half8 a[MM_G];
+      unsigned need = 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rl = 32 * k + 8 * kq + u;
+        const bool inN = 32 * sb + rl < N;
+        float xj32[D];
+#pragma unroll
+        for (int q = 0; q < D; ++q) xj32[q] = xs[rl * D + q];
+#pragma unroll
+        for (int g = 0; g < MM_G; ++g) {
+          const float s32 = dist2f<D>(xj32, xp32[g]);
+          const bool in = s32 < cut_in[g] && s32 > 0.0f;
+          const bool open = !in && !(s32 > cut_out[g]) && inN;
+          a[g][u] = in ? (_Float16)1.0f : (_Float16)0.0f;
+          need |= (open ? 1u : 0u) << (u * MM_G + g);
+        }
+      }
+      if (__ballot(need != 0u)) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+#pragma unroll
+          for (int g = 0; g < MM_G; ++g) {
+            if ((need >> (u * MM_G + g)) & 1u) {
+              const int64_t j = 32 * sb + 32 * k + 8 * kq + u;
+              const int64_t pn = p0 + 16 * g + (lane & 15);
+              const int64_t pe = pn < N ? pn : N - 1;
+              double xj[D], xp[D];
+#pragma unroll
+              for (int q = 0; q < D; ++q) { xj[q] = X[j * D + q]; xp[q] = X[pe * D + q]; }
+              const unsigned long long key =
+                  (unsigned long long)__double_as_longlong(dist2v<D>(xj, xp));
+              const bool member = key < vs[g] || (key == vs[g] && j < jcut[g]);
+              a[g][u] = (member && j != r0[g]) ? (_Float16)1.0f : (_Float16)0.0f;
+            }
+          }
+        }
+      }
+      const half8* b = bs + k * NT * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const half8 bt = b[t * 64];
+#pragma unroll
+        for (int g = 0; g < MM_G; ++g)
+          acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[g], bt, acc[g][t], 0, 0, 0);
+      }
+      if (++since == MM_FLUSH) flush();
+    }
+  }
+  if (since > 0 || first) flush();
+}
+
+// limbs + chunks -> raw sums -> moments centred at X_n in local_finish's
+// layout [NM][N]; flags a particle whose rounding bound is not far below its
+// local variance
+template <int D>
+__global__ __launch_bounds__(256) void mm_finish_kernel(const double* __restrict__ X, int64_t N,
+                                                        int64_t nq,
+                                                        const double* __restrict__ part,
+                                                        int RS, const double* __restrict__ bnd,
+                                                        double* __restrict__ out,
+                                                        int* __restrict__ flag) {
+  constexpr int NM = local_nm<D>(), NCP = 16 * mm_nt<D>();
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  double S[NM], E[NM];
+  for (int f = 0; f < NM; ++f) {
+    const int e = mm_fexp<D>(f, bnd);
+    double v = 0.0;
+    for (int l = ML_NL - 1; l >= 0; --l) {   // smallest limb first
+      double c = 0.0;
+      for (int y = 0; y < RS; ++y) c += part[((int64_t)y * NCP + f * ML_NL + l) * N + n];
+      v += ldexp(c, e - 11 * (l + 1));
+    }
+    S[f] = v;
+    // last-limb rounding per member + the limb sum's own rounding
+    E[f] = (double)nq * ldexp(1.0, e - 11 * ML_NL - 1) + 4.0 * MM_EPS * fabs(v);
+  }
+  double yn[D];
+  for (int a = 0; a < D; ++a) yn[a] = X[n * D + a] - X[a];
+  const double S0 = S[0];
+  out[0 * N + n] = S0;
+  out[1 * N + n] = S[1];
+  double m1[D];
+  for (int a = 0; a < D; ++a) {
+    m1[a] = S[2 + a] - S0 * yn[a];
+    out[(int64_t)(2 + a) * N + n] = m1[a];
+  }
+  bool bad = !(S0 > 0.0);
+  int c = 2 + D;
+  for (int a = 0; a < D; ++a)
+    for (int b = a; b < D; ++b, ++c) {
+      const double t1 = S[2 + a] * yn[b], t2 = S[2 + b] * yn[a], t3 = S0 * yn[a] * yn[b];
+      const double v = ((S[c] - t1) - t2) + t3;
+      out[(int64_t)c * N + n] = v;
+      if (a == b) {
+        // error of v (absolute) against the local variance about the mean
+        const double err = E[c] + E[2 + a] * fabs(yn[b]) + E[2 + b] * fabs(yn[a]) +
+                           E[0] * fabs(yn[a] * yn[b]) +
+                           8.0 * MM_EPS * (fabs(S[c]) + fabs(t1) + fabs(t2) + fabs(t3));
+        const double var = v - m1[a] * m1[a] / S0;
+        if (!(err <= 1e-11 * var)) bad = true;
+      }
+    }
+  if (bad) atomicOr(flag, 1);
+}
+
+inline int mm_chunks(int64_t N, int64_t nsteps) {
+  const int64_t nblk = (N + MM_PB - 1) / MM_PB;
+  int64_t rs = (1024 + nblk - 1) / nblk;
+  if (rs > 8) rs = 8;
+  if (rs > nsteps) rs = nsteps;
+  return (int)(rs < 1 ? 1 : rs);
+}
+
 // particles per selection block (their coordinates in registers)
 template <int D> constexpr int sel_pb() { return D <= 8 ? 8 : 4; }
 
@@ -740,12 +1073,51 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   const int RS = N > 1 ? moments_chunks(N) : 1;
   double* part = cv.take<double>((size_t)RS * NM * (size_t)N);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
-  if (N > 1) {
+  // dense neighbourhoods (k > N / 16, d <= 7): the moments on f16 MFMA
+  bool dense = D <= 7 && N >= 64 && nq * 16 > N && !(ABC_LOCAL_MOMENTS_VALU);
+  const double* mom = part;
+  int mom_rs = RS;
+  if constexpr (D <= 7) if (dense) {
+    const int64_t nsteps = ceil_div(N, 32);
+    const int RS16 = mm_chunks(N, nsteps);
+    unsigned long long* bnd = cv.take<unsigned long long>(1 + D);
+    int* flag = cv.take<int>(1);
+    half8* img = cv.take<half8>((size_t)nsteps * mm_nt<D>() * 64);
+    double* part16 = cv.take<double>((size_t)RS16 * 16 * mm_nt<D>() * (size_t)N);
+    double* cen = cv.take<double>((size_t)NM * N);
+    if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
+    ABC_HIP(hipMemsetAsync(bnd, 0, sizeof(unsigned long long) * (1 + D), s));
+    ABC_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+    const int64_t bb = ceil_div(N, 256) < 256 ? ceil_div(N, 256) : 256;
+    hipLaunchKernelGGL((mm_bounds_kernel<D>), dim3((unsigned)bb), dim3(256), 0, s, X, w, N, bnd);
+    ABC_LAUNCHED();
+    hipLaunchKernelGGL((mm_bimg_kernel<D>), dim3((unsigned)ceil_div(nsteps * mm_nt<D>() * 64, 256)),
+                       dim3(256), 0, s, X, w, N, nsteps, (const double*)bnd, img);
+    ABC_LAUNCHED();
+    hipLaunchKernelGGL((mm_moments_kernel<D>), dim3((unsigned)ceil_div(N, MM_PB), (unsigned)RS16),
+                       dim3(512), 0, s, X, (const float*)X32, (const double*)Mx,
+                       (const half8*)img, N, nsteps, (const unsigned long long*)sel_v,
+                       (const long long*)sel_ties, (const long long*)sel_rank0, part16);
+    ABC_LAUNCHED();
+    hipLaunchKernelGGL((mm_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
+                       X, N, nq, (const double*)part16, RS16, (const double*)bnd, cen, flag);
+    ABC_LAUNCHED();
+    int h_flag = 0;
+    ABC_HIP(hipMemcpyAsync(&h_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+    ABC_HIP(hipStreamSynchronize(s));
+    if (h_flag) {
+      dense = false;   // rounding bound not met somewhere: the VALU kernel
+    } else {
+      mom = cen;
+      mom_rs = 1;
+    }
+  }
+  if (N > 1 && !dense) {
     launch_moments<D, 0>(X, X32, Mx, w, N, sel_v, sel_ties, sel_rank0, part, RS, s);
     ABC_LAUNCHED();
   }
   hipLaunchKernelGGL((local_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256),
-                     0, s, X, N, nq, scaling, eps, (const double*)part, RS, covs, inv,
+                     0, s, X, N, nq, scaling, eps, mom, mom_rs, covs, inv,
                      dets, chol, lnorm);
   ABC_LAUNCHED();
   return ABC_OK;
@@ -1013,6 +1385,16 @@ extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
   // partial moments of the row chunks (local_moments_kernel)
   const size_t nm = 2 + (size_t)d + (size_t)d * (d + 1) / 2;
   size_only<double>(off, (size_t)moments_chunks(N > 1 ? N : 1) * nm * (size_t)(N > 0 ? N : 1));
+  if (d <= 7) {   // dense-neighbourhood MFMA path (mm_*_kernel)
+    const int64_t n1 = N > 0 ? N : 1;
+    const int64_t nsteps = (n1 + 31) / 32;
+    const int64_t nt = ((int64_t)nm * ML_NL + 15) / 16;
+    size_only<unsigned long long>(off, 1 + (size_t)d);
+    size_only<int>(off, 1);
+    size_only<half8>(off, (size_t)(nsteps * nt * 64));
+    size_only<double>(off, (size_t)mm_chunks(n1, nsteps) * 16 * nt * (size_t)n1);
+    size_only<double>(off, nm * (size_t)n1);
+  }
   return off + 256;
 }
 

@@ -257,6 +257,26 @@ def test_local_fit_selection_paths_vs_oracle(dev, grid, N, d, k):
     np.testing.assert_allclose(dets.cpu().numpy(), ref["dets"], rtol=1e-8)
 
 
+@pytest.mark.parametrize("scale", [1e3, 1e7])
+def test_local_fit_dense_outlier(dev, scale):
+    """k > N / 16 takes the f16-limb moments GEMM (abc_local.hip
+    mm_moments_kernel), whose block exponents come from the population's
+    largest |x - x_0|.  One far outlier stretches them: the per-particle
+    rounding bound then decides between the GEMM and the VALU kernel (at
+    1e7 it sends the fit back), and either way the covariances must be the
+    oracle's."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(int(scale))
+    N, d, k = 3000, 3, 700
+    X = rng.normal(size=(N, d))
+    X[17] = scale
+    w = np.exp(0.3 * rng.standard_normal(N))
+    w /= w.sum()
+    ref = oracle.local_fit(X, w, k=k, k_fraction=None)
+    covs, inv, dets, chol, lnorm = gpu.local_fit(gpu.as_dev(X), gpu.as_dev(w), k, 1.0, 1e-3)
+    np.testing.assert_allclose(covs.cpu().numpy(), ref["covs"], rtol=1e-9, atol=1e-12)
+
+
 @pytest.mark.parametrize("offset,spread,k", [(1e3, 0.01, 50), (1e3, 0.01, 700),
                                              (-3e5, 1.0, 50), (0.0, 1e-6, 50)])
 def test_local_fit_fp32_prefilter_stress(dev, offset, spread, k):
