@@ -145,12 +145,17 @@ class _FusedRound:
             rec_x.copy_(torch.from_numpy(x))
         return idx, torch.tensor([len(acc)])
 
-    def regen(self, lo, idx):
+    def regen(self, lo, idx, out=None):
         i = idx.numpy()
         B = int(i.max()) + 1 if len(i) else 0
         th, lp, anc, x, d = self._rows(lo, B)
-        return tuple(torch.from_numpy(np.ascontiguousarray(a[i]))
+        rows = tuple(torch.from_numpy(np.ascontiguousarray(a[i]))
                      for a in (th, lp, anc, x, d))
+        if out is None:
+            return rows
+        for o, r in zip(out, rows):   # the sampler's preallocated views
+            o.copy_(r.reshape(o.shape))
+        return tuple(out)
 
 
 def _run(n, eps, batch, record, fused=False):
