@@ -727,6 +727,7 @@ constexpr double MM_EPS = 2.220446049250313e-16;  // fp64 epsilon
 constexpr int MM_FLUSH = 256;   // 32-row steps between fp64 flushes (8192 rows)
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // feature f of a row with weight lw and offsets y (local_nm order)
 template <int D>
@@ -838,9 +839,10 @@ __global__ __launch_bounds__(256) void mm_bimg_kernel(const double* __restrict__
 // rows: every particle group re-reads it).  grid (ceil(N / 256), RS row
 // chunks of whole 32-row steps); part [RS][16 NT][N] (exact integer sums).
 constexpr int MM_G = 2, MM_W = 8, MM_SB = 4;
+constexpr int MM_T = MM_W * 64;          // threads per block
 constexpr int MM_PB = MM_W * MM_G * 16;   // particles per block
 template <int D>
-__global__ __launch_bounds__(512) void mm_moments_kernel(
+__global__ __launch_bounds__(MM_T) void mm_moments_kernel(
     const double* __restrict__ X, const float* __restrict__ X32,
     const double* __restrict__ Mp, const half8* __restrict__ img, int64_t N,
     int64_t nsteps, const unsigned long long* __restrict__ sel_v,
@@ -872,6 +874,10 @@ __global__ __launch_bounds__(512) void mm_moments_kernel(
     cut_in[g] = f32_cut_below<D>(key_val(vs[g]), M);
     cut_out[g] = f32_cut_above<D>(key_val(vs[g]), M);
   }
+  static_assert(MM_G == 2, "packed distances pair the two tiles");
+  f32x2 xp2[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) xp2[q] = f32x2{xp32[0][q], xp32[1][q]};
   f32x4 acc[MM_G][NT];
 #pragma unroll
   for (int g = 0; g < MM_G; ++g)
@@ -898,49 +904,87 @@ __global__ __launch_bounds__(512) void mm_moments_kernel(
     first = false;
     since = 0;
   };
+  // The next stage's B fragments and rows are loaded into registers while
+  // the current one computes (one block per CU at this register count, so a
+  // synchronous stage would idle the CU for a full HBM/L2 round trip).
+  constexpr int PF = (MM_SB * NT * 64 + MM_T - 1) / MM_T, PFX = (MM_SB * 32 * D + MM_T - 1) / MM_T;
+  half8 pf[PF];
+  float pfx[PFX];
+  auto fetch = [&](int64_t sb) {
+    const int nk = (int)((s1 - sb) < MM_SB ? (s1 - sb) : MM_SB);
+    const int64_t jb = 32 * sb;
+    const int64_t cnt = ((N - jb) < MM_SB * 32 ? (N - jb) : MM_SB * 32) * D;
+#pragma unroll
+    for (int i = 0; i < PFX; ++i) {
+      const int e = threadIdx.x + MM_T * i;
+      pfx[i] = e < cnt ? X32[jb * D + e] : 0.0f;
+    }
+    const half8* src = img + sb * NT * 64;
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = threadIdx.x + MM_T * i;
+      if (e < nk * NT * 64) pf[i] = src[e];
+    }
+  };
+  if (s0 < s1) fetch(s0);
   for (int64_t sb = s0; sb < s1; sb += MM_SB) {
     const int nk = (int)((s1 - sb) < MM_SB ? (s1 - sb) : MM_SB);
     __syncthreads();
-    {
-      const int64_t jb = 32 * sb;
-      const int64_t cnt = ((N - jb) < MM_SB * 32 ? (N - jb) : MM_SB * 32) * D;
-      for (int e = threadIdx.x; e < MM_SB * 32 * D; e += 512)
-        xs[e] = e < cnt ? X32[jb * D + e] : 0.0f;
-      const half8* src = img + sb * NT * 64;
-      for (int e = threadIdx.x; e < nk * NT * 64; e += 512) bs[e] = src[e];
+#pragma unroll
+    for (int i = 0; i < PFX; ++i) {
+      const int e = threadIdx.x + MM_T * i;
+      if (e < MM_SB * 32 * D) xs[e] = pfx[i];
+    }
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int e = threadIdx.x + MM_T * i;
+      if (e < nk * NT * 64) bs[e] = pf[i];
     }
     __syncthreads();
+    if (sb + MM_SB < s1) fetch(sb + MM_SB);
     for (int k = 0; k < nk; ++k) {
       // fp32 prefilter of the 8 x MM_G pairs without branches; pairs between
       // the cuts (and distance 0: duplicates, the particle itself) go to the
       // exact fp64 test below, entered when any lane of the wave has one
       // (rows past N have zero features, so their bits do not matter; the
-      // excluded rank-0 row has distance 0 and always takes the exact test)
+      // excluded rank-0 row has distance 0 and always takes the exact test).
+      // The two tiles' distances run as packed f32 pairs (the same sub / fma
+      // per element as dist2f, so the same bits).
       half8 a[MM_G];
-      unsigned need = 0;
+      bool anyopen = false;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int rl = 32 * k + 8 * kq + u;
         const bool inN = 32 * sb + rl < N;
-        float xj32[D];
+        f32x2 s2 = f32x2{0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < D; ++q) xj32[q] = xs[rl * D + q];
+        for (int q = 0; q < D; ++q) {
+          const float xq = xs[rl * D + q];
+          const f32x2 t = f32x2{xq, xq} - xp2[q];
+          s2 = __builtin_elementwise_fma(t, t, s2);
+        }
 #pragma unroll
         for (int g = 0; g < MM_G; ++g) {
-          const float s32 = dist2f<D>(xj32, xp32[g]);
+          const float s32 = s2[g];
           const bool in = s32 < cut_in[g] && s32 > 0.0f;
-          const bool open = !in && !(s32 > cut_out[g]) && inN;
+          anyopen |= !in && !(s32 > cut_out[g]) && inN;
           a[g][u] = in ? (_Float16)1.0f : (_Float16)0.0f;
-          need |= (open ? 1u : 0u) << (u * MM_G + g);
         }
       }
-      if (__ballot(need != 0u)) {
+      if (__ballot(anyopen)) {
+        // rare: redo the prefilter per pair and settle the open ones in fp64
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
+          const int rl = 32 * k + 8 * kq + u;
+          const int64_t j = 32 * sb + rl;
 #pragma unroll
           for (int g = 0; g < MM_G; ++g) {
-            if ((need >> (u * MM_G + g)) & 1u) {
-              const int64_t j = 32 * sb + 32 * k + 8 * kq + u;
+            float xj32[D];
+#pragma unroll
+            for (int q = 0; q < D; ++q) xj32[q] = xs[rl * D + q];
+            const float s32 = dist2f<D>(xj32, xp32[g]);
+            const bool in = s32 < cut_in[g] && s32 > 0.0f;
+            if (!in && !(s32 > cut_out[g]) && j < N) {
               const int64_t pn = p0 + 16 * g + (lane & 15);
               const int64_t pe = pn < N ? pn : N - 1;
               double xj[D], xp[D];
@@ -1073,11 +1117,12 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   const int RS = N > 1 ? moments_chunks(N) : 1;
   double* part = cv.take<double>((size_t)RS * NM * (size_t)N);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
-  // dense neighbourhoods (k > N / 16, d <= 7): the moments on f16 MFMA
-  bool dense = D <= 7 && N >= 64 && nq * 16 > N && !(ABC_LOCAL_MOMENTS_VALU);
+  // dense neighbourhoods (k > N / 16, d <= 5; above, the kernel's registers
+  // spill): the moments on f16 MFMA
+  bool dense = D <= 5 && N >= 64 && nq * 16 > N && !(ABC_LOCAL_MOMENTS_VALU);
   const double* mom = part;
   int mom_rs = RS;
-  if constexpr (D <= 7) if (dense) {
+  if constexpr (D <= 5) if (dense) {
     const int64_t nsteps = ceil_div(N, 32);
     const int RS16 = mm_chunks(N, nsteps);
     unsigned long long* bnd = cv.take<unsigned long long>(1 + D);
@@ -1095,7 +1140,7 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
                        dim3(256), 0, s, X, w, N, nsteps, (const double*)bnd, img);
     ABC_LAUNCHED();
     hipLaunchKernelGGL((mm_moments_kernel<D>), dim3((unsigned)ceil_div(N, MM_PB), (unsigned)RS16),
-                       dim3(512), 0, s, X, (const float*)X32, (const double*)Mx,
+                       dim3(MM_T), 0, s, X, (const float*)X32, (const double*)Mx,
                        (const half8*)img, N, nsteps, (const unsigned long long*)sel_v,
                        (const long long*)sel_ties, (const long long*)sel_rank0, part16);
     ABC_LAUNCHED();
@@ -1385,7 +1430,7 @@ extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
   // partial moments of the row chunks (local_moments_kernel)
   const size_t nm = 2 + (size_t)d + (size_t)d * (d + 1) / 2;
   size_only<double>(off, (size_t)moments_chunks(N > 1 ? N : 1) * nm * (size_t)(N > 0 ? N : 1));
-  if (d <= 7) {   // dense-neighbourhood MFMA path (mm_*_kernel)
+  if (d <= 5) {   // dense-neighbourhood MFMA path (mm_*_kernel)
     const int64_t n1 = N > 0 ? N : 1;
     const int64_t nsteps = (n1 + 31) / 32;
     const int64_t nt = ((int64_t)nm * ML_NL + 15) / 16;

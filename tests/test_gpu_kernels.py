@@ -239,8 +239,8 @@ def test_local_fit_selection_paths_vs_oracle(dev, grid, N, d, k):
     path (small and large k) and the radix-pass fallback (a {0,1}^3 grid: buckets of hundreds of exact ties,
     taken by index) against the oracle's (distance, index) order.  d = 9..16
     run the 4-particle selection blocks and the sliced moments (several
-    kernels over one moment list each).  k > N / 16 takes the moments GEMM
-    (local_moments_mfma_kernel), including grids of ties and k = N - 1."""
+    kernels over one moment list each).  k > N / 16 at d <= 5 takes the f16-limb moments
+    GEMM (mm_moments_kernel), including grids of ties and d = 1."""
     from pyabc_amd import gpu
     rng = np.random.default_rng(N + k)
     if grid is None:
@@ -259,7 +259,7 @@ def test_local_fit_selection_paths_vs_oracle(dev, grid, N, d, k):
 
 @pytest.mark.parametrize("scale", [1e3, 1e7])
 def test_local_fit_dense_outlier(dev, scale):
-    """k > N / 16 takes the f16-limb moments GEMM (abc_local.hip
+    """k > N / 16 at d <= 5 takes the f16-limb moments GEMM (abc_local.hip
     mm_moments_kernel), whose block exponents come from the population's
     largest |x - x_0|.  One far outlier stretches them: the per-particle
     rounding bound then decides between the GEMM and the VALU kernel (at
