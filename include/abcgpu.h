@@ -52,6 +52,12 @@ extern "C" {
 #define ABC_PRIOR_LOGNORM 4 /* params: s, loc, scale                    */
 #define ABC_PRIOR_GAMMA 5   /* params: a, loc, scale                    */
 #define ABC_PRIOR_BETA 6    /* params: a, b, loc, scale                 */
+/* any other scipy.stats family: the device knows only its support [lo, hi]
+ * (re-draw test) and a point c inside it (the t = 0 draw, which the host
+ * replaces by ppf(u) of abc_prior_uniforms); density factor 1 on the
+ * support -- the host adds the scipy log density of the kept rows.
+ * params: lo, hi, c */
+#define ABC_PRIOR_HOST 7
 
 const char* abc_last_error(void);
 int abc_version(void);
@@ -171,6 +177,14 @@ int abc_propose(const double* X, const double* cdf, const int32_t* guide,
 int abc_prior_logpdf(const double* theta, int64_t B, int d,
                      const int32_t* prior_kind, const double* prior_params,
                      double* out, void* stream);
+/* u[b] in (0, 1): the uniform of candidate idx0 + b's prior stream for
+ * dimension k in the attempt it accepted (attempts[b], from abc_propose; null:
+ * the first attempt).  An ABC_PRIOR_HOST coordinate's t = 0 draw is the
+ * host's ppf(u) (Distribution.rvs, random_variables.py:412-423, for a family
+ * without a device sampler), keyed like every other draw. */
+int abc_prior_uniforms(const int32_t* attempts, double* u, int64_t B, int k,
+                       uint64_t seed, uint32_t generation, int64_t idx0,
+                       void* stream);
 
 /* ---- vectorised synthetic simulator (the Model.sample boundary,
  * pyabc/model.py:89-116): x[b,k] = a[k] * theta[b, src[k]] + sigma[k] * e,
@@ -190,9 +204,12 @@ int abc_pnorm(const double* x, int64_t B, int S, const double* x0,
 
 /* A proposal that exhausted max_attempts (attempts > max_attempts) is not a
  * valid candidate (the reference keeps drawing, smc.py:649-662): its
- * distance becomes +inf so that no acceptor takes it. */
+ * distance becomes `value` so that no acceptor takes it -- NaN for a
+ * distance (NaN <= eps is false even at eps = +inf), the zero-probability
+ * density (-inf on log scale, 0 on linear scale) for a StochasticAcceptor,
+ * whose "distance" is a noise-model density (higher = more likely). */
 int abc_mask_gave_up(double* dist, const int32_t* attempts, int64_t B,
-                     int max_attempts, void* stream);
+                     int max_attempts, double value, void* stream);
 
 /* ---- UniformAcceptor (acceptor.py:235-244) + order-preserving compaction -
  * accept[b] = d[b] <= eps.  Writes the positions of accepted rows in
@@ -323,16 +340,19 @@ int abc_column_mad(const double* X, int64_t R, int S, double* out, void* ws,
  * 1/(1 - sum a^2)), all-zero -> diag(|X[0]|), times scaling, then
  * "while det <= 0: cov += eps I".  Writes covs, inverse covs, dets,
  * Cholesky factors (for rvs) and log normalisation
- * log sqrt((2 pi)^d det) per particle.  d <= 8. */
+ * log sqrt((2 pi)^d det) per particle.  d <= 64: d <= 16 on the templated
+ * select / moments kernels, 16 < d <= 64 on runtime-d kernels (one
+ * workgroup per particle, abc_local_wide.hip).  N < 2^31. */
 size_t abc_local_fit_workspace(int64_t N, int d);
 int abc_local_fit(const double* X, const double* w, int64_t N, int d,
                   int64_t k, double scaling, double eps, double* covs,
                   double* inv_covs, double* dets, double* chol,
                   double* log_norm, void* ws, size_t ws_bytes, void* stream);
 /* pdf: out[i] = log( sum_j w_j exp(-d_ij^T inv_j d_ij / 2 - log_norm_j)
- * / sum_j w_j ), d_ij = X_j - x_i.  The quadratic form is a GEMM over the
- * candidates' quadratic features on fp64 MFMA (workspace: packed population
- * coefficients + per-chunk partial sums). */
+ * / sum_j w_j ), d_ij = X_j - x_i.  d <= 16: the quadratic form is a GEMM
+ * over the candidates' quadratic features on fp64 MFMA (workspace: packed
+ * population coefficients + per-chunk partial sums); 16 < d <= 64: a direct
+ * fp64 quadratic form per pair (no workspace). */
 size_t abc_local_logpdf_workspace(int64_t M, int64_t N, int d);
 int abc_local_logpdf(const double* x, int64_t M, const double* X,
                      const double* w, int64_t N, int d, const double* inv_covs,

@@ -112,6 +112,24 @@ def propose_mvn(X, w, L, seed, generation, idx0, B, kinds=None, params=None,
     return theta, lp, anc, att
 
 
+def prior_uniforms(index, att, k, generation, seed):
+    """The (0, 1) uniform of candidate `index`'s prior stream for dimension
+    k in the attempt it accepted (device abc_prior_uniforms): words 0..1 of
+    slot (att - 1) * 65536 + SLOT_PRIOR + 512 k, 53 bits plus a half.  An
+    ABC_PRIOR_HOST coordinate's t = 0 draw is scipy's ppf of it."""
+    index = np.asarray(index, dtype=np.uint64)
+    att = np.maximum(np.asarray(att, dtype=np.int64) - 1, 0)
+    out = np.empty(index.shape)
+    for a in np.unique(att):
+        sel = att == a
+        r = philox4x32_10(index[sel], int(a) * SLOTS_PER_ATTEMPT + SLOT_PRIOR + 512 * k,
+                          generation, seed)
+        hi = (r[:, 0] >> np.uint32(5)).astype(np.float64)
+        lo = (r[:, 1] >> np.uint32(6)).astype(np.float64)
+        out[sel] = (hi * 67108864.0 + lo + 0.5) / 9007199254740992.0
+    return out
+
+
 def simulate_linear_gaussian(theta, src, a, sigma, seed, generation, idx0):
     """x[b, k] = a[k] theta[b, src[k]] + sigma[k] n_k (normal k of the
     candidate's simulation stream)."""

@@ -9,8 +9,7 @@ import logging
 import os
 
 from .parameters import Parameter
-from .random_variables import (Distribution, ModelPerturbationKernel, RV,
-                               RVBase, RVDecorator, LowerBoundDecorator)
+from .random_variables import Distribution, RV, RVBase
 from .distance import (Distance, NoDistance, IdentityFakeDistance,
                        AcceptAllDistance, SimpleFunctionDistance,
                        PNormDistance, AdaptivePNormDistance, to_distance,
@@ -25,14 +24,14 @@ from .epsilon import (Epsilon, NoEpsilon, ConstantEpsilon, QuantileEpsilon,
                       PolynomialDecayFixedIterScheme, DalyScheme,
                       FrielPettittScheme, EssScheme)
 from .sampler import (Sampler, Sample, SingleCoreSampler, BatchedGPUSampler)
-from .smc import ABCSMC, GenerationSpec
+from .smc import ABCSMC, GenerationSpec, ModelPerturbationKernel
 from .storage import History, create_sqlite_db_id
 from .acceptor import (Acceptor, SimpleFunctionAcceptor, UniformAcceptor,
                        StochasticAcceptor, pdf_norm_from_kernel,
                        pdf_norm_max_found, ScaledPDFNorm)
 from . import distance, epsilon, acceptor, storage
-from .model import (Model, SimpleModel, ModelResult, IntegratedModel,
-                    VectorizedModel, LinearGaussianModel)
+from .model import (Model, SimpleModel, ModelResult, VectorizedModel,
+                    LinearGaussianModel)
 from .transition import (Transition, MultivariateNormalTransition,
                          LocalTransition, NotEnoughParticles)
 from .population import Particle, Population

@@ -46,10 +46,11 @@ SIGNATURES = {
     "abc_propose": (I32, [P, P, P, I64, I32, P, P, P, U64, U32, I64, I64, I32,
                           P, P, P, P, P]),
     "abc_prior_logpdf": (I32, [P, I64, I32, P, P, P, P]),
+    "abc_prior_uniforms": (I32, [P, P, I64, I32, U64, U32, I64, P]),
     "abc_simulate_linear_gaussian": (I32, [P, I64, I32, I32, P, P, P, U64,
                                            U32, I64, P, P]),
     "abc_pnorm": (I32, [P, I64, I32, P, P, D, P, P]),
-    "abc_mask_gave_up": (I32, [P, P, I64, I32, P]),
+    "abc_mask_gave_up": (I32, [P, P, I64, I32, D, P]),
     "abc_compact_workspace": (SZ, [I64]),
     "abc_accept_compact": (I32, [P, I64, D, P, P, P, SZ, P]),
     "abc_candidates_workspace": (SZ, [I64]),
@@ -118,7 +119,7 @@ ABC_PREC_F32 = 1
 ABC_PREC_X3 = 2
 
 PRIOR_KINDS = {"norm": 0, "uniform": 1, "expon": 2, "laplace": 3,
-               "lognorm": 4, "gamma": 5, "beta": 6}
+               "lognorm": 4, "gamma": 5, "beta": 6, "host": 7}
 
 
 class NativeError(RuntimeError):

@@ -79,6 +79,8 @@ __device__ __noinline__ double prior_logpdf1(int kind, const double* p, double x
       double t2 = (b == 1.0) ? 0.0 : (b - 1.0) * log1p(-y);
       return t1 + t2 - lb - log(p[3]);
     }
+    case ABC_PRIOR_HOST:  // lo, hi, c: factor 1 on the support (host adds scipy's)
+      return (x >= p[0] && x <= p[1]) ? 0.0 : -INFINITY;
   }
   return NAN;
 }
@@ -121,6 +123,8 @@ __device__ __forceinline__ bool prior_in_support1(int kind, const double* p, dou
       if (y == 1.0 && p[1] > 1.0) return false;
       return true;
     }
+    case ABC_PRIOR_HOST:
+      return x >= p[0] && x <= p[1];
   }
   return false;
 }
@@ -175,6 +179,8 @@ __device__ __noinline__ double prior_draw1(int kind, const double* p, uint64_t g
       double y = gamma_draw(p[1], g, base + 1 + 256, gen, seed);
       return p[2] + p[3] * x / (x + y);
     }
+    case ABC_PRIOR_HOST:  // a support point; the host writes ppf(u) over it
+      return p[2];
   }
   return NAN;
 }
@@ -291,6 +297,7 @@ __device__ __forceinline__ void support_bounds_wave(int kind, const double* pg, 
     case ABC_PRIOR_LOGNORM: case ABC_PRIOR_GAMMA: c = p[1] + p[2]; break;
     case ABC_PRIOR_BETA: c = p[2] + 0.5 * p[3]; break;
     case ABC_PRIOR_NORM: case ABC_PRIOR_LAPLACE: c = p[0]; break;
+    case ABC_PRIOR_HOST: c = p[2]; break;
     default: c = 0.0;
   }
   if (!prior_in_support1(kind, p, c)) {
@@ -572,7 +579,12 @@ __device__ __forceinline__ bool lazy_filter_ok(const BlockConsts& C, const Propo
   }
 }
 
+// (contraction is off for the whole header, line 20; restated in each of
+// these three so that no include order or later edit can let the compiler
+// turn s + v * v into an fma in one kernel and not in another: the round's
+// accept bit and the regenerated / staged distance must be the same bits)
 __device__ __forceinline__ double pterm(double v, double p) {
+#pragma clang fp contract(off)
   return (p == 1.0) ? v : (p == 2.0 ? v * v : pow(v, p));
 }
 // running p-norm state s (sum of |.|^p, or max for p = inf); order = k order.
@@ -582,11 +594,13 @@ __device__ __forceinline__ double pterm(double v, double p) {
 // (~30 VGPRs), so the hot kernels are instantiated for p == 2 separately.
 template <int PK = 0>
 __device__ __forceinline__ double pnorm_acc(double s, double v, double p) {
+#pragma clang fp contract(off)
   if constexpr (PK == 2) return s + v * v;
   return isinf(p) ? fmax(s, v) : s + pterm(v, p);
 }
 template <int PK = 0>
 __device__ __forceinline__ double pnorm_finish(double s, double p) {
+#pragma clang fp contract(off)
   if constexpr (PK == 2) return sqrt(s);
   return isinf(p) ? s : ((p == 1.0) ? s : (p == 2.0 ? sqrt(s) : pow(s, 1.0 / p)));
 }

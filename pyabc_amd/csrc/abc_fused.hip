@@ -41,8 +41,9 @@ struct RoundArgs {
 };
 
 // Full evaluation of candidate g: proposal + simulation + distance.  Returns
-// the distance (+inf when the proposal gave up on the prior support), the
-// attempts and the ancestor through the references; x (nullable) gets the row.
+// the distance (NaN when the proposal gave up on the prior support: never
+// accepted, even at eps = +inf), the attempts and the ancestor through the
+// references; x (nullable) gets the row.
 template <int D, int MODE, int PK>
 __device__ __forceinline__ double evaluate_full(const RoundArgs& A, const BlockConsts& C,
                                                 uint64_t g,
@@ -56,7 +57,7 @@ __device__ __forceinline__ double evaluate_full(const RoundArgs& A, const BlockC
     s = sim_pnorm_range<PK>(A.M, C, th, 1, g, A.P.gen, A.P.seed, 0, A.M.S, 0.0, x);
   }
   const double dist = pnorm_finish<PK>(s, A.M.p);
-  return att <= A.P.max_attempts ? dist : INFINITY;
+  return att <= A.P.max_attempts ? dist : NAN;
 }
 
 // Rows written through LDS: one group = FR_T candidates (one per thread)
@@ -99,7 +100,7 @@ __device__ __forceinline__ double evaluate_staged(const RoundArgs& A, const Bloc
     __syncthreads();
   }
   const double dist = pnorm_finish<PK>(s, A.M.p);
-  return att <= A.P.max_attempts ? dist : INFINITY;
+  return att <= A.P.max_attempts ? dist : NAN;
 }
 
 template <int D, int MODE, bool FILTER, int PK>

@@ -1418,11 +1418,21 @@ int launch_pdf(const double* x, int64_t M, const double* X, const double* w,
 }
 
 }  // namespace
+
+// 16 < d <= 64: runtime-d kernels (abc_local_wide.hip)
+size_t local_wide_fit_workspace(int64_t N, int d);
+int local_wide_fit(const double* X, const double* w, int64_t N, int d, int64_t nq,
+                   double scaling, double eps, double* covs, double* invs, double* dets,
+                   double* chol, double* lnorm, void* ws, size_t ws_bytes, hipStream_t s);
+int local_wide_logpdf(const double* x, int64_t M, const double* X, const double* w,
+                      int64_t N, int d, const double* inv, const double* lnorm,
+                      double* out, hipStream_t s);
 }  // namespace abc
 
 using namespace abc;
 
 extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
+  if (d > 16) return local_wide_fit_workspace(N, d);
   size_t off = 0;
   for (int i = 0; i < 3; ++i) size_only<int64_t>(off, (size_t)(N > 0 ? N : 1));
   size_only<float>(off, (size_t)(N > 0 ? N : 1) * (size_t)d);   // X32
@@ -1448,11 +1458,15 @@ extern "C" int abc_local_fit(const double* X, const double* w, int64_t N,
                              double* covs, double* inv_covs, double* dets,
                              double* chol, double* log_norm, void* ws,
                              size_t ws_bytes, void* stream) {
-  ABC_CHECK_ARG(N >= 1 && d >= 1 && d <= 16 && k >= 1, "local_fit: bad N/d/k (d <= 16)");
+  ABC_CHECK_ARG(N >= 1 && d >= 1 && d <= 64 && k >= 1, "local_fit: bad N/d/k (d <= 64)");
+  ABC_CHECK_ARG(N < (1ll << 31), "local_fit: N >= 2^31");
   ABC_CHECK_ARG(ws && ws_bytes >= abc_local_fit_workspace(N, d), "local_fit: workspace");
   ABC_CHECK_ARG(X && w && covs && inv_covs && dets && chol && log_norm, "local_fit: null pointer");
   const int64_t nq = (k + 1) < N ? (k + 1) : N;
   hipStream_t s = as_stream(stream);
+  if (d > 16)
+    return local_wide_fit(X, w, N, d, nq, scaling, eps, covs, inv_covs, dets, chol, log_norm,
+                          ws, ws_bytes, s);
   switch (d) {
 #define ABC_D(n) case n: return launch_fit<n>(X, w, N, nq, scaling, eps, covs, inv_covs, dets, chol, log_norm, ws, ws_bytes, s);
     ABC_D(1) ABC_D(2) ABC_D(3) ABC_D(4) ABC_D(5) ABC_D(6) ABC_D(7) ABC_D(8)
@@ -1477,10 +1491,14 @@ extern "C" int abc_local_logpdf(const double* x, int64_t M, const double* X,
                                 const double* inv_covs,
                                 const double* log_norm, double* out,
                                 void* ws, size_t ws_bytes, void* stream) {
-  ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= 16, "local_logpdf: bad M/N/d (d <= 16)");
+  ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= 64, "local_logpdf: bad M/N/d (d <= 64)");
   if (M == 0) return ABC_OK;
-  ABC_CHECK_ARG(x && X && w && inv_covs && log_norm && out && ws, "local_logpdf: null pointer");
   hipStream_t s = as_stream(stream);
+  if (d > 16) {
+    ABC_CHECK_ARG(x && X && w && inv_covs && log_norm && out, "local_logpdf: null pointer");
+    return local_wide_logpdf(x, M, X, w, N, d, inv_covs, log_norm, out, s);
+  }
+  ABC_CHECK_ARG(x && X && w && inv_covs && log_norm && out && ws, "local_logpdf: null pointer");
   switch (d) {
 #define ABC_D(n) case n: return launch_pdf<n>(x, M, X, w, N, inv_covs, log_norm, out, ws, ws_bytes, s);
     ABC_D(1) ABC_D(2) ABC_D(3) ABC_D(4) ABC_D(5) ABC_D(6) ABC_D(7) ABC_D(8)

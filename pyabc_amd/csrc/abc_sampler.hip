@@ -78,6 +78,22 @@ __global__ void prior_logpdf_kernel(const double* __restrict__ th, int64_t B,
   if (b < B) out[b] = prior_logpdf(kind, params, d, th + b * d);
 }
 
+// u[b] in (0, 1) from word 0..1 of candidate b's prior stream for dimension
+// k in the attempt it accepted (slot (att - 1) 65536 + SLOT_PRIOR + 512 k):
+// the uniform an ABC_PRIOR_HOST coordinate's t = 0 draw ppf(u) is made from
+__global__ void prior_uniforms_kernel(const int32_t* __restrict__ att, int64_t B, int k,
+                                      uint64_t seed, uint32_t gen, int64_t idx0,
+                                      double* __restrict__ u) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int a = att ? (att[b] > 0 ? att[b] - 1 : 0) : 0;
+  const u32x4 r = philox((uint64_t)(idx0 + b),
+                         (uint32_t)a * SLOTS_PER_ATTEMPT + SLOT_PRIOR + 512u * (uint32_t)k,
+                         gen, seed);
+  u[b] = ((double)(r.x >> 5) * 67108864.0 + (double)(r.y >> 6) + 0.5) *
+         (1.0 / 9007199254740992.0);
+}
+
 // x[b,k] = a[k] theta[b, src[k]] + sigma[k] n_k; stat k uses normal k of the
 // candidate's simulation stream (slot SLOT_SIM + k/4).
 __global__ __launch_bounds__(256) void simulate_lg_kernel(
@@ -217,9 +233,9 @@ __global__ __launch_bounds__(CT_T) void accept_write_kernel(
 }
 
 __global__ void mask_gave_up_kernel(double* __restrict__ d, const int32_t* __restrict__ att,
-                                    int64_t B, int max_attempts) {
+                                    int64_t B, int max_attempts, double value) {
   const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < B && att[b] > max_attempts) d[b] = INFINITY;
+  if (b < B && att[b] > max_attempts) d[b] = value;
 }
 
 }  // namespace
@@ -228,12 +244,12 @@ __global__ void mask_gave_up_kernel(double* __restrict__ d, const int32_t* __res
 using namespace abc;
 
 extern "C" int abc_mask_gave_up(double* dist, const int32_t* attempts, int64_t B,
-                                int max_attempts, void* stream) {
+                                int max_attempts, double value, void* stream) {
   ABC_CHECK_ARG(B >= 0, "mask_gave_up: B < 0");
   if (B == 0) return ABC_OK;
   ABC_CHECK_ARG(dist && attempts, "mask_gave_up: null pointer");
   hipLaunchKernelGGL(mask_gave_up_kernel, dim3((unsigned)ceil_div(B, 256)), dim3(256), 0,
-                     as_stream(stream), dist, attempts, B, max_attempts);
+                     as_stream(stream), dist, attempts, B, max_attempts, value);
   ABC_LAUNCHED();
   return ABC_OK;
 }
@@ -298,6 +314,18 @@ extern "C" int abc_prior_logpdf(const double* theta, int64_t B, int d,
   ABC_CHECK_ARG(theta && prior_kind && prior_params && out, "prior_logpdf: null pointer");
   hipLaunchKernelGGL(prior_logpdf_kernel, dim3((unsigned)ceil_div(B, 256)), dim3(256), 0,
                      as_stream(stream), theta, B, d, prior_kind, prior_params, out);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
+extern "C" int abc_prior_uniforms(const int32_t* attempts, double* u, int64_t B, int k,
+                                  uint64_t seed, uint32_t generation, int64_t idx0,
+                                  void* stream) {
+  ABC_CHECK_ARG(B >= 0 && k >= 0 && k < 64, "prior_uniforms: bad B/k");
+  if (B == 0) return ABC_OK;
+  ABC_CHECK_ARG(u, "prior_uniforms: null pointer");
+  hipLaunchKernelGGL(prior_uniforms_kernel, dim3((unsigned)ceil_div(B, 256)), dim3(256), 0,
+                     as_stream(stream), attempts, B, k, seed, generation, idx0, u);
   ABC_LAUNCHED();
   return ABC_OK;
 }

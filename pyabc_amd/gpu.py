@@ -263,10 +263,24 @@ def pnorm(x, x0, wf, pval, out=None):
     return out
 
 
-def mask_gave_up(dist, att, max_attempts):
-    """dist[b] = +inf where att[b] > max_attempts (in place)."""
-    nat.call("abc_mask_gave_up", p(dist), p(att), dist.numel(), int(max_attempts),
+def prior_uniforms(att, k, seed, generation, idx0, B=None):
+    """Uniforms in (0, 1) of the candidates' prior streams for dimension k
+    (abc_prior_uniforms): the source of an ABC_PRIOR_HOST coordinate's draw."""
+    B = att.numel() if B is None else B
+    dev = att.device if att is not None else require_device()
+    u = torch.empty(B, dtype=F64, device=dev)
+    nat.call("abc_prior_uniforms", p(att) if att is not None else None, p(u), B, int(k),
+             int(seed) & 0xFFFFFFFFFFFFFFFF, int(generation) & 0xFFFFFFFF, int(idx0),
              stream_ptr())
+    return u
+
+
+def mask_gave_up(dist, att, max_attempts, value=float("nan")):
+    """dist[b] = value where att[b] > max_attempts (in place); NaN (never
+    accepted, even at eps = inf) unless the caller passes the zero-probability
+    density of a StochasticAcceptor."""
+    nat.call("abc_mask_gave_up", p(dist), p(att), dist.numel(), int(max_attempts),
+             float(value), stream_ptr())
     return dist
 
 

@@ -150,9 +150,3 @@ class LinearGaussianModel(VectorizedModel):
         s["_dev"] = None
         return s
 
-
-class IntegratedModel(Model):
-    """Not on the GPU hot path (SURVEY.md §2 marks it out of scope)."""
-
-    def integrated_simulate(self, pars, eps):
-        raise NotImplementedError()

@@ -1,14 +1,27 @@
-"""Random variables and priors (pyabc/random_variables.py:16-538).
+"""Priors: pyABC's ``RV`` / ``Distribution`` interface
+(pyabc/random_variables.py:111-196 and :328-452) over ``scipy.stats``, plus
+the description the batched sampler needs to evaluate them.
 
-``RV`` / ``Distribution`` keep the reference's scipy-backed per-particle API.
-``Distribution.device_spec()`` describes the prior to the GPU kernels
-(kinds ABC_PRIOR_* of include/abcgpu.h) when every component is a supported
-scipy family; the batched sampler refuses priors it cannot evaluate on the
-device rather than falling back to the CPU.
+Per-candidate use (the reference's closure, SingleCoreSampler) goes straight
+to scipy.  For the batched GPU path every component becomes one of the
+device prior kinds of include/abcgpu.h:
+
+* the seven families the kernels implement (norm, uniform, expon, laplace,
+  lognorm, gamma, beta) -> their own kind and parameters;
+* any other scipy distribution -> ``ABC_PRIOR_HOST``: the device only knows
+  its support interval [lo, hi] (``dist.support()``) for the proposal's
+  re-draw test (smc.py:654-656) and a point inside it; the density and the
+  t = 0 draws of that coordinate are a vectorised host-scipy leg
+  (``host_logpdf`` on the accepted rows, ``host_ppf`` of the device's own
+  per-candidate uniforms), so the rest of the generation stays on the device
+  and the draws stay keyed by the global candidate index.
+
+The HOST kind assumes the density is positive inside the support interval
+(true of scipy's continuous families); a prior whose density vanishes
+inside its support is re-drawn by the reference and is not covered.
 """
 import logging
 from abc import ABC, abstractmethod
-from functools import reduce
 
 import numpy as np
 
@@ -16,8 +29,14 @@ from .parameters import Parameter, ParameterStructure
 
 rv_logger = logging.getLogger("RV")
 
+# scipy family -> (number of shape parameters, their keyword names)
+_DEVICE_FAMILIES = {"norm": (), "uniform": (), "expon": (), "laplace": (),
+                    "lognorm": ("s",), "gamma": ("a",), "beta": ("a", "b")}
+
 
 class RVBase(ABC):
+    """The interface a prior component offers (random_variables.py:16-108)."""
+
     @abstractmethod
     def copy(self):
         ...
@@ -39,168 +58,132 @@ class RVBase(ABC):
         ...
 
 
-class RV(RVBase):
-    """Pickleable wrapper of ``scipy.stats.<name>(*args, **kwargs)``."""
+def _frozen(name, args, kwargs):
+    import scipy.stats
+    return getattr(scipy.stats, name)(*args, **kwargs)
 
-    @classmethod
-    def from_dictionary(cls, dictionary: dict):
-        return cls(dictionary['type'], *dictionary.get('args', []),
-                   **dictionary.get('kwargs', {}))
+
+def _rebuild_rv(name, args, kwargs):
+    return RV(name, *args, **kwargs)
+
+
+class RV(RVBase):
+    """``scipy.stats.<name>(*args, **kwargs)`` that pickles by its recipe.
+
+    ``name``, ``args``, ``kwargs`` and the frozen ``distribution`` are
+    public as in the reference; unknown attributes (``mean``, ``ppf``, ...)
+    are looked up on the frozen distribution."""
 
     def __init__(self, name: str, *args, **kwargs):
         self.name = name
         self.args = args
         self.kwargs = kwargs
-        self.distribution = None
-        self.__setstate__(self.__getstate__())
+        self.distribution = _frozen(name, args, kwargs)
+
+    @classmethod
+    def from_dictionary(cls, dictionary: dict):
+        """{"type": name, "args": [...], "kwargs": {...}}."""
+        return cls(dictionary["type"], *dictionary.get("args", []),
+                   **dictionary.get("kwargs", {}))
+
+    def __reduce__(self):
+        return _rebuild_rv, (self.name, self.args, self.kwargs)
 
     def __getattr__(self, item):
-        if item in ("distribution", "__setstate__", "__getstate__"):
+        # only reached for names not set in __init__; "distribution" itself
+        # missing means a half-built object (unpickling): no recursion
+        if item == "distribution":
             raise AttributeError(item)
         return getattr(self.distribution, item)
 
-    def __getstate__(self):
-        return self.name, self.args, self.kwargs
-
-    def __setstate__(self, state):
-        self.name, self.args, self.kwargs = state
-        import scipy.stats as st
-        self.distribution = getattr(st, self.name)(*self.args, **self.kwargs)
-
     def copy(self):
-        return self.__class__(self.name, *self.args, **self.kwargs)
+        return RV(self.name, *self.args, **self.kwargs)
 
     def rvs(self, *args, **kwargs):
         return self.distribution.rvs(*args, **kwargs)
 
-    def pmf(self, x, *args, **kwargs):
-        return self.distribution.pmf(x, *args, **kwargs)
-
     def pdf(self, x, *args, **kwargs):
         return self.distribution.pdf(x, *args, **kwargs)
+
+    def pmf(self, x, *args, **kwargs):
+        return self.distribution.pmf(x, *args, **kwargs)
 
     def cdf(self, x, *args, **kwargs):
         return self.distribution.cdf(x, *args, **kwargs)
 
     def __repr__(self):
-        return (f"<RV(name={self.name}, args={self.args} "
-                f"kwargs={self.kwargs})>")
+        return f"<RV(name={self.name}, args={self.args} kwargs={self.kwargs})>"
 
-    # -- device description ------------------------------------------------
-    _SHAPES = {"norm": 0, "uniform": 0, "expon": 0, "laplace": 0,
-               "lognorm": 1, "gamma": 1, "beta": 2}
+    # -- batched-sampler description -----------------------------------------
+    @property
+    def is_discrete(self):
+        return not hasattr(self.distribution.dist, "pdf")
 
     def device_spec(self):
-        """(kind, [4 params]) for the GPU kernels, or None if unsupported."""
+        """(kind, [4 params]) for the device kernels: a device family, or
+        ABC_PRIOR_HOST with (lo, hi, centre) of the support interval."""
         from ._native import PRIOR_KINDS
-        if self.name not in self._SHAPES:
+        fam = self._device_family_params()
+        if fam is not None:
+            return PRIOR_KINDS[self.name], fam
+        lo, hi = (float(v) for v in self.distribution.support())
+        if np.isfinite(lo) and np.isfinite(hi):
+            c = 0.5 * (lo + hi)
+        elif np.isfinite(lo):
+            c = lo + 1.0
+        elif np.isfinite(hi):
+            c = hi - 1.0
+        else:
+            c = 0.0
+        return PRIOR_KINDS["host"], [lo, hi, c, 0.0]
+
+    def _device_family_params(self):
+        """[shape..., loc, scale] padded to 4, or None if the kernels have no
+        implementation of this distribution (or its parametrisation)."""
+        if self.name not in _DEVICE_FAMILIES:
             return None
-        nshape = self._SHAPES[self.name]
-        dist = self.distribution
-        shapes = list(dist.args[:nshape])
-        rest = list(dist.args[nshape:])
-        kw = dict(dist.kwds)
-        shape_names = {"lognorm": ["s"], "gamma": ["a"], "beta": ["a", "b"]}
-        for nm in shape_names.get(self.name, [])[len(shapes):]:
+        shape_names = _DEVICE_FAMILIES[self.name]
+        frozen = self.distribution
+        pos = list(frozen.args)
+        kw = dict(frozen.kwds)
+        shapes = pos[:len(shape_names)]
+        for nm in shape_names[len(shapes):]:
             if nm not in kw:
                 return None
             shapes.append(kw.pop(nm))
-        loc = rest[0] if len(rest) > 0 else kw.pop("loc", 0.0)
+        rest = pos[len(shape_names):]
+        loc = rest[0] if rest else kw.pop("loc", 0.0)
         scale = rest[1] if len(rest) > 1 else kw.pop("scale", 1.0)
         if kw:
             return None
-        p = [float(v) for v in shapes] + [float(loc), float(scale)]
-        p += [0.0] * (4 - len(p))
-        return PRIOR_KINDS[self.name], p
+        vals = [float(v) for v in (*shapes, loc, scale)]
+        return vals + [0.0] * (4 - len(vals))
 
+    def host_logpdf(self, x):
+        """Vectorised log density (log pmf for discrete families)."""
+        x = np.asarray(x, dtype=np.float64)
+        if self.is_discrete:
+            return self.distribution.logpmf(x)
+        return self.distribution.logpdf(x)
 
-class RVDecorator(RVBase):
-    def __init__(self, component: RVBase):
-        self.component = component
-
-    def rvs(self, *args, **kwargs):
-        return self.component.rvs(*args, **kwargs)
-
-    def pmf(self, x, *args, **kwargs):
-        return self.component.pmf(x, *args, **kwargs)
-
-    def pdf(self, x, *args, **kwargs):
-        return self.component.pdf(x, *args, **kwargs)
-
-    def cdf(self, x, *args, **kwargs):
-        return self.component.cdf(x, *args, **kwargs)
-
-    def copy(self):
-        return self.__class__(self.component.copy())
-
-    def decorator_repr(self):
-        return "Decorator"
-
-    def __repr__(self):
-        return f"[{self.decorator_repr()}]" + self.component.__repr__()
-
-    def device_spec(self):
-        return None
-
-
-class LowerBoundDecorator(RVDecorator):
-    """pyabc/random_variables.py:263-325 (host only)."""
-    MAX_TRIES = 10000
-
-    def __init__(self, component: RV, lower_bound: float):
-        if component.cdf(lower_bound) == 1:
-            raise Exception(
-                "LowerBoundDecorator: Conditioning on a set of measure zero.")
-        self.lower_bound = lower_bound
-        super().__init__(component)
-
-    def copy(self):
-        return self.__class__(self.component.copy(), self.lower_bound)
-
-    def decorator_repr(self):
-        return "Lower: X > {lower:2f}".format(lower=self.lower_bound)
-
-    def rvs(self, *args, **kwargs):
-        for _ in range(LowerBoundDecorator.MAX_TRIES):
-            sample = self.component.rvs()
-            if not (sample <= self.lower_bound):
-                return sample
-        return None
-
-    def pdf(self, x, *args, **kwargs):
-        if x <= self.lower_bound:
-            return 0.
-        return (self.component.pdf(x)
-                / (1 - self.component.cdf(self.lower_bound)))
-
-    def pmf(self, x, *args, **kwargs):
-        if x <= self.lower_bound:
-            return 0.
-        return (self.component.pmf(x)
-                / (1 - self.component.cdf(self.lower_bound)))
-
-    def cdf(self, x, *args, **kwargs):
-        if x <= self.lower_bound:
-            return 0.
-        lower_mass = self.component.cdf(self.lower_bound)
-        return (self.component.cdf(x) - lower_mass) / (1 - lower_mass)
+    def host_ppf(self, u):
+        return np.asarray(self.distribution.ppf(np.asarray(u, np.float64)),
+                          dtype=np.float64)
 
 
 class Distribution(ParameterStructure):
-    """Independent product of RVs: the prior of a model."""
+    """Independent product of RVs over named parameters: a model's prior
+    (random_variables.py:328-452)."""
 
     def __repr__(self):
-        return "<Distribution {keys}>".format(
-            keys=str(list(self.get_parameter_names()))[1:-1])
+        return "<Distribution {}>".format(str(list(self.get_parameter_names()))[1:-1])
 
     @classmethod
     def from_dictionary_of_dictionaries(cls, dict_of_dicts: dict):
-        return cls({key: RV.from_dictionary(value)
-                    for key, value in dict_of_dicts.items()})
+        return cls({key: RV.from_dictionary(spec) for key, spec in dict_of_dicts.items()})
 
     def copy(self):
-        return self.__class__(**{key: value.copy()
-                                 for key, value in self.items()})
+        return self.__class__(**{key: rv.copy() for key, rv in self.items()})
 
     def update_random_variables(self, **random_variables):
         self.update(random_variables)
@@ -209,70 +192,74 @@ class Distribution(ParameterStructure):
         return sorted(self.keys())
 
     def rvs(self) -> Parameter:
-        return Parameter(**{key: val.rvs() for key, val in self.items()})
+        return Parameter(**{key: rv.rvs() for key, rv in self.items()})
 
     def pdf(self, x):
+        """Product of the component densities (pmf where a component has no
+        pdf); the keys of x must be the prior's."""
         if sorted(x.keys()) != sorted(self.keys()):
-            raise Exception("Random variable parameter mismatch. Expected: " +
-                            str(sorted(self.keys())) +
-                            " got " + str(sorted(x.keys())))
-        if len(self) > 0:
-            res = []
-            for key, val in x.items():
-                try:
-                    res.append(self[key].pdf(val))
-                except AttributeError:
-                    res.append(self[key].pmf(val))
-            return reduce(lambda s, t: s * t, res)
-        return 1
+            raise Exception("Random variable parameter mismatch. Expected: "
+                            + str(sorted(self.keys())) + " got " + str(sorted(x.keys())))
+        dens = None
+        for key, value in x.items():
+            rv = self[key]
+            try:
+                term = rv.pdf(value)
+            except AttributeError:
+                term = rv.pmf(value)
+            dens = term if dens is None else dens * term
+        return 1 if dens is None else dens
 
+    # -- batched-sampler description -----------------------------------------
     def device_spec(self):
         """(kinds [d] int32, params [d*4] float64) in sorted-name order, or
-        None when a component has no device implementation."""
+        None when a component is not a scipy-backed RV."""
         kinds, params = [], []
         for name in self.get_parameter_names():
             rv = self[name]
-            spec = rv.device_spec() if hasattr(rv, "device_spec") else None
-            if spec is None:
+            if not hasattr(rv, "device_spec"):
                 return None
-            kinds.append(spec[0])
-            params.extend(spec[1])
+            kind, par = rv.device_spec()
+            kinds.append(kind)
+            params.extend(par)
         return np.asarray(kinds, dtype=np.int32), np.asarray(params, np.float64)
 
+    def host_components(self):
+        """[(column, RV)] of the components on the host-scipy leg
+        (ABC_PRIOR_HOST), columns in sorted-name order."""
+        from ._native import PRIOR_KINDS
+        out = []
+        for col, name in enumerate(self.get_parameter_names()):
+            rv = self[name]
+            if hasattr(rv, "device_spec") and rv.device_spec()[0] == PRIOR_KINDS["host"]:
+                out.append((col, rv))
+        return out
 
-class ModelPerturbationKernel:
-    """pyabc/random_variables.py:455-538."""
 
-    def __init__(self, nr_of_models: int, probability_to_stay=None):
-        self.nr_of_models = nr_of_models
-        if nr_of_models == 1:
-            self.probability_to_stay = 1
-        else:
-            if probability_to_stay is None:
-                self.probability_to_stay = 1 / nr_of_models
-            else:
-                self.probability_to_stay = min(max(probability_to_stay, 0), 1)
+def host_prior_logpdf(theta, host):
+    """Sum over the host-leg components of their log densities at the rows
+    of the device tensor theta [B, d]; a device tensor [B] (None if there are
+    no host components)."""
+    if not host:
+        return None
+    from . import gpu
+    cols = [c for c, _ in host]
+    vals = theta[:, cols].cpu().numpy()
+    s = np.zeros(vals.shape[0])
+    with np.errstate(divide="ignore"):
+        for q, (_, rv) in enumerate(host):
+            s += rv.host_logpdf(vals[:, q])
+    return gpu.as_dev(s, device=theta.device)
 
-    def _get_discrete_rv(self, m):
-        p_stay = self.probability_to_stay
-        p_move = (1 - p_stay) / (self.nr_of_models - 1)
-        probabilities = [p_stay if n == m else p_move
-                         for n in range(self.nr_of_models)]
-        return RV('rv_discrete',
-                  values=(range(len(probabilities)), probabilities))
 
-    def rvs(self, m: int) -> int:
-        if not 0 <= m <= self.nr_of_models - 1:
-            raise Exception('m has to be between 0 and nr_of_models - 1')
-        if self.nr_of_models == 1:
-            return 0
-        return self._get_discrete_rv(m).rvs()
-
-    def pmf(self, n: int, m: int) -> float:
-        if not (0 <= n <= self.nr_of_models
-                and 0 <= m <= self.nr_of_models - 1):
-            raise Exception(
-                'n and m have to be between 0 and nr_of_models - 1')
-        if self.nr_of_models == 1:
-            return 1 if n == m else 0
-        return self._get_discrete_rv(m).pmf(n)
+def host_prior_draw(theta, att, host, seed, generation, idx0):
+    """Replace the host-leg columns of a t = 0 prior draw (the device wrote a
+    point of the support) by scipy's ppf of the candidate's own uniform from
+    its prior stream (slot of the accepted attempt), in place."""
+    if not host:
+        return theta
+    from . import gpu
+    for col, rv in host:
+        u = gpu.prior_uniforms(att, col, seed, generation, idx0)
+        theta[:, col] = gpu.as_dev(rv.host_ppf(u.cpu().numpy()), device=theta.device)
+    return theta

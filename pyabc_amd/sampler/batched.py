@@ -33,6 +33,7 @@ from .._native import PRIOR_KINDS
 from ..distance.distance import SumStatMatrix
 from ..population import ColumnarParticles, Particle, Population
 from ..parameters import Parameter
+from ..random_variables import host_prior_draw, host_prior_logpdf
 from . import distributed as dd
 from .base import Sampler
 
@@ -103,6 +104,8 @@ class ColumnarSample:
 
 class BatchedGPUSampler(Sampler):
     """Batched, device-resident sampler (single model, nr_samples_per_param 1).
+    Closures outside that (a plain ``simulate_one``, a scalar model, ...) run
+    the reference's per-candidate loop instead (_sample_per_candidate).
 
     Parameters
     ----------
@@ -116,6 +119,10 @@ class BatchedGPUSampler(Sampler):
     check_max_eval: stop a generation once ``max_eval`` candidates are
         evaluated (sample not ok), like the reference samplers' flag of the
         same name (singlecore.py:14-26); off by default, as there.
+    record_device_budget_bytes: optional cap on the HBM the recorded rows of
+        one generation may take (default: none, as in the reference); when
+        hit, the first rows that fit are kept and
+        ``last_stats["records_truncated"]`` is set.
     """
 
     FUSED_MAX_STATS = 256     # abc_candidates_round: S <= SIM_SMAX
@@ -123,7 +130,8 @@ class BatchedGPUSampler(Sampler):
     def __init__(self, batch_size=None, max_batch_size=1 << 22, seed=None,
                  max_attempts=10000, check_max_eval=False, fused=True,
                  max_fused_batch_size=1 << 31, filter_below=0.0,
-                 filter_min_stats=5, record_budget_bytes=1 << 31):
+                 filter_min_stats=5, record_budget_bytes=1 << 31,
+                 record_device_budget_bytes=None):
         super().__init__()
         self.check_max_eval = check_max_eval
         self.batch_size = batch_size
@@ -153,10 +161,14 @@ class BatchedGPUSampler(Sampler):
         # first m recorded candidates are all that is used
         # (ABCSMC.max_nr_recorded_particles, smc.py:998-1001)
         self.max_nr_recorded = np.inf
-        # HBM held by the recorded rows of one generation (all ranks' rows
-        # in global order count); past it the first rows that fit are kept,
-        # as if max_nr_recorded_particles had been set (logged)
-        self.record_device_budget_bytes = 64 << 30
+        # optional cap on the HBM held by the recorded rows of one
+        # generation (all ranks' rows in global order count).  Off by
+        # default: the reference keeps every recorded row (smc.py:987-990),
+        # and a cap would make the adaptive scales depend on the GPU memory
+        # setting.  When set and hit, the first rows that fit are kept, as if
+        # max_nr_recorded_particles had been set: logged, and
+        # last_stats["records_truncated"] is True
+        self.record_device_budget_bytes = record_device_budget_bytes
         self._acc_rate = None
         self.last_stats = {}
 
@@ -177,11 +189,7 @@ class BatchedGPUSampler(Sampler):
                                 all_accepted=False, show_progress=False):
         spec = simulate_one
         if not getattr(spec, "batched_capable", False):
-            raise TypeError(
-                "BatchedGPUSampler needs the GenerationSpec built by "
-                "pyabc_amd.ABCSMC with a VectorizedModel, a device-capable "
-                "prior and transition, and a PNormDistance; got "
-                f"{type(spec).__name__}: {getattr(spec, 'why_not', '')}")
+            return self._sample_per_candidate(n, simulate_one, max_eval)
         dev = gpu.require_device()
         rank, ws = dd.world()
         seed = self._base_seed(dev)
@@ -214,6 +222,10 @@ class BatchedGPUSampler(Sampler):
                                         n_eval, ws)
             lo, _ = dd.rank_range(base, B, rank)
             theta, lp, anc, att = self._propose(spec, B, seed, gen, lo, d)
+            if spec.transition is None and getattr(spec, "host_prior", None):
+                # t = 0: the host-scipy leg draws its coordinates as ppf of
+                # the candidates' own prior-stream uniforms
+                host_prior_draw(theta, att, spec.host_prior, seed, gen, lo)
             x = spec.model.simulate_batch(theta, seed, gen, lo)
             if all_accepted or spec.distance is None:
                 dist = gpu.torch.full((B,), np.inf, dtype=gpu.F64, device=dev)
@@ -224,12 +236,24 @@ class BatchedGPUSampler(Sampler):
                                                  spec.sum_stat_keys)
                 # a proposal that exhausted max_attempts never enters the
                 # population (the reference loops until the prior density is
-                # positive, smc.py:649-662)
+                # positive, smc.py:649-662): its distance becomes NaN (never
+                # <= eps, even at eps = inf); under a StochasticAcceptor the
+                # "distance" is a density, so it becomes the zero-probability
+                # density instead (acceptance 0, weight 0, and a zero
+                # acceptance base in the temperature records)
                 if att is not None:
-                    gpu.mask_gave_up(dist, att, self.max_attempts)
+                    if stochastic:
+                        gpu.mask_gave_up(dist, att, self.max_attempts,
+                                         -np.inf if spec.stochastic[2] else 0.0)
+                    else:
+                        gpu.mask_gave_up(dist, att, self.max_attempts)
                 if stochastic:
                     key, accw = gpu.stochastic_accept(dist, *spec.stochastic,
                                                       seed, gen, lo)
+                    if att is not None:
+                        # key +inf: never accepted, and marks the row for
+                        # ABCSMC._device_records, which leaves it out
+                        gpu.mask_gave_up(key, att, self.max_attempts, np.inf)
                     idx, cnt = gpu.accept_compact(key, 0.0)
                 else:
                     idx, cnt = gpu.accept_compact(dist, spec.eps)
@@ -294,7 +318,8 @@ class BatchedGPUSampler(Sampler):
             self._acc_rate = max(tot_cnt / float(ws * B), 1e-6)
         self.nr_evaluations_ = int(n_eval)
         self.last_stats = dict(rounds=rounds, evaluations=int(n_eval),
-                               accepted=int(n_acc))
+                               accepted=int(n_acc),
+                               records_truncated=self._records_truncated)
         if n_acc < n:
             ok = False
         cols = self._assemble(spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
@@ -314,6 +339,39 @@ class BatchedGPUSampler(Sampler):
         return ColumnarSample(cols, recorded, spec.sum_stat_keys,
                               record, ok and n_acc == n, records=records)
 
+    def _sample_per_candidate(self, n, simulate_one, max_eval):
+        """A closure the batched kernels cannot run -- a plain
+        ``simulate_one``, or a GenerationSpec whose model is not vectorised,
+        whose distance or acceptor has no device form, ... (``why_not``) --
+        goes through the reference's per-candidate loop
+        (sampler/base.py:172-214, singlecore.py:20-38): candidates one at a
+        time until n are accepted, each candidate's transition, prior and
+        distance still calling the device kernels where they have them (a
+        batch of one).  With several ranks rank 0 runs the loop and the
+        sample is broadcast, so every rank holds the same population."""
+        why = getattr(simulate_one, "why_not", "")
+        logger.info("BatchedGPUSampler: per-candidate loop (%s)",
+                    why or type(simulate_one).__name__)
+        rank, ws = dd.world()
+        res = None
+        if rank == 0:
+            sample = self._create_empty_sample()
+            n_eval = 0
+            while sample.n_accepted < n:
+                if self.check_max_eval and n_eval >= max_eval:
+                    break
+                particle = simulate_one()
+                n_eval += 1
+                sample.append(particle)
+            if sample.n_accepted < n:
+                sample.ok = False
+            res = (sample, n_eval)
+        sample, n_eval = dd.broadcast_object(res)
+        self.nr_evaluations_ = int(n_eval)
+        self.last_stats = dict(rounds=0, evaluations=int(n_eval),
+                               accepted=int(sample.n_accepted), per_candidate=True)
+        return sample
+
     # ---- fused candidate rounds ------------------------------------------
     def _fused_round(self, spec, seed, gen, dev):
         """gpu.CandidateRound of this generation, or None when some piece has
@@ -321,6 +379,8 @@ class BatchedGPUSampler(Sampler):
         if not self.fused or getattr(spec, "stochastic", None) is not None \
                 or spec.distance is None:
             return None
+        if spec.transition is None and getattr(spec, "host_prior", None):
+            return None     # t = 0 draws of host-leg coordinates: staged path
         sim = (spec.model.fused_simulator(dev)
                if hasattr(spec.model, "fused_simulator") else None)
         fp = (spec.distance.fused_pnorm(spec.t, spec.sum_stat_keys, dev)
@@ -384,6 +444,10 @@ class BatchedGPUSampler(Sampler):
         return int(max(1, min(B, left // ws)))
 
     def _record_limit(self, S):
+        self._records_truncated = False
+        if self.record_device_budget_bytes is None:
+            self._budget_capped = False
+            return self.max_nr_recorded
         budget_rows = self.record_device_budget_bytes // (8 * max(S, 1))
         self._budget_capped = budget_rows < self.max_nr_recorded
         return min(self.max_nr_recorded, budget_rows)
@@ -399,8 +463,11 @@ class BatchedGPUSampler(Sampler):
             out[q] = min(int(rec_all[q]), left)
             left -= int(out[q])
         if left == 0 and out.sum() < rec_all.sum() and self._budget_capped:
-            logger.warning("recorded sum stats exceed record_device_budget_bytes "
-                           "(%d); keeping the first rows only", self.record_device_budget_bytes)
+            if not self._records_truncated:
+                logger.warning("recorded sum stats exceed record_device_budget_bytes "
+                               "(%d); keeping the first rows only",
+                               self.record_device_budget_bytes)
+            self._records_truncated = True
         return out, left
 
     def _sample_fused(self, n, fr, spec, max_eval, record, dev, rank, ws):
@@ -503,7 +570,8 @@ class BatchedGPUSampler(Sampler):
         self.nr_evaluations_ = int(n_eval)
         self.last_stats = dict(rounds=rounds, evaluations=int(n_eval),
                                accepted=int(n_acc), fused=True,
-                               candidates=int(tot_B), filtered_rounds=filtered)
+                               candidates=int(tot_B), filtered_rounds=filtered,
+                               records_truncated=self._records_truncated)
         if n_acc < n:
             ok = False
         out = self._assemble(spec, cols["theta"], cols["lp"], cols["dist"],
@@ -633,6 +701,9 @@ class BatchedGPUSampler(Sampler):
             anc = (cat(acc_anc) if acc_anc and
                    len(acc_anc) == len(acc_theta) else None)
             lt = spec.transition.logpdf_device(theta, hint=anc)
+            hl = host_prior_logpdf(theta, getattr(spec, "host_prior", None))
+            if hl is not None:
+                lp = lp + hl      # the host-scipy leg's density factors
             w = gpu.importance_weights(lp, lt, spec.weight_scale,
                                        acc_w=None if accw is None else accw.contiguous())
         if ws > 1:

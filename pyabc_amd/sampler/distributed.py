@@ -157,13 +157,26 @@ def all_gather_flat(out, t):
     use_comm(RcclComm) device tensors go through libabcgpu's RCCL wrappers."""
     if _comm is not None and t.is_cuda:
         return _comm.all_gather_into(out, t.contiguous())
-    if t.is_cuda and dist.get_backend() == "gloo":
-        host = torch.empty(out.shape, dtype=out.dtype)
-        dist.all_gather_into_tensor(host, t.cpu())
-        out.copy_(host)
-    else:
-        dist.all_gather_into_tensor(out, t)
+    # one collective call for every backend; only gloo with device tensors
+    # stages through host buffers
+    staged = t.is_cuda and dist.get_backend() == "gloo"
+    src = t.cpu() if staged else t
+    dst = torch.empty(out.shape, dtype=out.dtype) if staged else out
+    dist.all_gather_into_tensor(dst, src)
+    if staged:
+        out.copy_(dst)
     return out
+
+
+def broadcast_object(obj):
+    """Rank 0's picklable object on every rank (the per-candidate fallback
+    of BatchedGPUSampler runs on rank 0 only)."""
+    rank, ws = world()
+    if ws == 1:
+        return obj
+    box = [obj if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
 
 
 def broadcast_int(v, device):

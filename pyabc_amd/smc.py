@@ -27,7 +27,7 @@ from .model import Model, SimpleModel, VectorizedModel
 from .parameters import Parameter
 from .population import Particle, Population
 from .populationstrategy import ConstantPopulationSize, PopulationStrategy
-from .random_variables import RV, Distribution, ModelPerturbationKernel
+from .random_variables import RV, Distribution, host_prior_logpdf
 from .sampler import BatchedGPUSampler, Sampler, SingleCoreSampler
 from .storage import History
 from .transition import MultivariateNormalTransition, Transition
@@ -95,9 +95,12 @@ class GenerationSpec:
         if self.transition is not None and not hasattr(self.transition,
                                                        "propose_device"):
             why.append("transition has no device kernel")
-        spec = abc.parameter_priors[0].device_spec()
+        prior = abc.parameter_priors[0]
+        spec = prior.device_spec() if hasattr(prior, "device_spec") else None
         if spec is None:
-            why.append("prior component without a device kernel")
+            why.append("prior component that is not a scipy-backed RV")
+        # components without a device sampler: host-scipy density / draws
+        self.host_prior = prior.host_components() if spec is not None else []
         self.why_not = "; ".join(why)
         self.batched_capable = not why
         if self.batched_capable:
@@ -123,6 +126,41 @@ class GenerationSpec:
             else:
                 self._closure = self._abc._create_simulate_function_closure(self.t)
         return self._closure()
+
+
+class ModelPerturbationKernel:
+    """Model jump of multi-model runs (the role of
+    random_variables.py:455-538 at smc.py:641-649): from model m stay with
+    probability p_stay, else move to one of the other models uniformly.
+    Not on the batched path (single-model generations only)."""
+
+    def __init__(self, nr_of_models: int, probability_to_stay=None):
+        self.nr_of_models = int(nr_of_models)
+        if self.nr_of_models == 1:
+            p = 1.0
+        elif probability_to_stay is None:
+            p = 1.0 / self.nr_of_models
+        else:
+            p = float(np.clip(probability_to_stay, 0.0, 1.0))
+        self.probability_to_stay = p
+
+    def _row(self, m):
+        n = self.nr_of_models
+        if not 0 <= m < n:
+            raise Exception("m has to be between 0 and nr_of_models - 1")
+        if n == 1:
+            return np.ones(1)
+        row = np.full(n, (1.0 - self.probability_to_stay) / (n - 1))
+        row[m] = self.probability_to_stay
+        return row
+
+    def rvs(self, m: int) -> int:
+        row = self._row(int(m))
+        return 0 if row.size == 1 else int(np.random.choice(row.size, p=row))
+
+    def pmf(self, n: int, m: int) -> float:
+        row = self._row(int(m))
+        return float(row[n]) if 0 <= n < row.size else 0.0
 
 
 class ABCSMC:
@@ -359,29 +397,30 @@ class ABCSMC:
     @staticmethod
     def _generate_valid_proposal(t, m, p, model_prior, parameter_priors,
                                  model_perturbation_kernel, transitions):
+        """smc.py:610-662.  t = 0: (model, theta) from the priors.  Later:
+        a source model from the previous generation's probabilities p over
+        the alive models m, moved by the model perturbation kernel (a move to
+        a dead model is simply drawn again), theta from the target model's
+        transition; repeated until the pair has positive prior density."""
         if t == 0:
-            m_ss = int(model_prior.rvs())
-            theta_ss = parameter_priors[m_ss].rvs()
-            return m_ss, theta_ss
-        n_sample, n_sample_soft_limit = 0, 1000
+            model = int(model_prior.rvs())
+            return model, parameter_priors[model].rvs()
+        alive = {int(v) for v in m}
+        zero_density = 0
         while True:
+            model = int(m[0])
             if len(m) > 1:
-                index = int(np.random.choice(len(p), p=p))
-                m_s = m[index]
-                m_ss = model_perturbation_kernel.rvs(m_s)
-                if m_ss not in m:
+                source = int(m[np.random.choice(len(p), p=p)])
+                model = int(model_perturbation_kernel.rvs(source))
+                if model not in alive:
                     continue
-            else:
-                m_ss = m[0]
-            theta_ss = Parameter(**transitions[m_ss].rvs().to_dict())
-            if (model_prior.pmf(m_ss)
-                    * parameter_priors[m_ss].pdf(theta_ss) > 0):
-                return m_ss, theta_ss
-            n_sample += 1
-            if n_sample == n_sample_soft_limit:
-                logger.warning(
-                    "Unusually many (model, parameter) samples have prior "
-                    "density zero. The transition might be inappropriate.")
+            theta = Parameter(**transitions[model].rvs().to_dict())
+            if model_prior.pmf(model) * parameter_priors[model].pdf(theta) > 0:
+                return model, theta
+            zero_density += 1
+            if zero_density == 1000:
+                logger.warning("1000 proposals in a row fell outside the prior "
+                               "support; check the transition's scaling.")
 
     @staticmethod
     def _evaluate_proposal(m_ss, theta_ss, t, nr_samples_per_parameter, models,
@@ -599,11 +638,23 @@ class ABCSMC:
         if rec is None:
             return None
         theta, dist, key, anc = rec
+        # a proposal that exhausted the prior re-draws (key +inf, see
+        # BatchedGPUSampler) is not a candidate the reference could have
+        # recorded (it loops until the prior density is positive,
+        # smc.py:649-662): left out of the records
+        gave_up = key == np.inf
+        if bool(gave_up.any()):
+            keep = ~gave_up
+            theta, dist, key = theta[keep], dist[keep], key[keep]
+            anc = None if anc is None else anc[keep]
         if t - 1 == 0:
             spec = self.parameter_priors[0].device_spec()
             kinds = gpu.as_dev(spec[0], dtype=gpu.torch.int32, device=theta.device)
             lp_prev = gpu.prior_logpdf(theta, kinds,
                                        gpu.as_dev(spec[1], device=theta.device))
+            hl = host_prior_logpdf(theta, self.parameter_priors[0].host_components())
+            if hl is not None:
+                lp_prev = lp_prev + hl
         else:
             tr_prev = prev_transitions[0]
             if not hasattr(tr_prev, "logpdf_device"):

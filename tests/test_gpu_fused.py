@@ -196,17 +196,42 @@ def test_fused_prior_kinds_and_gave_up(dev):
     c["X"] = T(c["host"]["X"])
     lo, B = 77, 60_000
     for max_att in (1000, 2):
-        ref = _staged(c, lo, B, 1e300, max_attempts=max_att)
-        fr = _round(c, max_attempts=max_att)
-        n = _check_equal(c, fr, ref, lo, B, 1e300, False)
-        assert _check_equal(c, fr, ref, lo, B, 1e300, True) == n
-        if max_att == 2:
-            assert 0 < n < B     # some gave up and were rejected
-        assert torch.isfinite(fr.regen(lo, ref["idx"][:1000])[1]).all()
+        # eps = inf too: a proposal that gave up is NaN, never <= eps
+        for eps in (1e300, np.inf):
+            ref = _staged(c, lo, B, eps, max_attempts=max_att)
+            fr = _round(c, max_attempts=max_att)
+            n = _check_equal(c, fr, ref, lo, B, eps, False)
+            assert _check_equal(c, fr, ref, lo, B, eps, True) == n
+            if max_att == 2:
+                assert 0 < n < B     # some gave up and were rejected
+            assert torch.isfinite(fr.regen(lo, ref["idx"][:1000])[1]).all()
     # prior mode (t = 0) with the same bounded kinds
     c0 = _case(6, 6, mode="prior", kinds=kinds, params=params, seed=9)
     ref = _staged(c0, lo, B, 1e300)
     _check_equal(c0, _round(c0), ref, lo, B, 1e300, False)
+
+
+@pytest.mark.parametrize("p", [2.0, 1.0, np.inf, 3.0])
+def test_fused_eps_on_a_distance(dev, p):
+    """eps equal to some candidates' distances exactly: those candidates are
+    accepted (d <= eps) by the round's accept bit and by the staged
+    pipeline alike, and their regenerated distances are <= eps -- the round
+    (p = 2: pnorm_acc<2>), the regeneration and the staged p-norm must
+    round identically (no contraction anywhere, abc_candidate.h)."""
+    c = _case(10, 10, p=p, seed=21)
+    lo, B = 5_000, 80_000
+    d = _staged(c, lo, B, np.inf)["dist"].cpu().numpy()
+    fr = _round(c)
+    for q in (100, 1000, 5000, 20000):
+        eps = float(np.sort(d[np.isfinite(d)])[q])
+        ref = _staged(c, lo, B, eps)
+        hit = np.nonzero(d == eps)[0]
+        assert len(hit) >= 1
+        assert set(hit.tolist()) <= set(ref["idx"].cpu().numpy().tolist())
+        n = _check_equal(c, fr, ref, lo, B, eps, False)
+        assert n >= q + 1
+        dist = fr.regen(lo, ref["idx"][:n])[4]
+        assert bool((dist <= eps).all())
 
 
 @pytest.mark.parametrize("variant", ["wide_uniform", "narrow_uniform", "src_late",

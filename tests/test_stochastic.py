@@ -375,6 +375,46 @@ def test_stochastic_abc_exact_posterior_batched():
 
 
 @gpu_mark
+def test_stochastic_abc_gave_up_proposals():
+    """A narrow bounded prior with max_attempts = 2: some proposals exhaust
+    their prior re-draws.  Under a StochasticAcceptor the "distance" is a
+    density, so such a proposal must get the zero-probability density (never
+    accepted, acceptance weight 0) and stay out of the temperature records --
+    not +inf, which would accept it with an infinite weight and NaN the
+    population's normalisation."""
+    import pyabc_amd as pa
+    from pyabc_amd import gpu
+    np.random.seed(3)
+    model = pa.LinearGaussianModel(["x"], ["y"], src=[0], sigma=[0.0])
+    prior = pa.Distribution(x=pa.RV("uniform", 1.2, 0.3))
+    sampler = pa.BatchedGPUSampler(seed=91, max_attempts=2)
+    abc = pa.ABCSMC(model, prior, pa.IndependentNormalKernel(var=[0.25]),
+                    population_size=3000, sampler=sampler,
+                    eps=pa.Temperature(), acceptor=pa.StochasticAcceptor())
+    abc.new("sqlite://", {"y": 2.0})
+    gave_up = []
+    orig = gpu.mask_gave_up
+
+    def spy(dist, att, max_attempts, value=float("nan")):
+        gave_up.append(int((att > max_attempts).sum()))
+        return orig(dist, att, max_attempts, value)
+    gpu.mask_gave_up = spy
+    try:
+        h = abc.run(max_nr_populations=4)
+    finally:
+        gpu.mask_gave_up = orig
+    assert sum(gave_up) > 0
+    for t in range(h.max_t + 1):
+        df, w = h.get_distribution(0, t)
+        assert np.isfinite(w).all() and (w > 0).all()
+        np.testing.assert_allclose(w.sum(), 1.0, rtol=1e-12)
+        x = df["x"].to_numpy()
+        assert ((x >= 1.2) & (x <= 1.5)).all()
+    temps = abc.eps.temperatures
+    assert all(np.isfinite(v) and v >= 1.0 for v in temps.values())
+
+
+@gpu_mark
 def test_stochastic_abc_per_particle_and_pdf_norms():
     """test_acceptor.py:72-128 on the per-particle path (array-valued sum
     stats, user model) for every pdf normalisation."""
