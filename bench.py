@@ -229,7 +229,9 @@ def measured_traffic(args, n_pop):
     import glob
     if args.precision != "x3":
         return None, None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_x3_traffic_*.json"))):
+    # newest round first (profiles/rNN_...): the kernel that runs is HEAD's
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_x3_traffic_*.json")),
+                    reverse=True):
         try:
             t = json.load(open(f))
         except (OSError, ValueError):
@@ -331,9 +333,11 @@ def main():
             "candidates_per_s": n_cand / (c_ms * 1e-3) if c_ms else None,
             "bytes_per_candidate": {"written": 0.125,
                                     "read_cached": 8 * (args.dim + 3) + 8},
-            "bound": ("VALU issue: ~1460 VALU instructions per candidate "
-                      "(PMC, profiles/r02_fused_pmc.txt): Philox4x32-10 + "
-                      "fp64 Box-Muller dominate; not HBM"),
+            "bound": ("random accesses + VALU issue, not HBM: per candidate "
+                      "1.67 L2 misses + 0.88 L2 hits (ancestor guide entry + "
+                      "record) at c3's skewed weights and ~1380 VALU lane-"
+                      "instructions (Philox4x32-10 and the fp32 Box-Muller "
+                      "transform); PMC in profiles/r03_fused_pmc_skewed_w.txt"),
             "candidates_per_generation": timed_cands}
     # unique bytes one launch must move: the population and candidate
     # operand images (KB blocks of 32 f16 per row) + the fp64 result
@@ -346,22 +350,30 @@ def main():
         if not args.no_cpu_baseline and ws == 1:
             hist = abc.history
             df, w = hist.get_distribution(0, hist.max_t)
-            acc_rate = n_pop / gens[-1]["n_sim"]
             cores = max(1, min(args.cpu_cores, os.cpu_count() or 1))
             cand_rate, pdf_rate, n_c, n_p = cpu_baseline(
                 args, (df.values, w), tr.cov, args.cpu_baseline_seconds, cores)
-            # per accepted particle: 1/acceptance candidates + one density
-            per_acc = 1.0 / (cand_rate * acc_rate) + 1.0 / pdf_rate
-            cpu = {"value": 1.0 / per_acc, "unit": "accepted particles/s",
+            # the same generations as the GPU value: per timed generation its
+            # evaluated candidates (n_sim, at that generation's acceptance)
+            # and one transition density per accepted particle; value = all
+            # accepted particles / the summed CPU time
+            cpu_s = sum(g["n_sim"] / cand_rate + n_pop / pdf_rate for g in gens)
+            acc_last = n_pop / gens[-1]["n_sim"]
+            last = 1.0 / (1.0 / (cand_rate * acc_last) + 1.0 / pdf_rate)
+            cpu = {"value": steps * n_pop / cpu_s, "unit": "accepted particles/s",
                    "cores": cores, "kind": "port",
                    "sample": (f"oracle (numpy fp64 restatement) on {cores} worker "
                               f"processes of this host, MulticoreEval-shaped: "
                               f"{n_c} candidates (rvs, prior, simulate, distance) "
                               f"at {cand_rate:.3e}/s and {n_p} transition densities "
-                              f"vs the full N={n_pop} population at {pdf_rate:.3e}/s, "
-                              f"combined at the last timed generation's acceptance "
-                              f"rate {acc_rate:.3e}; the reference's own samplers are "
-                              f"slower than this port by the ratio in BASELINE.md §3"),
+                              f"vs the full N={n_pop} population at {pdf_rate:.3e}/s; "
+                              f"value = the timed generations' accepted particles "
+                              f"over the CPU time of their own candidate counts "
+                              f"(n_sim, acceptance {n_pop / gens[0]['n_sim']:.2e} .. "
+                              f"{acc_last:.2e}) and densities; the reference's own "
+                              f"samplers are slower than this port by the ratio in "
+                              f"BASELINE.md §3"),
+                   "value_last_generation": last,
                    "candidates_per_s": cand_rate, "densities_per_s": pdf_rate}
         out = {
             "metric": "accepted particles/sec/generation",

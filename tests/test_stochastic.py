@@ -388,9 +388,12 @@ def test_stochastic_abc_gave_up_proposals():
     model = pa.LinearGaussianModel(["x"], ["y"], src=[0], sigma=[0.0])
     prior = pa.Distribution(x=pa.RV("uniform", 1.2, 0.3))
     sampler = pa.BatchedGPUSampler(seed=91, max_attempts=2)
+    # a wide perturbation kernel: many proposals leave the narrow support
     abc = pa.ABCSMC(model, prior, pa.IndependentNormalKernel(var=[0.25]),
                     population_size=3000, sampler=sampler,
-                    eps=pa.Temperature(), acceptor=pa.StochasticAcceptor())
+                    transitions=pa.MultivariateNormalTransition(scaling=50),
+                    eps=pa.Temperature(initial_temperature=8.0),
+                    acceptor=pa.StochasticAcceptor())
     abc.new("sqlite://", {"y": 2.0})
     gave_up = []
     orig = gpu.mask_gave_up
@@ -410,6 +413,7 @@ def test_stochastic_abc_gave_up_proposals():
         np.testing.assert_allclose(w.sum(), 1.0, rtol=1e-12)
         x = df["x"].to_numpy()
         assert ((x >= 1.2) & (x <= 1.5)).all()
+    assert h.max_t >= 1
     temps = abc.eps.temperatures
     assert all(np.isfinite(v) and v >= 1.0 for v in temps.values())
 
