@@ -209,6 +209,7 @@ class BatchedGPUSampler(Sampler):
         keeps = []          # per round: accepted rows kept by each rank
         rec_keeps = []      # per round: recorded rows of each rank
         rec_left = self._record_limit(len(spec.sum_stat_keys))
+        cut = None          # ws > 1: the last round's cutoff, resolved in _assemble
         n_acc = 0
         base = 0
         n_eval = 0
@@ -276,14 +277,17 @@ class BatchedGPUSampler(Sampler):
             rec_all = np.full(ws, B, dtype=np.int64)
             if n_acc + total_keep >= n:
                 c_rank = int(np.nonzero(keep)[0][-1])
-                if ws == 1 and not (all_accepted or spec.distance is None):
-                    pos = pos_hint
+                if ws > 1:
+                    # the cutoff position travels in the generation's packed
+                    # row gather (_assemble), not in a collective of its own
+                    cut = self._pending_cut(idx, keep, c_rank, rank, B, dev)
+                    evaluated = 0
                 else:
-                    pos = self._local_cutoff_pos(idx, keep[c_rank]) if rank == c_rank else -1
-                    pos = dd.allgather_counts(pos, dev)[c_rank]
-                evaluated = c_rank * B + pos + 1
-                rec_all[c_rank] = pos + 1
-                rec_all[c_rank + 1:] = 0
+                    pos = (pos_hint if not (all_accepted or spec.distance is None)
+                           else self._local_cutoff_pos(idx, keep[c_rank]))
+                    evaluated = c_rank * B + pos + 1
+                    rec_all[c_rank] = pos + 1
+                    rec_all[c_rank + 1:] = 0
             else:
                 evaluated = ws * B
             rec_rows = int(rec_all[rank])
@@ -300,7 +304,13 @@ class BatchedGPUSampler(Sampler):
                     acc_anc.append(got[4])
                 if stochastic:
                     acc_w.append(got[-1])
-            if record:
+            if record and cut is not None:
+                # rows trimmed once the cutoff position is known (_finish_cut)
+                rec_x.append(x)
+                rec_keeps.append(None)
+                if rec_extra is not None:
+                    rec_extra.append((theta, dist, key, anc))
+            elif record:
                 rec_all, rec_left = self._cap_records(rec_all, rec_left)
                 rec_rows = int(rec_all[rank])
                 rec_x.append(x[:rec_rows].clone() if rec_rows < B // 2 else x[:rec_rows])
@@ -316,14 +326,18 @@ class BatchedGPUSampler(Sampler):
             rounds += 1
             tot_cnt = int(counts.sum())
             self._acc_rate = max(tot_cnt / float(ws * B), 1e-6)
+        if n_acc < n:
+            ok = False
+        cols = self._assemble(spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
+                              all_accepted, keeps, acc_anc, acc_w, cut=cut)
+        if cut is not None:
+            n_eval, rec_left = self._finish_cut(cut, n_eval, rec_left, rec_keeps,
+                                                rec_x if record else None,
+                                                rec_extra, rank, ws)
         self.nr_evaluations_ = int(n_eval)
         self.last_stats = dict(rounds=rounds, evaluations=int(n_eval),
                                accepted=int(n_acc),
                                records_truncated=self._records_truncated)
-        if n_acc < n:
-            ok = False
-        cols = self._assemble(spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
-                              all_accepted, keeps, acc_anc, acc_w)
         recorded = None
         records = None
         if record:
@@ -482,6 +496,7 @@ class BatchedGPUSampler(Sampler):
         arena, arena_off = None, 0
         kept, kept_off = None, 0
         rec_left = self._record_limit(S)
+        cut = None
         n_acc = n_eval = base = rounds = 0
         ok = True
         rate, measured = self._acc_rate, False
@@ -522,14 +537,14 @@ class BatchedGPUSampler(Sampler):
             rec_all = np.full(ws, B, dtype=np.int64)
             if n_acc + total_keep >= n:
                 c_rank = int(np.nonzero(keep)[0][-1])
-                if ws == 1:
-                    pos = pos_hint
+                if ws > 1:
+                    cut = self._pending_cut(idx, keep, c_rank, rank, B, dev)
+                    evaluated = 0
                 else:
-                    pos = self._local_cutoff_pos(idx, keep[c_rank]) if rank == c_rank else -1
-                    pos = dd.allgather_counts(pos, dev)[c_rank]
-                evaluated = c_rank * B + pos + 1
-                rec_all[c_rank] = pos + 1
-                rec_all[c_rank + 1:] = 0
+                    pos = pos_hint
+                    evaluated = c_rank * B + pos + 1
+                    rec_all[c_rank] = pos + 1
+                    rec_all[c_rank + 1:] = 0
             else:
                 evaluated = ws * B
             if k_mine:
@@ -549,7 +564,10 @@ class BatchedGPUSampler(Sampler):
                 for k, v in zip(("theta", "lp", "dist", "x", "anc"),
                                 (th, lp, dist, x, anc)):
                     cols[k].append(v)
-            if record:
+            if record and cut is not None and rx is not None:
+                rec_x.append(rx)            # trimmed in _finish_cut
+                rec_keeps.append(None)
+            elif record:
                 if rx is None:
                     rec_all = np.zeros(ws, dtype=np.int64)
                 rec_all, rec_left = self._cap_records(rec_all, rec_left)
@@ -567,16 +585,21 @@ class BatchedGPUSampler(Sampler):
             tot_cnt += int(counts.sum())
             rate, measured = max(int(counts.sum()) / float(ws * B), 1e-12), True
         self._acc_rate = max(tot_cnt / float(max(tot_B, 1)), 1e-12)
+        if n_acc < n:
+            ok = False
+        out = self._assemble(spec, cols["theta"], cols["lp"], cols["dist"],
+                             cols["x"], dev, fr.d, False, keeps,
+                             cols["anc"] if spec.transition is not None else (),
+                             cut=cut)
+        if cut is not None:
+            n_eval, rec_left = self._finish_cut(cut, n_eval, rec_left, rec_keeps,
+                                                rec_x if record else None, None,
+                                                rank, ws)
         self.nr_evaluations_ = int(n_eval)
         self.last_stats = dict(rounds=rounds, evaluations=int(n_eval),
                                accepted=int(n_acc), fused=True,
                                candidates=int(tot_B), filtered_rounds=filtered,
                                records_truncated=self._records_truncated)
-        if n_acc < n:
-            ok = False
-        out = self._assemble(spec, cols["theta"], cols["lp"], cols["dist"],
-                             cols["x"], dev, fr.d, False, keeps,
-                             cols["anc"] if spec.transition is not None else ())
         recorded = None
         if record:
             recorded = self._gather_recorded(rec_x, rec_keeps, dev, ws)
@@ -616,6 +639,43 @@ class BatchedGPUSampler(Sampler):
     @staticmethod
     def _local_cutoff_pos(idx, k):
         return int(idx[int(k) - 1].item())
+
+    @staticmethod
+    def _pending_cut(idx, keep, c_rank, rank, B, dev):
+        """The completing round of a multi-rank generation: the cut rank's
+        local position of its last kept candidate stays on the device (no
+        host read, no collective of its own) and rides in the packed row
+        gather of _assemble; every other rank sends -1."""
+        torch = gpu.torch
+        if rank == c_rank:
+            k = int(keep[c_rank])
+            pos = idx[k - 1:k].to(gpu.F64)
+        else:
+            pos = torch.full((1,), -1.0, dtype=gpu.F64, device=dev)
+        return dict(c_rank=c_rank, B=int(B), pos=pos)
+
+    def _finish_cut(self, cut, n_eval, rec_left, rec_keeps, rec_x, rec_extra,
+                    rank, ws):
+        """Resolve the pending cutoff once _assemble has gathered the cut
+        rank's position: evaluations up to the n-th accepted (global order),
+        the last round's recorded rows per rank (capped like every round), and
+        this rank's recorded pieces of that round trimmed to them."""
+        c_rank, B = cut["c_rank"], cut["B"]
+        pos = int(cut["gathered"][c_rank])
+        n_eval += c_rank * B + pos + 1
+        if rec_x is not None and rec_keeps and rec_keeps[-1] is None:
+            rec_all = np.full(ws, B, dtype=np.int64)
+            rec_all[c_rank] = pos + 1
+            rec_all[c_rank + 1:] = 0
+            rec_all, rec_left = self._cap_records(rec_all, rec_left)
+            rr = int(rec_all[rank])
+            rec_keeps[-1] = rec_all
+            if rec_x and rec_x[-1].shape[0] != rr:
+                rec_x[-1] = rec_x[-1][:rr]
+            if rec_extra:
+                rec_extra[-1] = tuple(None if a is None else a[:rr]
+                                      for a in rec_extra[-1])
+        return n_eval, rec_left
 
     def _propose(self, spec, B, seed, gen, lo, d):
         if spec.transition is None:
@@ -669,7 +729,7 @@ class BatchedGPUSampler(Sampler):
         return gpu.torch.cat([t[a:a + n] for a, n in pieces], 0)
 
     def _assemble(self, spec, acc_theta, acc_lp, acc_d, acc_x, dev, d,
-                  all_accepted, keeps, acc_anc=(), acc_w=()):
+                  all_accepted, keeps, acc_anc=(), acc_w=(), cut=None):
         rank, ws = dd.world()
         torch = gpu.torch
         def cat(lst):
@@ -710,12 +770,22 @@ class BatchedGPUSampler(Sampler):
             # one packed all-gather; the rows come back in global
             # candidate-index order so the population (and every later draw
             # keyed on it) is the same for any number of ranks
+            # (the cut rank's cutoff position rides in the same collective)
             parts = [theta, w, dist, x]
+            extra = None if cut is None else cut["pos"]
             if len({a.dtype for a in parts}) == 1:
-                theta, w, dist, x = dd.allgather_rows_ordered(parts, keeps, dev)
+                got = dd.allgather_rows_ordered(parts, keeps, dev, extra=extra)
             else:
-                theta, w, dist, x = (dd.allgather_rows_ordered([a], keeps, dev)[0]
-                                     for a in parts)
+                got = [dd.allgather_rows_ordered([a], keeps, dev,
+                                                 extra=extra if i == 0 else None)
+                       for i, a in enumerate(parts)]
+                if extra is not None:
+                    got = ([got[0][0][0]] + [g[0] for g in got[1:]], got[0][1])
+                else:
+                    got = [g[0] for g in got]
+            if extra is not None:
+                got, cut["gathered"] = got
+            theta, w, dist, x = got
         if theta.shape[0] == 0:
             return None
         return ColumnarParticles(theta.contiguous(), w.contiguous(),

@@ -84,9 +84,13 @@ def allgather_rows(t, device):
     return torch.cat([o[: int(k)] for o, k in zip(out, n)], dim=0)
 
 
-def allgather_rows_ordered(tensors, keeps, device):
+def allgather_rows_ordered(tensors, keeps, device, extra=None):
     """All-gather several per-rank row blocks in ONE collective and return
     them in global candidate-index order.
+
+    ``extra``: an optional 1-element f64 tensor per rank (the sampler's
+    cutoff position of the generation's last round) carried in one more row
+    of the same collective; the call then returns (rows, extras[ws]).
 
     tensors: list of same-dtype tensors [n_mine, c_i] or [n_mine] with the
     same leading size (this rank's rows, round after round); keeps: [rounds x
@@ -101,6 +105,8 @@ def allgather_rows_ordered(tensors, keeps, device):
     rank, ws = world()
     k = np.asarray(keeps, dtype=np.int64).reshape(len(keeps), -1)
     if ws == 1:
+        if extra is not None:
+            return list(tensors), extra.reshape(1).to(torch.float64).cpu().numpy()
         return list(tensors)
     per_rank = k.sum(0)
     nmax = int(per_rank.max()) if per_rank.size else 0
@@ -114,12 +120,15 @@ def allgather_rows_ordered(tensors, keeps, device):
     if n_mine != int(per_rank[rank]):
         raise AssertionError(
             f"rank {rank}: {n_mine} rows, cutoff says {int(per_rank[rank])}")
-    pad = torch.zeros((max(nmax, 1), C), dtype=cols[0].dtype, device=cols[0].device)
+    rows = max(nmax, 1) + (1 if extra is not None else 0)
+    pad = torch.zeros((rows, C), dtype=cols[0].dtype, device=cols[0].device)
     c0 = 0
     for c, wdt in zip(cols, widths):
         if n_mine:
             pad[:n_mine, c0:c0 + wdt] = c
         c0 += wdt
+    if extra is not None:
+        pad[rows - 1, :1] = extra.reshape(1).to(pad.dtype)
     out = torch.empty((ws * pad.shape[0], C), dtype=pad.dtype, device=pad.device)
     all_gather_flat(out, pad)
     # piece (round r, rank q) starts at q * nmax + rows q kept in rounds < r
@@ -135,6 +144,9 @@ def allgather_rows_ordered(tensors, keeps, device):
         piece = full[:, c0:c0 + wdt]
         res.append(piece.reshape((full.shape[0],) + tuple(t.shape[1:])).contiguous())
         c0 += wdt
+    if extra is not None:
+        ex = out.view(ws, rows, C)[:, rows - 1, 0].cpu().numpy()
+        return res, ex
     return res
 
 

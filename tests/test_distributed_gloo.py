@@ -170,7 +170,21 @@ def _run(n, eps, batch, record, fused=False):
     return dict(theta=c.theta.numpy(), w=c.weights.numpy(),
                 d=c.distances.numpy(), x=c.sum_stats.numpy(),
                 n_eval=np.array(s.nr_evaluations_),
+                rounds=np.array(s.last_stats["rounds"]),
                 rec=(rec.numpy() if rec is not None else np.zeros(0)))
+
+
+def _count_collectives():
+    """Wrap the all-gathers the sampler may call; returns the call counter."""
+    calls = {"n": 0}
+    for name in ("all_gather", "all_gather_into_tensor"):
+        f = getattr(dist, name)
+
+        def wrapped(*a, _f=f, **k):
+            calls["n"] += 1
+            return _f(*a, **k)
+        setattr(dist, name, wrapped)
+    return calls
 
 
 def _worker(rank, ws, port, out_dir, n, eps, batch, record, fused=False):
@@ -178,32 +192,39 @@ def _worker(rank, ws, port, out_dir, n, eps, batch, record, fused=False):
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
         _install_cpu_doubles(setattr)
+        calls = _count_collectives()
         res = _run(n, eps, batch, record, fused)
+        res["collectives"] = np.array(calls["n"])
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("fused", [False, True])
-@pytest.mark.parametrize("n,batch,record", [(300, 256, True), (37, 64, False),
-                                            (1, 128, True)])
-def test_sharded_sampler_matches_single_rank(monkeypatch, n, batch, record, fused):
-    """Staged and fused sampler loops: 2 gloo ranks == 1 rank, and the
-    fused loop == the staged loop (same streams, same cutoff)."""
+@pytest.mark.parametrize("n,batch,record,ws", [(300, 256, True, 2), (37, 64, False, 2),
+                                               (1, 128, True, 2), (300, 128, True, 4),
+                                               (5, 64, True, 4)])
+def test_sharded_sampler_matches_single_rank(monkeypatch, n, batch, record, ws, fused):
+    """Staged and fused sampler loops: 2 and 4 gloo ranks == 1 rank, and the
+    fused loop == the staged loop (same streams, same cutoff).  n = 1 and 5
+    leave the later ranks with no kept rows.  Collectives: one count gather
+    per round, then ONE packed row gather that also carries the cutoff
+    position (+ one for the recorded rows)."""
     eps = 1.6
     _install_cpu_doubles(monkeypatch.setattr)
-    ref = _run(n, eps, batch * 2, record, fused)   # 1 rank, same global round size
+    ref = _run(n, eps, batch * ws, record, fused)  # 1 rank, same global round size
     if fused:
-        staged = _run(n, eps, batch * 2, record, False)
+        staged = _run(n, eps, batch * ws, record, False)
         for k in ("theta", "w", "d", "x", "n_eval", "rec"):
             np.testing.assert_array_equal(ref[k], staged[k], err_msg=k)
     with tempfile.TemporaryDirectory() as tmp:
-        mp.start_processes(_worker, args=(2, _free_port(), tmp, n, eps, batch,
+        mp.start_processes(_worker, args=(ws, _free_port(), tmp, n, eps, batch,
                                           record, fused),
-                           nprocs=2, join=True, start_method="spawn")
-        for rank in range(2):
+                           nprocs=ws, join=True, start_method="spawn")
+        for rank in range(ws):
             got = dict(np.load(os.path.join(tmp, f"r{rank}.npz")))
             assert int(got["n_eval"]) == int(ref["n_eval"])
+            assert int(got["collectives"]) == int(got["rounds"]) + 1 + int(record)
             for k in ("theta", "w", "d", "x"):
                 assert got[k].shape[0] == n
                 np.testing.assert_array_equal(got[k], ref[k], err_msg=k)

@@ -28,9 +28,9 @@ def _port():
     return p
 
 
-def _run(tmp_path, nproc, mode="uniform"):
-    out = str(tmp_path / f"pop_{mode}_{nproc}.npz")
-    env = dict(os.environ, OUT=out, POP="20000", GENS="4", MODE=mode)
+def _run(tmp_path, nproc, mode="uniform", pop=20000, gens=4):
+    out = str(tmp_path / f"pop_{mode}_{nproc}_{pop}.npz")
+    env = dict(os.environ, OUT=out, POP=str(pop), GENS=str(gens), MODE=mode)
     if nproc == 1:
         cmd = [sys.executable, WORKER]
     else:
@@ -44,11 +44,23 @@ def _run(tmp_path, nproc, mode="uniform"):
 
 
 def test_sharded_generations_bit_identical(tmp_path):
+    """1 vs 2, 3, 4 and 8 ranks (1/2/4/8-rank runs produce an
+    identical accepted set)."""
     ref = _run(tmp_path, 1)
-    for nproc in (2, 3):
+    for nproc in (2, 3, 4, 8):
         got = _run(tmp_path, nproc)
         for k in ("theta", "w", "eps", "samples"):
             np.testing.assert_array_equal(got[k], ref[k], err_msg=f"{k} @ {nproc} ranks")
+
+
+def test_sharded_tiny_population_bit_identical(tmp_path):
+    """A population of 7 on 8 ranks: every round is at least 4096 candidates
+    per rank, so rank 0 alone completes each generation and ranks 1..7 keep
+    no rows (empty shards in the packed gather, the cutoff on rank 0)."""
+    ref = _run(tmp_path, 1, pop=7, gens=3)
+    got = _run(tmp_path, 8, pop=7, gens=3)
+    for k in ("theta", "w", "eps", "samples"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
 
 
 def test_sharded_stochastic_generations_bit_identical(tmp_path):
