@@ -124,6 +124,8 @@ __global__ __launch_bounds__(256) void local_prep_kernel(const double* __restric
   }
 }
 
+#include "abc_local_knn.h"
+
 // LU with partial pivoting (getrf order: pivot = first max |a[r][c]|,
 // multipliers l = a[r][c] * (1 / pivot)); returns det and keeps the factors
 // in a, the row permutation in perm.  The determinant and the inverse come
@@ -271,7 +273,7 @@ template <int D, int PB>
 __global__ __launch_bounds__(256) void local_select_kernel(
     const double* __restrict__ X, int64_t N, int64_t nq,
     unsigned long long* __restrict__ sel_v, long long* __restrict__ sel_jcut,
-    long long* __restrict__ sel_rank0) {
+    long long* __restrict__ sel_rank0, const int* __restrict__ need) {
   __shared__ unsigned hist[PB][BR_NB];
   __shared__ long long s_tot[PB];
   __shared__ int s_cnt[4];
@@ -288,6 +290,13 @@ __global__ __launch_bounds__(256) void local_select_kernel(
   unsigned long long (*s_lkey)[2 * SEL_CAP] = s_buf;
   const int tid = threadIdx.x;
   const int64_t n0 = (int64_t)blockIdx.x * PB;
+  if (need) {
+    // re-selection of the particles knn_select_kernel flagged: blocks
+    // without one exit at once
+    bool any = false;
+    for (int p = 0; p < PB && n0 + p < N; ++p) any = any || need[n0 + p] != 0;
+    if (!any) return;
+  }
   for (int e = tid; e < PB * D; e += 256) {
     const int p = e / D, q = e % D;
     const int64_t n = n0 + p < N ? n0 + p : N - 1;  // pad: duplicate, not written
@@ -531,13 +540,17 @@ __global__ __launch_bounds__(256) void local_moments_kernel(
     const double* __restrict__ Mp, const double* __restrict__ w, int64_t N,
     const unsigned long long* __restrict__ sel_v,
     const long long* __restrict__ sel_jcut,
-    const long long* __restrict__ sel_rank0, double* __restrict__ part) {
+    const long long* __restrict__ sel_rank0, double* __restrict__ part,
+    const int* __restrict__ done) {
   constexpr int NM = local_nm<D>();
   constexpr int C0 = SL * MSLICE;
   constexpr int C1 = C0 + MSLICE < NM ? C0 + MSLICE : NM;
   constexpr int NS = C1 - C0;
   const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t ne = n < N ? n : N - 1;
+  // particles whose moments knn_select_kernel already summed (list mode):
+  // a wave with none left exits
+  if (done && __builtin_amdgcn_ballot_w64(n < N && !done[ne]) == 0ull) return;
   const int RS = gridDim.y;
   const int64_t j0 = (N * (int64_t)blockIdx.y) / RS, j1 = (N * ((int64_t)blockIdx.y + 1)) / RS;
   double xp[D];
@@ -619,10 +632,12 @@ __global__ __launch_bounds__(256) void local_finish_kernel(
     const double* __restrict__ X, int64_t N, int64_t nq, double scaling, double eps,
     const double* __restrict__ part, int RS, double* __restrict__ covs,
     double* __restrict__ invs, double* __restrict__ dets,
-    double* __restrict__ chol, double* __restrict__ lnorm) {
+    double* __restrict__ chol, double* __restrict__ lnorm,
+    const int* __restrict__ done, const double* __restrict__ lmom) {
   constexpr int NM = local_nm<D>();
   const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
+  const bool listed = done && done[n];   // moments summed by knn_select_kernel
   double cov[D][D];
   if (N == 1) {
     // indices is 1-D -> deltas = |X|, one sample -> diag(|X[0]|)
@@ -632,7 +647,9 @@ __global__ __launch_bounds__(256) void local_finish_kernel(
     double M[NM];
     for (int t = 0; t < NM; ++t) {
       double v = 0.0;
-      for (int y = 0; y < RS; ++y) v += part[((int64_t)y * NM + t) * N + n];
+      if (listed) v = lmom[(int64_t)t * N + n];
+      else
+        for (int y = 0; y < RS; ++y) v += part[((int64_t)y * NM + t) * N + n];
       M[t] = v;
     }
     double S2[D][D];
@@ -717,6 +734,12 @@ inline int moments_chunks(int64_t N) {
 // local variance: a particle that fails it sends the whole fit back to the
 // VALU kernel (a device flag read by the host; never seen on the tests'
 // populations).
+#ifndef ABC_LOCAL_SELECT_FP64
+#define ABC_LOCAL_SELECT_FP64 0   // build-time A/B: 1 keeps the fp64 select kernel
+#endif
+#ifndef ABC_LOCAL_DENSE_OLD
+#define ABC_LOCAL_DENSE_OLD 0     // build-time A/B: 1 keeps mm_moments_kernel after the k-NN select
+#endif
 #ifndef ABC_LOCAL_MOMENTS_VALU
 #define ABC_LOCAL_MOMENTS_VALU 0   // build-time A/B: 1 keeps the VALU kernel for all k
 #endif
@@ -1067,6 +1090,8 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const double* __restrict
   if (bad) atomicOr(flag, 1);
 }
 
+#include "abc_local_dense.h"
+
 inline int mm_chunks(int64_t N, int64_t nsteps) {
   const int64_t nblk = (N + MM_PB - 1) / MM_PB;
   int64_t rs = (1024 + nblk - 1) / nblk;
@@ -1081,11 +1106,12 @@ template <int D> constexpr int sel_pb() { return D <= 8 ? 8 : 4; }
 template <int D, int SL>
 void launch_moments(const double* X, const float* X32, const double* M, const double* w,
                     int64_t N, const unsigned long long* sel_v, const long long* sel_ties,
-                    const long long* sel_rank0, double* part, int RS, hipStream_t s) {
+                    const long long* sel_rank0, double* part, int RS, hipStream_t s,
+                    const int* done = nullptr) {
   hipLaunchKernelGGL((local_moments_kernel<D, SL>), dim3((unsigned)ceil_div(N, 256), (unsigned)RS),
-                     dim3(256), 0, s, X, X32, M, w, N, sel_v, sel_ties, sel_rank0, part);
+                     dim3(256), 0, s, X, X32, M, w, N, sel_v, sel_ties, sel_rank0, part, done);
   if constexpr (SL + 1 < local_nslices<D>())
-    launch_moments<D, SL + 1>(X, X32, M, w, N, sel_v, sel_ties, sel_rank0, part, RS, s);
+    launch_moments<D, SL + 1>(X, X32, M, w, N, sel_v, sel_ties, sel_rank0, part, RS, s, done);
 }
 
 template <int D>
@@ -1108,14 +1134,67 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
                        reinterpret_cast<unsigned long long*>(Mx));
     ABC_LAUNCHED();
   }
-  if (N > 1) {
+  constexpr int NM = local_nm<D>();
+  // k-NN selection on fp32 MFMA keys (abc_local_knn.h) for N >= KN_MIN_N;
+  // small k sums the moments in the same kernel (list mode)
+  const bool knn = N >= KN_MIN_N && !(ABC_LOCAL_SELECT_FP64);
+  const bool list_ok = knn && kn_list_capable<D>() && nq + KN_MARGIN <= KN_CAP;
+  int* done = nullptr;
+  double* lmom = nullptr;
+  double* cen = nullptr;
+  unsigned long long* r2 = nullptr;
+  int h_cnt[2] = {0, 0};
+  if (knn) {
+    const int64_t nt = ceil_div(N, 16) + 8 * KN_PF;   // + prefetch padding
+    cen = cv.take<double>(D);
+    float* img = cv.take<float>((size_t)nt * kn_kb<D>() * 64);
+    r2 = cv.take<unsigned long long>(1);
+    int* need = cv.take<int>((size_t)N);
+    done = cv.take<int>((size_t)N);
+    int* cnt = cv.take<int>(2);
+    lmom = cv.take<double>(kn_list_capable<D>() ? (size_t)NM * N : 1);
+    if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
+    ABC_HIP(hipMemsetAsync(r2, 0, sizeof(unsigned long long), s));
+    ABC_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(int), s));
+    hipLaunchKernelGGL((knn_center_kernel<D>), dim3(1), dim3(1024), 0, s, X, N, cen);
+    ABC_LAUNCHED();
+    hipLaunchKernelGGL((knn_prep_kernel<D>), dim3((unsigned)ceil_div(nt * 16, 256)), dim3(256), 0,
+                       s, X, N, (const double*)cen, img, r2);
+    ABC_LAUNCHED();
+    hipLaunchKernelGGL((knn_select_kernel<D>), dim3((unsigned)ceil_div(N, KN_PB)), dim3(256), 0,
+                       s, X, w, N, nq, (const double*)cen, (const float*)img,
+                       (const double*)r2, (int)list_ok, sel_v, sel_ties, sel_rank0, need,
+                       done, lmom, cnt);
+    ABC_LAUNCHED();
+    // particles whose window missed the rank or whose list overflowed: the
+    // fp64 radix select (blocks without such a particle exit at once)
+    hipLaunchKernelGGL((local_select_kernel<D, sel_pb<D>()>),
+                       dim3((unsigned)ceil_div(N, sel_pb<D>())), dim3(256), 0, s, X, N, nq,
+                       sel_v, sel_ties, sel_rank0, (const int*)need);
+    ABC_LAUNCHED();
+#ifdef ABC_KNN_TIMING
+    ABC_HIP(hipMemcpyAsync(covs, lmom, sizeof(double) * 8 * ceil_div(N, KN_PB), hipMemcpyDeviceToDevice, s));
+    return ABC_OK;
+#endif
+#ifdef ABC_KNN_DEBUG
+    ABC_HIP(hipMemcpyAsync(covs, lmom, sizeof(double) * 16 * N, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL((knn_keys_debug_kernel<D>), dim3(1), dim3(64), 0, s, X, N,
+                       (const double*)cen, (const float*)img, inv);
+    return ABC_OK;
+#endif
+    if (list_ok) {
+      // one 8-byte read decides whether any particle still needs a sweep
+      ABC_HIP(hipMemcpyAsync(h_cnt, cnt, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+      ABC_HIP(hipStreamSynchronize(s));
+    }
+  } else if (N > 1) {
     hipLaunchKernelGGL((local_select_kernel<D, sel_pb<D>()>), dim3((unsigned)ceil_div(N, sel_pb<D>())),
-                       dim3(256), 0, s, X, N, nq, sel_v, sel_ties, sel_rank0);
+                       dim3(256), 0, s, X, N, nq, sel_v, sel_ties, sel_rank0, (const int*)nullptr);
     ABC_LAUNCHED();
   }
-  constexpr int NM = local_nm<D>();
+  const bool all_listed = list_ok && h_cnt[1] == N;
   const int RS = N > 1 ? moments_chunks(N) : 1;
-  double* part = cv.take<double>((size_t)RS * NM * (size_t)N);
+  double* part = cv.take<double>(all_listed ? 1 : (size_t)RS * NM * (size_t)N);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
   // dense neighbourhoods (k > N / 16, d <= 5; above, the kernel's registers
   // spill): the moments on f16 MFMA
@@ -1127,9 +1206,11 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
     const int RS16 = mm_chunks(N, nsteps);
     unsigned long long* bnd = cv.take<unsigned long long>(1 + D);
     int* flag = cv.take<int>(1);
-    half8* img = cv.take<half8>((size_t)nsteps * mm_nt<D>() * 64);
+    // (+ DM_SB steps: knn_dense_kernel's stage loads past the last step)
+    half8* img = cv.take<half8>((size_t)(nsteps + DM_SB) * mm_nt<D>() * 64);
     double* part16 = cv.take<double>((size_t)RS16 * 16 * mm_nt<D>() * (size_t)N);
-    double* cen = cv.take<double>((size_t)NM * N);
+    double* cenm = cv.take<double>((size_t)NM * N);
+    float* drows = cv.take<float>((size_t)(nsteps + DM_SB) * 32 * DM_ROWF);
     if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
     ABC_HIP(hipMemsetAsync(bnd, 0, sizeof(unsigned long long) * (1 + D), s));
     ABC_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
@@ -1139,13 +1220,26 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
     hipLaunchKernelGGL((mm_bimg_kernel<D>), dim3((unsigned)ceil_div(nsteps * mm_nt<D>() * 64, 256)),
                        dim3(256), 0, s, X, w, N, nsteps, (const double*)bnd, img);
     ABC_LAUNCHED();
-    hipLaunchKernelGGL((mm_moments_kernel<D>), dim3((unsigned)ceil_div(N, MM_PB), (unsigned)RS16),
-                       dim3(MM_T), 0, s, X, (const float*)X32, (const double*)Mx,
-                       (const half8*)img, N, nsteps, (const unsigned long long*)sel_v,
-                       (const long long*)sel_ties, (const long long*)sel_rank0, part16);
+    if (knn && !(ABC_LOCAL_DENSE_OLD)) {
+      // membership from the centred fp32 keys of the k-NN select
+      const int64_t nrows = (nsteps + DM_SB) * 32;
+      hipLaunchKernelGGL((knn_rows_kernel<D>), dim3((unsigned)ceil_div(nrows, 256)), dim3(256), 0,
+                         s, X, N, nrows, (const double*)cen, drows);
+      ABC_LAUNCHED();
+      hipLaunchKernelGGL((knn_dense_kernel<D>), dim3((unsigned)ceil_div(N, DM_PB), (unsigned)RS16),
+                         dim3(DM_T), 0, s, X, (const double*)cen, (const double*)r2,
+                         (const float*)drows, (const half8*)img, N, nsteps,
+                         (const unsigned long long*)sel_v, (const long long*)sel_ties,
+                         (const long long*)sel_rank0, part16);
+    } else {
+      hipLaunchKernelGGL((mm_moments_kernel<D>), dim3((unsigned)ceil_div(N, MM_PB), (unsigned)RS16),
+                         dim3(MM_T), 0, s, X, (const float*)X32, (const double*)Mx,
+                         (const half8*)img, N, nsteps, (const unsigned long long*)sel_v,
+                         (const long long*)sel_ties, (const long long*)sel_rank0, part16);
+    }
     ABC_LAUNCHED();
     hipLaunchKernelGGL((mm_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
-                       X, N, nq, (const double*)part16, RS16, (const double*)bnd, cen, flag);
+                       X, N, nq, (const double*)part16, RS16, (const double*)bnd, cenm, flag);
     ABC_LAUNCHED();
     int h_flag = 0;
     ABC_HIP(hipMemcpyAsync(&h_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1153,17 +1247,20 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
     if (h_flag) {
       dense = false;   // rounding bound not met somewhere: the VALU kernel
     } else {
-      mom = cen;
+      mom = cenm;
       mom_rs = 1;
     }
   }
-  if (N > 1 && !dense) {
-    launch_moments<D, 0>(X, X32, Mx, w, N, sel_v, sel_ties, sel_rank0, part, RS, s);
+  if (N > 1 && !dense && !all_listed) {
+    // (after a partly listed select only the remaining particles' waves run)
+    launch_moments<D, 0>(X, X32, Mx, w, N, sel_v, sel_ties, sel_rank0, part, RS, s,
+                         list_ok ? (const int*)done : nullptr);
     ABC_LAUNCHED();
   }
   hipLaunchKernelGGL((local_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256),
                      0, s, X, N, nq, scaling, eps, mom, mom_rs, covs, inv,
-                     dets, chol, lnorm);
+                     dets, chol, lnorm, (const int*)(list_ok ? done : nullptr),
+                     (const double*)lmom);
   ABC_LAUNCHED();
   return ABC_OK;
 }
@@ -1440,15 +1537,27 @@ extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
   // partial moments of the row chunks (local_moments_kernel)
   const size_t nm = 2 + (size_t)d + (size_t)d * (d + 1) / 2;
   size_only<double>(off, (size_t)moments_chunks(N > 1 ? N : 1) * nm * (size_t)(N > 0 ? N : 1));
+  {  // fp32-MFMA k-NN select (abc_local_knn.h)
+    const int64_t n1 = N > 0 ? N : 1;
+    const int64_t nt = (n1 + 15) / 16;
+    size_only<double>(off, (size_t)d);
+    size_only<float>(off, (size_t)(nt + 32) * ((d + 5) / 4) * 64);
+    size_only<unsigned long long>(off, 1);
+    size_only<int>(off, (size_t)n1);
+    size_only<int>(off, (size_t)n1);
+    size_only<int>(off, 2);
+    size_only<double>(off, nm * (size_t)n1);
+  }
   if (d <= 5) {   // dense-neighbourhood MFMA path (mm_*_kernel)
     const int64_t n1 = N > 0 ? N : 1;
     const int64_t nsteps = (n1 + 31) / 32;
     const int64_t nt = ((int64_t)nm * ML_NL + 15) / 16;
     size_only<unsigned long long>(off, 1 + (size_t)d);
     size_only<int>(off, 1);
-    size_only<half8>(off, (size_t)(nsteps * nt * 64));
+    size_only<half8>(off, (size_t)((nsteps + DM_SB) * nt * 64));
     size_only<double>(off, (size_t)mm_chunks(n1, nsteps) * 16 * nt * (size_t)n1);
     size_only<double>(off, nm * (size_t)n1);
+    size_only<float>(off, (size_t)(nsteps + DM_SB) * 32 * DM_ROWF);
   }
   return off + 256;
 }

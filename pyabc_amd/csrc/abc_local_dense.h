@@ -1,0 +1,216 @@
+// Dense-neighbourhood moments of the LocalTransition fit (k a sizeable
+// fraction of N, the default k = N/4) on f16 MFMA, fed by fp32 expanded-form
+// keys (included by abc_local.hip after mm_finish_kernel; the membership
+// bound is abc_local_knn.h's kn_bound).
+//
+// Reference: pyabc/transition/local_transition.py:125-139 (weighted
+// covariance of the k neighbours' offsets).
+//
+// The raw sums S_n,f = sum_j m_nj F_j,f are the [particles x rows] x [rows x
+// features] product of mm_moments_kernel (same exact 11-bit limb image of
+// F, same fp64 flushes, same mm_finish_kernel), with two changes that
+// matter at k = N/4, where every row of every wave has members:
+//  * the membership key is s^ = n^_n + sum_q y^_jq (-2 y^_nq) + n^_j on the
+//    centred fp32 rows of knn_prep_kernel (D fma + 1 add per pair instead of
+//    D sub + D fma; any evaluation order is inside kn_bound), decided
+//    against the fp32 cuts of v* and settled exactly in fp64 between them;
+//  * both operand streams reach LDS by global_load_lds (16 B per lane, no
+//    staging registers), double-buffered per DM_SB 32-row steps, so the
+//    wave's registers go to its 2 x 7 accumulator tiles.
+#ifndef ABC_DM_W
+#define ABC_DM_W 4
+#endif
+#ifndef ABC_DM_WPE
+#define ABC_DM_WPE 0
+#endif
+constexpr int DM_W = ABC_DM_W;             // waves per block
+constexpr int DM_G = 2;                    // particle tiles per wave
+constexpr int DM_T = DM_W * 64;
+constexpr int DM_PB = DM_W * DM_G * 16;    // particles per block
+constexpr int DM_SB = 2;                   // 32-row steps per LDS stage
+constexpr int DM_ROWF = 8;                 // floats per staged row: y^ (D <= 7), n^
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(
+      (const __attribute__((address_space(1))) void*)g,
+      (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// rows [y^_0 .. y^_{D-1}, n^, 0...] per row (rows >= N: n^ = +inf, key +inf)
+template <int D>
+__global__ __launch_bounds__(256) void knn_rows_kernel(const double* __restrict__ X, int64_t N,
+                                                       int64_t nrows,
+                                                       const double* __restrict__ cen,
+                                                       float* __restrict__ rows) {
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= nrows) return;
+  float f[DM_ROWF];
+#pragma unroll
+  for (int k = 0; k < DM_ROWF; ++k) f[k] = 0.0f;
+  if (j < N) {
+    float y[D];
+    const float n = kn_feat<D>(X, j, cen, y);
+#pragma unroll
+    for (int q = 0; q < D; ++q) f[q] = y[q];
+    f[D] = n;
+  } else {
+    f[D] = INFINITY;
+  }
+#pragma unroll
+  for (int k = 0; k < DM_ROWF; ++k) rows[j * DM_ROWF + k] = f[k];
+}
+
+template <int D>
+__global__ __launch_bounds__(DM_T)
+#if ABC_DM_WPE
+__attribute__((amdgpu_waves_per_eu(ABC_DM_WPE)))
+#endif
+void knn_dense_kernel(
+    const double* __restrict__ X, const double* __restrict__ cen,
+    const double* __restrict__ R2p, const float* __restrict__ rows,
+    const half8* __restrict__ img, int64_t N, int64_t nsteps,
+    const unsigned long long* __restrict__ sel_v, const long long* __restrict__ sel_jcut,
+    const long long* __restrict__ sel_rank0, double* __restrict__ part) {
+  static_assert(D + 1 <= DM_ROWF, "staged row holds y^ and n^");
+  constexpr int NT = mm_nt<D>(), NCP = 16 * NT;
+  constexpr int BP = DM_SB * NT * 64;              // B pieces (16 B) per stage
+  constexpr int RP = DM_SB * 32 * DM_ROWF / 4;     // row pieces per stage
+  constexpr int SP = BP + RP;
+  static_assert(BP % 64 == 0 && RP % 64 == 0, "whole wave-instructions per stream");
+  constexpr int PW = (SP / 64 + DM_W - 1) / DM_W;  // wave-instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char stage[2][SP * 16];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int RS = gridDim.y;
+  const int64_t s0 = (nsteps * (int64_t)blockIdx.y) / RS;
+  const int64_t s1 = (nsteps * ((int64_t)blockIdx.y + 1)) / RS;
+  const int64_t p0 = ((int64_t)blockIdx.x * DM_W + wv) * (DM_G * 16);
+  const int kq = lane >> 4;
+  const KnBound Bd = kn_bound<D>(*R2p);
+  const float zc = kn_cut_above(0.0, Bd);
+
+  // the lane's particle in each tile: -2 y^_n, n^_n and the fp32 cuts of v*
+  float m2y[DM_G][D], nn[DM_G], cin[DM_G], cout[DM_G];
+#pragma unroll
+  for (int g = 0; g < DM_G; ++g) {
+    const int64_t pn = p0 + 16 * g + (lane & 15);
+    const int64_t pe = pn < N ? pn : N - 1;
+    float y[D];
+    nn[g] = kn_feat<D>(X, pe, cen, y);
+#pragma unroll
+    for (int q = 0; q < D; ++q) m2y[g][q] = -2.0f * y[q];
+    const double v = key_val(sel_v[pe]);
+    cin[g] = kn_cut_below(v, Bd);
+    cout[g] = kn_cut_above(v, Bd);
+  }
+  f32x4 acc[DM_G][NT];
+#pragma unroll
+  for (int g = 0; g < DM_G; ++g)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bool first = true;
+  int since = 0;
+  auto flush = [&]() {
+#pragma unroll
+    for (int g = 0; g < DM_G; ++g)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int c = 16 * t + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t n = p0 + 16 * g + 4 * kq + r;
+          if (n < N) {
+            double* dst = part + ((int64_t)blockIdx.y * NCP + c) * N + n;
+            *dst = (first ? 0.0 : *dst) + (double)acc[g][t][r];
+          }
+        }
+        acc[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    first = false;
+    since = 0;
+  };
+  // one stage: the B image of DM_SB steps, then their rows (both streams
+  // padded by DM_SB steps past nsteps, so a partial last stage loads safely)
+  auto issue = [&](int buf, int64_t sb) {
+    const char* bsrc = reinterpret_cast<const char*>(img + sb * NT * 64);
+    const char* rsrc = reinterpret_cast<const char*>(rows + sb * 32 * DM_ROWF);
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int wi = wv * PW + i;              // wave-instruction index (uniform)
+      if (wi * 64 < SP) {
+        const int e = wi * 64 + lane;
+        const char* src = e < BP ? bsrc + (size_t)e * 16 : rsrc + (size_t)(e - BP) * 16;
+        glds16(src, &stage[buf][(size_t)wi * 64 * 16]);
+      }
+    }
+  };
+  if (s0 < s1) issue(0, s0);
+  int buf = 0;
+  for (int64_t sb = s0; sb < s1; sb += DM_SB, buf ^= 1) {
+    __syncthreads();                 // stage sb landed (vmcnt(0) + barrier); buf ^ 1 free
+    if (sb + DM_SB < s1) issue(buf ^ 1, sb + DM_SB);
+    const half8* bs = reinterpret_cast<const half8*>(&stage[buf][0]);
+    const float* rs = reinterpret_cast<const float*>(&stage[buf][(size_t)BP * 16]);
+    const int nk = (int)((s1 - sb) < DM_SB ? (s1 - sb) : DM_SB);
+    for (int k = 0; k < nk; ++k) {
+      half8 a[DM_G];
+      uint32_t openm = 0u, inm = 0u;   // bit 8 g + u: pair (tile g, row u)
+      // rows one at a time (not unrolled: the 8 rows' features would
+      // otherwise be loaded up front and cost the occupancy)
+#pragma unroll 2
+      for (int u = 0; u < 8; ++u) {
+        const float* rf = rs + (k * 32 + 8 * kq + u) * DM_ROWF;
+        const f32x4 r0 = *reinterpret_cast<const f32x4*>(rf);
+        const f32x4 r1 = *reinterpret_cast<const f32x4*>(rf + 4);
+        float y[8] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
+#pragma unroll
+        for (int g = 0; g < DM_G; ++g) {
+          float sk = nn[g];
+#pragma unroll
+          for (int q = 0; q < D; ++q) sk = __builtin_fmaf(y[q], m2y[g][q], sk);
+          sk += y[D];
+          const bool in = sk < cin[g] && sk > zc;
+          openm |= (!in && !(sk > cout[g])) ? (1u << (8 * g + u)) : 0u;
+          inm |= in ? (1u << (8 * g + u)) : 0u;
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < DM_G; ++g)
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          a[g][u] = ((inm >> (8 * g + u)) & 1u) ? (_Float16)1.0f : (_Float16)0.0f;
+      if (__builtin_amdgcn_ballot_w64(openm != 0u) != 0ull) {
+        // rare: settle the open pairs in fp64 (rank-0 row excluded)
+#pragma unroll
+        for (int g = 0; g < DM_G; ++g) {
+          if (!((openm >> (8 * g)) & 0xFFu)) continue;
+          const int64_t pn = p0 + 16 * g + (lane & 15);
+          const int64_t pe = pn < N ? pn : N - 1;
+          double xp[D];
+#pragma unroll
+          for (int q = 0; q < D; ++q) xp[q] = X[pe * D + q];
+          const unsigned long long vs = sel_v[pe];
+          const long long jc = sel_jcut[pe], r0 = sel_rank0[pe];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int64_t j = 32 * (sb + k) + 8 * kq + u;
+            if (!((openm >> (8 * g + u)) & 1u) || j >= N) continue;
+            const unsigned long long key = (unsigned long long)__double_as_longlong(dist2<D>(X, j, xp));
+            const bool member = (key < vs || (key == vs && j < jc)) && j != r0;
+            a[g][u] = member ? (_Float16)1.0f : (_Float16)0.0f;
+          }
+        }
+      }
+      const half8* b = bs + k * NT * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const half8 bt = b[t * 64];
+#pragma unroll
+        for (int g = 0; g < DM_G; ++g)
+          acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[g], bt, acc[g][t], 0, 0, 0);
+      }
+      if (++since == MM_FLUSH) flush();
+    }
+  }
+  if (since > 0 || first) flush();
+}
