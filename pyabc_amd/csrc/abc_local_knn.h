@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
   __shared__ int s_sh[KN_PB], s_fail[KN_PB], s_rank[KN_PB];
   __shared__ double s_tlo[KN_PB], s_thi[KN_PB];
   __shared__ float s_clo[KN_PB], s_chi[KN_PB];
-  __shared__ int s_list, s_nest[KN_PB];
+  __shared__ int s_list, s_nest[KN_PB], s_lm[KN_PB];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
@@ -352,7 +352,12 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     const double pf = (double)(nq - 1) / (double)N;
     const int64_t mrg = 3 + (int64_t)(5.0 * sqrt(KN_SK * pf * (1.0 - pf)));
     const int64_t jk = ((nq - 1) * KN_SK) / N;
-    const uint32_t s0 = u.sample[p][0];
+    // the smallest NONZERO sampled distance (the particle itself, or an
+    // exact duplicate, in the sample would start the window at 0 and bin it
+    // by whole binades)
+    int z = 0;
+    while (z < KN_SK - 1 && u.sample[p][z] == 0u) ++z;
+    const uint32_t s0 = u.sample[p][z];
     const uint32_t lo = jk - mrg >= 0 ? u.sample[p][jk - mrg]
                                       : (s0 > (12u << 23) ? s0 - (12u << 23) : 0u);
     uint32_t hi = jk + mrg >= KN_SK ? 0x7F800000u : u.sample[p][jk + mrg];
@@ -444,17 +449,20 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     }
   }
   __syncthreads();
+  // list mode per particle: every neighbour fits the list
+  if (tid < KN_PB)
+    s_lm[tid] = (list_ok && kn_list_capable<D>() && !s_fail[tid] &&
+                 s_nest[tid] + KN_MARGIN <= KN_CAP) ? 1 : 0;
   if (tid == 0) {
-    int lm = list_ok && kn_list_capable<D>();
-    for (int p = 0; p < KN_PB; ++p)
-      if (p0 + p < N && (s_fail[p] || s_nest[p] + KN_MARGIN > KN_CAP)) lm = 0;
-    s_list = lm;
+    int any = 0;
+    for (int p = 0; p < KN_PB; ++p) any |= s_lm[p];
+    s_list = any;
   }
   __syncthreads();
-  const bool listm = s_list != 0;
+  const bool listm = s_list != 0;     // some particle of the block is listed
   if (tid < KN_PB) {
     const int p = tid;
-    if (listm) s_tlo[p] = -INFINITY;
+    if (s_lm[p]) s_tlo[p] = -INFINITY;
     else if (!s_fail[p] && s_rank[p] + KN_MARGIN > KN_CAP) s_fail[p] = 1;
     s_clo[p] = s_fail[p] ? -INFINITY : kn_cut_below(s_tlo[p], Bd);
     s_chi[p] = s_fail[p] ? -INFINITY : kn_cut_above(s_thi[p], Bd);
@@ -574,14 +582,14 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
       double* dg = lmom + (int64_t)(p0 + p) * 16;
       dg[0] = s_fail[p]; dg[1] = s_nest[p]; dg[2] = s_rank[p]; dg[3] = s_cnt[p];
       dg[4] = s_below[p]; dg[5] = s_tlo[p]; dg[6] = s_thi[p]; dg[7] = s_chi[p];
-      dg[8] = s_clo[p]; dg[9] = *R2p; dg[10] = s_lo[p]; dg[11] = s_sh[p]; dg[12] = listm;
+      dg[8] = s_clo[p]; dg[9] = *R2p; dg[10] = s_lo[p]; dg[11] = s_sh[p]; dg[12] = s_lm[p];
       dg[13] = (double)rr; dg[14] = Bd(0.0); dg[15] = 0;
     }
 #endif
     need[p0 + p] = bad ? 1 : 0;
-    done[p0 + p] = (!bad && listm) ? 1 : 0;
+    done[p0 + p] = (!bad && s_lm[p]) ? 1 : 0;
     if (bad) atomicAdd(&counts[0], 1);
-    else if (listm) atomicAdd(&counts[1], 1);
+    else if (s_lm[p]) atomicAdd(&counts[1], 1);
     s_fail[p] = bad ? 1 : 0;
   }
   KN_TS(5);
@@ -609,7 +617,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     // fixed-order wave reduction (deterministic)
     for (int p = wv; p < KN_PB; p += 4) {
       const int64_t n = p0 + p;
-      if (n >= N || s_fail[p]) continue;
+      if (n >= N || s_fail[p] || !s_lm[p]) continue;
       const long long r0 = s_rank0[p] == 0xFFFFFFFFu ? N : (long long)s_rank0[p];
       double xp[D];
 #pragma unroll

@@ -19,21 +19,10 @@ bad = (dg[:, 0] > 0) | (dg[:, 3] > 256) | (dg[:, 13] < 0) | (dg[:, 13] >= np.min
 print("bad frac", bad.mean())
 for i in list(range(3)) + list(np.nonzero(bad)[0][:3]):
     print(i, dg[i])
-# keys of particles 0..15 (debug kernel, written into the inverse-covariance
-# output): the sweeps' MFMA keys against numpy's fp32 expanded form
-inv = gpu.local_fit(gpu.as_dev(X), gpu.as_dev(w), k, 1.0, 1e-3)[1]
-keys = inv.reshape(-1)[: 16 * N].reshape(2, 8, N).cpu().numpy()
-c = 0.5 * X.min(0) + 0.5 * X.max(0)
-y = (X - c).astype(np.float32)
-s64 = ((X[None, :8] - X[:, None]) ** 2).sum(-1).T      # [8, N]
-rows0 = np.nonzero(((np.arange(N) // 16) % 4) == 0)[0]
-rows0 = rows0[rows0 < (N // 128) * 128]
-for v, name in ((0, "2-tile"), (1, "1-tile")):
-    sel = rows0 if v == 0 else np.arange(N)
-    err = np.abs(keys[v][:, sel] - s64[:, sel])
-    print(name, "max |s^ - s64|", err.max(), "at", np.unravel_index(err.argmax(), err.shape))
-    print("  sample keys", keys[v][0, :8], "s64", s64[0, :8])
-
-for i in range(8):
-    h = dg[i, 6] - dg[i, 14]
-    print(i, "nest", dg[i, 1], "#{s^ < h}", int((keys[1][i] < h).sum()), "#{s64 < thi}", int((s64[i] < dg[i, 6]).sum()), "list", dg[i, 3])
+lm = dg[:, 12]
+print("listmode frac", lm.mean(), "fail frac", dg[:, 0].mean())
+nl = np.nonzero(lm == 0)[0]
+print("non-list particles", len(nl), "first", nl[:20])
+blk = nl // 16
+for b in np.unique(blk)[:5]:
+    print("block", b); print(dg[16 * b: 16 * b + 16, [0, 1, 2, 3, 4, 10, 11, 13]])
