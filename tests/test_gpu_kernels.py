@@ -623,3 +623,26 @@ def test_cdf_guide_search_edges(dev):
         t = np.arange(N) * (c[-1] / N)
         np.testing.assert_array_equal(
             g, np.minimum(np.searchsorted(c, t, side="right"), N - 1), err_msg=name)
+
+
+@pytest.mark.parametrize("d,k,jitter", [(3, 40, 1e-7), (4, 700, 1e-7), (5, 50, 3e-8),
+                                         (8, 90, 1e-7), (12, 300, 1e-7), (5, 1500, 0.0)])
+def test_local_fit_knn_keys_at_the_fp32_bound(dev, d, k, jitter):
+    """The k-NN select sorts on fp32 MFMA keys and settles only the keys
+    within its rigorous fp32/fp64 bound in fp64 (abc_local_knn.h kn_bound).
+    A jittered integer grid puts thousands of distances within a few fp32
+    ulps of one another -- and of the k-th distance -- so the cuts decide
+    exactly at the bound's edge (jitter 0: exact ties, taken by index).
+    N >= 2048 runs the MFMA select; d = 8 its in-kernel moments (list mode),
+    d = 12 three feature blocks; k = 700, 1500 the bin mode."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(d * 1000 + k)
+    N = 3000
+    X = rng.integers(0, 4, size=(N, d)).astype(float) + jitter * rng.standard_normal((N, d))
+    X += 250.0          # far from the origin: the keys are centred first
+    w = np.exp(0.3 * rng.standard_normal(N))
+    w /= w.sum()
+    ref = oracle.local_fit(X, w, k=k, k_fraction=None)
+    covs, inv, dets, chol, lnorm = gpu.local_fit(gpu.as_dev(X), gpu.as_dev(w), k, 1.0, 1e-3)
+    np.testing.assert_allclose(covs.cpu().numpy(), ref["covs"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(dets.cpu().numpy(), ref["dets"], rtol=1e-8)
