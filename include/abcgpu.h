@@ -289,6 +289,22 @@ int abc_candidates_regen(const abc_candidate_spec* spec, int64_t idx0,
                          double* prior_logpdf, int64_t* ancestor, double* x,
                          double* dist, void* stream);
 
+/* Proposals only, candidates idx0 .. idx0 + B - 1: theta [B x d], prior
+ * log-density [B] (-inf when the proposal gave up), ancestor [B] (may be
+ * null), attempts [B] (may be null).  The fused round's proposal
+ * (propose_one over the ancestor table, the prior support box computed once):
+ * bit-identical to abc_propose / abc_local_propose and to the rows
+ * abc_candidates_regen returns.  The spec's simulator / distance fields must
+ * be valid but are not read.  Replaces, for the staged sampler path,
+ * MultivariateNormalTransition.rvs / LocalTransition.rvs_single + the prior
+ * re-draw loop (pyabc/smc.py:610-662, transition/multivariatenormal.py:85-97,
+ * transition/local_transition.py:141-145).  Workspace:
+ * abc_candidates_propose_workspace() bytes. */
+size_t abc_candidates_propose_workspace(void);
+int abc_candidates_propose(const abc_candidate_spec* spec, int64_t idx0, int64_t B,
+                           double* theta, double* prior_logpdf, int64_t* ancestor,
+                           int32_t* attempts, void* ws, size_t ws_bytes, void* stream);
+
 /* Gather rows: out[i, :] = in[idx[i], :] (row width `cols` doubles). */
 int abc_gather_rows(const double* in, const int64_t* idx, int64_t n, int cols,
                     double* out, void* stream);

@@ -355,6 +355,53 @@ __global__ __launch_bounds__(256) void fused_regen_kernel(
   dist[i] = dd;
 }
 
+// ---- proposals only (the staged path of models without a fused simulator) --
+// Rows [0, B) of candidates idx0 + b: theta (through an LDS tile, so a
+// block's rows leave as consecutive doubles), prior log-density, ancestor,
+// attempts.  The same propose_one as the round and the regeneration (the
+// ancestor table, the support box computed once), so the staged path's
+// proposals are the fused path's bits; each block proposes FP_CPT groups of
+// FR_T candidates with its constants staged once.
+constexpr int FP_CPT = 4;
+template <int D, int MODE>
+__global__ __launch_bounds__(256) void fused_propose_kernel(
+    RoundArgs A, int64_t idx0, int64_t B, double* __restrict__ theta,
+    double* __restrict__ lp, int64_t* __restrict__ anc, int32_t* __restrict__ att_out) {
+  constexpr int DM = D > 0 ? D : 64;
+  constexpr int TW = D > 0 ? D : 16;          // LDS tile width (D = 0: 16-column chunks)
+  __shared__ BlockConsts C;
+  __shared__ double tile[FR_T][TW + 1];
+  stage_block_consts<D, MODE, true>(C, A.P, nullptr, A.box);
+  const int d = D > 0 ? D : A.P.d;
+  for (int c = 0; c < FP_CPT; ++c) {
+    const int64_t i0 = ((int64_t)blockIdx.x * FP_CPT + c) * FR_T;
+    if (i0 >= B) break;                        // uniform over the block
+    const int64_t i = i0 + threadIdx.x;
+    const bool valid = i < B;
+    const int nvalid = B - i0 < FR_T ? (int)(B - i0) : FR_T;
+    double th[DM];
+    int64_t j = -1;
+    int att = A.P.max_attempts + 1;
+    if (valid) att = propose_one<D, MODE, true>(A.P, C, (uint64_t)(idx0 + i), th, j);
+    for (int k0 = 0; k0 < d; k0 += TW) {
+      const int w = d - k0 < TW ? d - k0 : TW;
+#pragma unroll
+      for (int k = 0; k < TW; ++k)
+        if (k < w && valid) tile[threadIdx.x][k] = th[k0 + k];
+      __syncthreads();
+      for (int e = threadIdx.x; e < FR_T * w; e += FR_T) {
+        const int r = e / w, q = e - r * w;
+        if (r < nvalid) theta[(i0 + r) * d + k0 + q] = tile[r][q];
+      }
+      __syncthreads();
+    }
+    if (!valid) continue;
+    lp[i] = att <= A.P.max_attempts ? prior_logpdf(A.P.kind, A.P.params, d, th) : -INFINITY;
+    if (anc) anc[i] = j;
+    if (att_out) att_out[i] = att;
+  }
+}
+
 // ---- ancestor table (abc_candidate.h) ---------------------------------------
 __global__ __launch_bounds__(256) void anc_records_kernel(const double* __restrict__ X,
                                                           const double* __restrict__ cdf,
@@ -597,6 +644,34 @@ extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0
                        s, bits, nwords, tcnt, cap, idx);
     ABC_LAUNCHED();
   }
+  return ABC_OK;
+}
+
+extern "C" size_t abc_candidates_propose_workspace() { return 128 * sizeof(double) + 256; }
+
+extern "C" int abc_candidates_propose(const abc_candidate_spec* spec, int64_t idx0, int64_t B,
+                                      double* theta, double* prior_logpdf, int64_t* ancestor,
+                                      int32_t* attempts, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  const int rc = check_spec(spec);
+  if (rc != ABC_OK) return rc;
+  ABC_CHECK_ARG(B >= 0 && B < (1ll << 40), "candidates_propose: bad B");
+  if (B == 0) return ABC_OK;
+  ABC_CHECK_ARG(theta && prior_logpdf, "candidates_propose: null pointer");
+  if (ws_bytes < abc_candidates_propose_workspace())
+    return set_error(ABC_ERR_WORKSPACE, "candidates_propose: workspace too small");
+  hipStream_t s = as_stream(stream);
+  Carver c(ws, ws_bytes);
+  double* box = c.take<double>(128);
+  hipLaunchKernelGGL(support_box_kernel, dim3((unsigned)spec->d), dim3(64), 0, s,
+                     spec->prior_kind, spec->prior_params, spec->d, box);
+  ABC_LAUNCHED();
+  const RoundArgs A = round_args(spec, box);
+  const int64_t nb = ceil_div(B, (int64_t)FR_T * FP_CPT);
+  ABC_CHECK_ARG(nb < (1ll << 31), "candidates_propose: too many blocks");
+  ABC_FUSED_DISPATCH(fused_propose_kernel, dim3((unsigned)nb), s, A, idx0, B, theta,
+                     prior_logpdf, ancestor, attempts);
+  ABC_LAUNCHED();
   return ABC_OK;
 }
 

@@ -347,6 +347,25 @@ class CandidateRound:
                  p(ws), ws.numel(), stream_ptr())
         return idx, cnt
 
+    def propose(self, idx0, B):
+        """Proposals of candidates idx0 .. idx0 + B - 1 only
+        (abc_candidates_propose): theta [B, d], prior log-density [B],
+        ancestor [B] (int64), attempts [B] (int32) -- the rows gpu.propose
+        returns, through the round's proposal (ancestor table, support box
+        computed once)."""
+        import ctypes as C
+        dev = self.device
+        B = int(B)
+        theta = torch.empty((B, self.d), dtype=F64, device=dev)
+        lp = torch.empty(B, dtype=F64, device=dev)
+        anc = torch.empty(B, dtype=I64, device=dev)
+        att = torch.empty(B, dtype=torch.int32, device=dev)
+        if B:
+            ws = workspace(nat.query("abc_candidates_propose_workspace"), "propose")
+            nat.call("abc_candidates_propose", C.addressof(self.spec), int(idx0), B,
+                     p(theta), p(lp), p(anc), p(att), p(ws), ws.numel(), stream_ptr())
+        return theta, lp, anc, att
+
     def regen(self, idx0, idx, out=None):
         """Rows of the candidates idx0 + idx[i] (abc_candidates_regen):
         theta [n, d], prior log-density [n], ancestor [n], x [n, S], dist [n];

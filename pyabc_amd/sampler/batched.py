@@ -111,7 +111,8 @@ class BatchedGPUSampler(Sampler):
     ----------
     batch_size: candidates per rank and round (None: adapt to the measured
         acceptance rate).
-    max_batch_size: cap on the adaptive batch.
+    max_batch_size: cap on the adaptive batch of the staged path (default:
+        what staged_round_bytes of candidate rows allow, at most 2^25).
     seed: base seed of the counter-based RNG (None: drawn from numpy's global
         RNG on rank 0 and broadcast).
     max_attempts: prior re-draws per candidate before giving up
@@ -127,7 +128,7 @@ class BatchedGPUSampler(Sampler):
 
     FUSED_MAX_STATS = 256     # abc_candidates_round: S <= SIM_SMAX
 
-    def __init__(self, batch_size=None, max_batch_size=1 << 22, seed=None,
+    def __init__(self, batch_size=None, max_batch_size=None, seed=None,
                  max_attempts=10000, check_max_eval=False, fused=True,
                  max_fused_batch_size=1 << 31, filter_below=0.0,
                  filter_min_stats=5, record_budget_bytes=1 << 31,
@@ -136,6 +137,11 @@ class BatchedGPUSampler(Sampler):
         self.check_max_eval = check_max_eval
         self.batch_size = batch_size
         self.max_batch_size = max_batch_size
+        # device bytes one staged round may hold in candidate rows (theta,
+        # sum stats, distance, ancestor, the user simulator's output): at
+        # low acceptance rounds of 2^22 candidates meant hundreds of rounds
+        # (one host read each) per generation
+        self.staged_round_bytes = 1 << 32
         self.seed = seed
         self.max_attempts = max_attempts
         # fused candidate rounds (abc_candidates_round): one kernel per round,
@@ -177,13 +183,17 @@ class BatchedGPUSampler(Sampler):
             self.seed = dd.broadcast_int(np.random.randint(0, 2 ** 62), device)
         return self.seed
 
-    def _round_size(self, needed, ws):
+    def _round_size(self, needed, ws, d=1, S=1):
         if self.batch_size is not None:
             return int(self.batch_size)
         rate = self._acc_rate if self._acc_rate else 0.5
         # 30% margin: a second round costs more than the extra candidates
-        b = int(math.ceil(needed / max(rate, 1e-4) * 1.3 / ws)) + 256
-        return int(min(max(b, 4096), self.max_batch_size))
+        b = int(math.ceil(needed / max(rate, 1e-9) * 1.3 / ws)) + 256
+        cap = self.max_batch_size
+        if cap is None:
+            per = 8 * (2 * d + 2 * S) + 48     # theta, x (+ a user copy), dist, idx, lp, anc
+            cap = max(1 << 16, min(1 << 25, self.staged_round_bytes // per))
+        return int(min(max(b, 4096), cap))
 
     def sample_until_n_accepted(self, n, simulate_one, max_eval=np.inf,
                                 all_accepted=False, show_progress=False):
@@ -219,7 +229,8 @@ class BatchedGPUSampler(Sampler):
             if self.check_max_eval and n_eval >= max_eval:
                 ok = False
                 break
-            B = self._limit_to_max_eval(self._round_size(n - n_acc, ws), max_eval,
+            B = self._limit_to_max_eval(self._round_size(n - n_acc, ws, d,
+                                                         len(spec.sum_stat_keys)), max_eval,
                                         n_eval, ws)
             lo, _ = dd.rank_range(base, B, rank)
             theta, lp, anc, att = self._propose(spec, B, seed, gen, lo, d)
@@ -677,7 +688,37 @@ class BatchedGPUSampler(Sampler):
                                       for a in rec_extra[-1])
         return n_eval, rec_left
 
+    def _proposal_round(self, spec, seed, gen, dev):
+        """A proposal-only gpu.CandidateRound of this generation (dummy
+        simulator / distance fields, never read), cached per generation:
+        the staged path's proposals through the fused kernel's propose_one
+        (ancestor table, support box computed once per launch; the same bits
+        as gpu.propose).  None when the transition has no proposal arrays."""
+        key = (id(spec), seed, gen)
+        if getattr(self, "_prop_key", None) == key:
+            return self._prop_round
+        arrays = None
+        if spec.transition is not None:
+            fn = getattr(spec.transition, "proposal_arrays", None)
+            arrays = fn() if fn is not None else None
+            if arrays is None:
+                return None
+        torch = gpu.torch
+        z = torch.zeros(1, dtype=gpu.F64, device=dev)
+        fr = gpu.CandidateRound(len(spec.param_names), 1, spec.prior_kind,
+                                spec.prior_params, torch.zeros(1, dtype=torch.int32, device=dev),
+                                z, z, z, z, 2.0, seed, gen, self.max_attempts,
+                                **(arrays or {}))
+        self._prop_key, self._prop_round = key, fr
+        return fr
+
     def _propose(self, spec, B, seed, gen, lo, d):
+        fr = None
+        if not (spec.transition is None and getattr(spec, "host_prior", None)):
+            fr = self._proposal_round(spec, seed, gen, gpu.require_device())
+        if fr is not None:
+            th, lp, anc, att = fr.propose(lo, B)
+            return th, lp, (anc if spec.transition is not None else None), att
         if spec.transition is None:
             th, lp, _, att = gpu.propose(None, None, None, spec.prior_kind,
                                          spec.prior_params, seed, gen, lo, B,

@@ -422,3 +422,40 @@ def test_box_muller_accuracy(dev):
         ulp = np.abs(x[:, 2 * h:2 * h + 2] - exact) / \
             np.spacing(R.astype(np.float32)).astype(np.float64)[:, None]
         assert ulp.max() <= 4, ulp.max()
+
+
+@pytest.mark.parametrize("mode,d", [("mvn", 10), ("mvn", 3), ("local", 5), ("prior", 10),
+                                    ("mvn", 7), ("mvn", 20)])
+def test_proposal_only_round_equals_propose(dev, mode, d):
+    """abc_candidates_propose (the staged sampler path's proposals through
+    the fused kernel's propose_one: ancestor table, support box once per
+    launch, theta rows leaving through LDS) returns gpu.propose's rows bit
+    for bit: theta, prior log-density, ancestor, attempts -- including
+    ragged block tails, d > 16 (runtime-d kernel) and bounded priors that
+    exhaust max_attempts = 2."""
+    from pyabc_amd import gpu
+    c = _case(d, 1, mode=mode, seed=d)
+    lo = 12345
+    for B, max_att in ((1, 1000), (1023, 1000), (70_001, 1000)):
+        fr = _round(c, max_attempts=max_att)
+        th, lp, anc, att = fr.propose(lo, B)
+        th2, lp2, anc2, att2 = gpu.propose(c["X"], c["cdf"], c["L"], c["kind"], c["params"],
+                                           11, 3, lo, B, max_att, d,
+                                           per_particle_L=c["ppl"], guide=c["guide"])
+        assert torch.equal(th, th2) and torch.equal(lp, lp2) and torch.equal(att, att2)
+        if mode != "prior":
+            assert torch.equal(anc, anc2)
+    # bounded priors, attempts exhausted
+    kinds = ["uniform", "expon", "gamma", "beta", "lognorm", "laplace"]
+    params = [[0.0, 1.0, 0, 0], [0.2, 0.5, 0, 0], [2.0, 0.0, 1.0, 0],
+              [2.0, 3.0, 0.0, 1.0], [0.5, 0.0, 1.0, 0], [0.0, 1.0, 0, 0]]
+    c = _case(6, 1, kinds=kinds, params=params, seed=9)
+    c["host"]["X"] = np.abs(c["host"]["X"]) * 0.5 + 0.1
+    c["X"] = T(c["host"]["X"])
+    fr = _round(c, max_attempts=2)
+    th, lp, anc, att = fr.propose(77, 50_000)
+    th2, lp2, anc2, att2 = gpu.propose(c["X"], c["cdf"], c["L"], c["kind"], c["params"],
+                                       11, 3, 77, 50_000, 2, 6, guide=c["guide"])
+    assert (att > 2).any() and torch.isinf(lp[att > 2]).all()
+    assert torch.equal(th, th2) and torch.equal(lp, lp2) and torch.equal(att, att2)
+    assert torch.equal(anc, anc2)

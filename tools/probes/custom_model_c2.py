@@ -47,5 +47,8 @@ def run(model, tag):
           flush=True)
 
 
-run(pa.LinearGaussianModel(names, keys, src=list(range(d)), sigma=[0.5] * d), "builtin")
-run(pa.VectorizedModel(user_sim, keys), "user")
+which = sys.argv[2] if len(sys.argv) > 2 else "both"
+if which in ("both", "builtin"):
+    run(pa.LinearGaussianModel(names, keys, src=list(range(d)), sigma=[0.5] * d), "builtin")
+if which in ("both", "user"):
+    run(pa.VectorizedModel(user_sim, keys), "user")
