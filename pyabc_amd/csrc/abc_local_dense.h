@@ -24,14 +24,14 @@
 #define ABC_DM_WPE 0
 #endif
 constexpr int DM_W = ABC_DM_W;             // waves per block
-constexpr int DM_G = 2;                    // particle tiles per wave
+#ifndef ABC_DM_G
+#define ABC_DM_G 1
+#endif
+constexpr int DM_G = ABC_DM_G;             // particle tiles per wave
 constexpr int DM_T = DM_W * 64;
 constexpr int DM_PB = DM_W * DM_G * 16;    // particles per block
 #ifndef ABC_DM_SB
 #define ABC_DM_SB 2
-#endif
-#ifndef ABC_DM_UNROLL
-#define ABC_DM_UNROLL 2
 #endif
 constexpr int DM_SB = ABC_DM_SB;           // 32-row steps per LDS stage
 constexpr int DM_ROWF = 8;                 // floats per staged row: y^ (D <= 7), n^
@@ -163,7 +163,7 @@ void knn_dense_kernel(
       uint32_t openm = 0u, inm = 0u;   // bit 8 g + u: pair (tile g, row u)
       // rows one at a time (not unrolled: the 8 rows' features would
       // otherwise be loaded up front and cost the occupancy)
-#pragma unroll ABC_DM_UNROLL
+#pragma unroll 2
       for (int u = 0; u < 8; ++u) {
         const float* rf = rs + (k * 32 + 8 * kq + u) * DM_ROWF;
         const f32x4 r0 = *reinterpret_cast<const f32x4*>(rf);
