@@ -194,21 +194,32 @@ __device__ __forceinline__ void kn_sweep(const float* __restrict__ img, int nt, 
   float ld[KN_PF][KB];
   knf4 cn[KN_PF];
   auto load = [&](int t0) {
+#if defined(ABC_KNN_EXP) && ABC_KNN_EXP == 3
+    // timing experiment: no loads (the MFMA operands stay in registers)
+#pragma unroll
+    for (int i = 0; i < KN_PF; ++i)
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) ld[i][kb] = bfr[kb] + (float)(t0 & 7);
+#else
 #pragma unroll
     for (int i = 0; i < KN_PF; ++i) {
       const float* src = img + (size_t)(t0 + 4 * i) * (KB * 64);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) ld[i][kb] = src[kb * 64 + lane];
     }
+#endif
   };
+  // k-block-major order: the KN_PF tiles' MFMAs of one k-block are
+  // independent and issue back to back; each accumulator's next k-block
+  // comes KN_PF MFMAs later (past the 40-cycle dependent latency)
   auto mfma = [&]() {
 #pragma unroll
-    for (int i = 0; i < KN_PF; ++i) {
-      cn[i] = knf4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < KN_PF; ++i) cn[i] = knf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int i = 0; i < KN_PF; ++i)
         cn[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(ld[i][kb], bfr[kb], cn[i], 0, 0, 0);
-    }
   };
   constexpr int G = 4 * KN_PF;
   load(wv);
@@ -381,7 +392,7 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
   // follows the active lanes).  Pad rows (key +inf) can only land in a bin
   // whose upper edge is +inf, and then T_hi = +inf.
   uint32_t* const hrow = &u.h.bins[pl][0];
-#if defined(ABC_KNN_EXP) && ABC_KNN_EXP == 2
+#if defined(ABC_KNN_EXP) && (ABC_KNN_EXP == 2 || ABC_KNN_EXP == 3)
   kn_sweep<KB>(img, nt, wv, lane, bfr, [&](int, const knf4& c) {
     below += __float_as_uint(c[0] + c[1] + c[2] + c[3]) >> 30;
   });
