@@ -740,6 +740,9 @@ inline int moments_chunks(int64_t N) {
 #ifndef ABC_LOCAL_DENSE_OLD
 #define ABC_LOCAL_DENSE_OLD 0     // build-time A/B: 1 keeps mm_moments_kernel after the k-NN select
 #endif
+#ifndef ABC_KNN_NO_DEFER
+#define ABC_KNN_NO_DEFER 0        // build-time A/B: 1 keeps the select's own collect sweep at dense k
+#endif
 #ifndef ABC_LOCAL_MOMENTS_VALU
 #define ABC_LOCAL_MOMENTS_VALU 0   // build-time A/B: 1 keeps the VALU kernel for all k
 #endif
@@ -1044,7 +1047,8 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const double* __restrict
                                                         const double* __restrict__ part,
                                                         int RS, const double* __restrict__ bnd,
                                                         double* __restrict__ out,
-                                                        int* __restrict__ flag) {
+                                                        int* __restrict__ flag,
+                                                        const double* __restrict__ extra) {
   constexpr int NM = local_nm<D>(), NCP = 16 * mm_nt<D>();
   const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
@@ -1057,6 +1061,8 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const double* __restrict
       for (int y = 0; y < RS; ++y) c += part[((int64_t)y * NCP + f * ML_NL + l) * N + n];
       v += ldexp(c, e - 11 * (l + 1));
     }
+    // (deferred collect: + the queued members' fp64 sums)
+    if (extra) v += extra[(int64_t)f * N + n];
     S[f] = v;
     // last-limb rounding per member + the limb sum's own rounding
     E[f] = (double)nq * ldexp(1.0, e - 11 * ML_NL - 1) + 4.0 * MM_EPS * fabs(v);
@@ -1139,11 +1145,20 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   // small k sums the moments in the same kernel (list mode)
   const bool knn = N >= KN_MIN_N && !(ABC_LOCAL_SELECT_FP64);
   const bool list_ok = knn && kn_list_capable<D>() && nq + KN_MARGIN <= KN_CAP;
+  // dense neighbourhoods (k > N / 16, d <= 5; above, the kernel's registers
+  // spill): the moments on f16 MFMA
+  bool dense = D <= 5 && N >= 64 && nq * 16 > N && !(ABC_LOCAL_MOMENTS_VALU);
+  // dense k after the k-NN select's count sweep: the moments sweep does the
+  // collect (deferred collect, abc_local_dense.h) -- one sweep less
+  const bool defer = knn && !list_ok && dense && !(ABC_LOCAL_DENSE_OLD) && !(ABC_KNN_NO_DEFER);
   int* done = nullptr;
   double* lmom = nullptr;
   double* cen = nullptr;
   unsigned long long* r2 = nullptr;
   int h_cnt[2] = {0, 0};
+  int* knn_need = nullptr;
+  int* knn_cnt = nullptr;
+  float* knn_img = nullptr;
   if (knn) {
     const int64_t nt = ceil_div(N, 16) + 8 * KN_PF;   // + prefetch padding
     cen = cv.take<double>(D);
@@ -1161,17 +1176,22 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
     hipLaunchKernelGGL((knn_prep_kernel<D>), dim3((unsigned)ceil_div(nt * 16, 256)), dim3(256), 0,
                        s, X, N, (const double*)cen, img, r2);
     ABC_LAUNCHED();
+    knn_need = need;
+    knn_img = img;
+    knn_cnt = cnt;
     hipLaunchKernelGGL((knn_select_kernel<D>), dim3((unsigned)ceil_div(N, KN_PB)), dim3(256), 0,
                        s, X, w, N, nq, (const double*)cen, (const float*)img,
-                       (const double*)r2, (int)list_ok, sel_v, sel_ties, sel_rank0, need,
-                       done, lmom, cnt);
+                       (const double*)r2, (int)list_ok, (int)defer, sel_v, sel_ties, sel_rank0,
+                       need, done, lmom, cnt);
     ABC_LAUNCHED();
     // particles whose window missed the rank or whose list overflowed: the
     // fp64 radix select (blocks without such a particle exit at once)
-    hipLaunchKernelGGL((local_select_kernel<D, sel_pb<D>()>),
-                       dim3((unsigned)ceil_div(N, sel_pb<D>())), dim3(256), 0, s, X, N, nq,
-                       sel_v, sel_ties, sel_rank0, (const int*)need);
-    ABC_LAUNCHED();
+    if (!defer) {
+      hipLaunchKernelGGL((local_select_kernel<D, sel_pb<D>()>),
+                         dim3((unsigned)ceil_div(N, sel_pb<D>())), dim3(256), 0, s, X, N, nq,
+                         sel_v, sel_ties, sel_rank0, (const int*)need);
+      ABC_LAUNCHED();
+    }
 #ifdef ABC_KNN_TIMING
     ABC_HIP(hipMemcpyAsync(covs, lmom, sizeof(double) * 8 * ceil_div(N, KN_PB), hipMemcpyDeviceToDevice, s));
     return ABC_OK;
@@ -1196,16 +1216,16 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   const int RS = N > 1 ? moments_chunks(N) : 1;
   double* part = cv.take<double>(all_listed ? 1 : (size_t)RS * NM * (size_t)N);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
-  // dense neighbourhoods (k > N / 16, d <= 5; above, the kernel's registers
-  // spill): the moments on f16 MFMA
-  bool dense = D <= 5 && N >= 64 && nq * 16 > N && !(ABC_LOCAL_MOMENTS_VALU);
   const double* mom = part;
   int mom_rs = RS;
   if constexpr (D <= 5) if (dense) {
     const int64_t nsteps = ceil_div(N, 32);
     const int RS16 = mm_chunks(N, nsteps);
     unsigned long long* bnd = cv.take<unsigned long long>(1 + D);
-    int* flag = cv.take<int>(1);
+    int* flag = cv.take<int>(2);            // [rounding bound missed, deferred-collect failures]
+    int* qcnt = cv.take<int>((size_t)N);
+    int* cbelow = cv.take<int>((size_t)N);
+    int* qidx = cv.take<int>((size_t)N * KN_QCAP);
     // (+ DM_SB steps: knn_dense_kernel's stage loads past the last step)
     half8* img = cv.take<half8>((size_t)(nsteps + DM_SB) * mm_nt<D>() * 64);
     double* part16 = cv.take<double>((size_t)RS16 * 16 * mm_nt<D>() * (size_t)N);
@@ -1213,37 +1233,87 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
     float* drows = cv.take<float>((size_t)(nsteps + DM_SB) * 32 * DM_ROWF);
     if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
     ABC_HIP(hipMemsetAsync(bnd, 0, sizeof(unsigned long long) * (1 + D), s));
-    ABC_HIP(hipMemsetAsync(flag, 0, sizeof(int), s));
+    ABC_HIP(hipMemsetAsync(flag, 0, 2 * sizeof(int), s));
     const int64_t bb = ceil_div(N, 256) < 256 ? ceil_div(N, 256) : 256;
     hipLaunchKernelGGL((mm_bounds_kernel<D>), dim3((unsigned)bb), dim3(256), 0, s, X, w, N, bnd);
     ABC_LAUNCHED();
     hipLaunchKernelGGL((mm_bimg_kernel<D>), dim3((unsigned)ceil_div(nsteps * mm_nt<D>() * 64, 256)),
                        dim3(256), 0, s, X, w, N, nsteps, (const double*)bnd, img);
     ABC_LAUNCHED();
+    int h_flag = 0;
+    bool finished = false;   // mm_finish ran already (deferred collect)
     if (knn && !(ABC_LOCAL_DENSE_OLD)) {
       // membership from the centred fp32 keys of the k-NN select
       const int64_t nrows = (nsteps + DM_SB) * 32;
       hipLaunchKernelGGL((knn_rows_kernel<D>), dim3((unsigned)ceil_div(nrows, 256)), dim3(256), 0,
                          s, X, N, nrows, (const double*)cen, drows);
       ABC_LAUNCHED();
-      hipLaunchKernelGGL((knn_dense_kernel<D>), dim3((unsigned)ceil_div(N, DM_PB), (unsigned)RS16),
-                         dim3(DM_T), 0, s, X, (const double*)cen, (const double*)r2,
-                         (const float*)drows, (const half8*)img, N, nsteps,
-                         (const unsigned long long*)sel_v, (const long long*)sel_ties,
-                         (const long long*)sel_rank0, part16);
+      bool plain = !defer;
+      if (defer) {
+        ABC_HIP(hipMemsetAsync(qcnt, 0, sizeof(int) * N, s));
+        ABC_HIP(hipMemsetAsync(cbelow, 0, sizeof(int) * N, s));
+        hipLaunchKernelGGL((knn_dense_kernel<D, true>), dim3((unsigned)ceil_div(N, DM_PB), (unsigned)RS16),
+                           dim3(DM_T), 0, s, X, (const double*)cen, (const double*)r2,
+                           (const float*)drows, (const half8*)img, N, nsteps,
+                           (const unsigned long long*)sel_v, (const long long*)sel_ties,
+                           (const long long*)sel_rank0, part16, qcnt, qidx, cbelow);
+        ABC_LAUNCHED();
+        hipLaunchKernelGGL((knn_resolve_kernel<D>), dim3((unsigned)ceil_div(N, 4)), dim3(256), 0, s,
+                           X, w, N, nq, (const int*)knn_need, sel_v, sel_ties, sel_rank0,
+                           (const int*)qcnt, (const int*)qidx, (const int*)cbelow,
+                           part, flag + 1);
+        ABC_LAUNCHED();
+        hipLaunchKernelGGL((mm_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
+                           X, N, nq, (const double*)part16, RS16, (const double*)bnd, cenm, flag,
+                           (const double*)part);
+        ABC_LAUNCHED();
+        int h_f[2] = {0, 0};
+        ABC_HIP(hipMemcpyAsync(h_f, flag, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+        ABC_HIP(hipStreamSynchronize(s));
+        if (h_f[1]) {
+          // some particle's bracket or queue failed: the select with its own
+          // collect sweep (and the fp64 radix select behind it), then the
+          // plain moments sweep
+          ABC_HIP(hipMemsetAsync(knn_cnt, 0, 2 * sizeof(int), s));
+          ABC_HIP(hipMemsetAsync(flag, 0, 2 * sizeof(int), s));
+          hipLaunchKernelGGL((knn_select_kernel<D>), dim3((unsigned)ceil_div(N, KN_PB)), dim3(256),
+                             0, s, X, w, N, nq, (const double*)cen, (const float*)knn_img,
+                             (const double*)r2, 0, 0, sel_v, sel_ties, sel_rank0, knn_need,
+                             done, lmom, knn_cnt);
+          ABC_LAUNCHED();
+          hipLaunchKernelGGL((local_select_kernel<D, sel_pb<D>()>),
+                             dim3((unsigned)ceil_div(N, sel_pb<D>())), dim3(256), 0, s, X, N, nq,
+                             sel_v, sel_ties, sel_rank0, (const int*)knn_need);
+          ABC_LAUNCHED();
+          plain = true;
+        } else {
+          h_flag = h_f[0];
+          finished = true;
+        }
+      }
+      if (plain) {
+        hipLaunchKernelGGL((knn_dense_kernel<D, false>), dim3((unsigned)ceil_div(N, DM_PB), (unsigned)RS16),
+                           dim3(DM_T), 0, s, X, (const double*)cen, (const double*)r2,
+                           (const float*)drows, (const half8*)img, N, nsteps,
+                           (const unsigned long long*)sel_v, (const long long*)sel_ties,
+                           (const long long*)sel_rank0, part16, nullptr, nullptr, nullptr);
+        ABC_LAUNCHED();
+      }
     } else {
       hipLaunchKernelGGL((mm_moments_kernel<D>), dim3((unsigned)ceil_div(N, MM_PB), (unsigned)RS16),
                          dim3(MM_T), 0, s, X, (const float*)X32, (const double*)Mx,
                          (const half8*)img, N, nsteps, (const unsigned long long*)sel_v,
                          (const long long*)sel_ties, (const long long*)sel_rank0, part16);
+      ABC_LAUNCHED();
     }
-    ABC_LAUNCHED();
-    hipLaunchKernelGGL((mm_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
-                       X, N, nq, (const double*)part16, RS16, (const double*)bnd, cenm, flag);
-    ABC_LAUNCHED();
-    int h_flag = 0;
-    ABC_HIP(hipMemcpyAsync(&h_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
-    ABC_HIP(hipStreamSynchronize(s));
+    if (!finished) {
+      hipLaunchKernelGGL((mm_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
+                         X, N, nq, (const double*)part16, RS16, (const double*)bnd, cenm, flag,
+                         (const double*)nullptr);
+      ABC_LAUNCHED();
+      ABC_HIP(hipMemcpyAsync(&h_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
+      ABC_HIP(hipStreamSynchronize(s));
+    }
     if (h_flag) {
       dense = false;   // rounding bound not met somewhere: the VALU kernel
     } else {
@@ -1553,7 +1623,10 @@ extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
     const int64_t nsteps = (n1 + 31) / 32;
     const int64_t nt = ((int64_t)nm * ML_NL + 15) / 16;
     size_only<unsigned long long>(off, 1 + (size_t)d);
-    size_only<int>(off, 1);
+    size_only<int>(off, 2);
+    size_only<int>(off, (size_t)n1);                 // deferred collect: queue lengths
+    size_only<int>(off, (size_t)n1);                 //   certain-below counts
+    size_only<int>(off, (size_t)n1 * KN_QCAP);       //   queued rows
     size_only<half8>(off, (size_t)((nsteps + DM_SB) * nt * 64));
     size_only<double>(off, (size_t)mm_chunks(n1, nsteps) * 16 * nt * (size_t)n1);
     size_only<double>(off, nm * (size_t)n1);

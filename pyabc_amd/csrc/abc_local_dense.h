@@ -66,7 +66,16 @@ __global__ __launch_bounds__(256) void knn_rows_kernel(const double* __restrict_
   for (int k = 0; k < DM_ROWF; ++k) rows[j * DM_ROWF + k] = f[k];
 }
 
-template <int D>
+// DEFER (the deferred collect, see knn_select_kernel): sel_v / sel_jcut hold
+// the bracket [T_lo, T_hi) of the rank-k key as doubles instead of the
+// selected key; pairs certainly below T_lo are members (and counted into
+// cbelow), pairs between the cuts are not summed here but queued (qcnt,
+// qidx: KN_QCAP per particle) for knn_resolve_kernel, which selects the rank
+// among them and adds the members' limbs.  Queue slots come from an LDS
+// queue per block (DQ_L per particle), flushed to the global queue at the
+// end with one atomic per particle; a full LDS queue spills by global atomics.
+constexpr int DQ_L = 16;
+template <int D, bool DEFER>
 __global__ __launch_bounds__(DM_T)
 #if ABC_DM_WPE
 __attribute__((amdgpu_waves_per_eu(ABC_DM_WPE)))
@@ -76,7 +85,8 @@ void knn_dense_kernel(
     const double* __restrict__ R2p, const float* __restrict__ rows,
     const half8* __restrict__ img, int64_t N, int64_t nsteps,
     const unsigned long long* __restrict__ sel_v, const long long* __restrict__ sel_jcut,
-    const long long* __restrict__ sel_rank0, double* __restrict__ part) {
+    const long long* __restrict__ sel_rank0, double* __restrict__ part,
+    int* __restrict__ qcnt, int* __restrict__ qidx, int* __restrict__ cbelow) {
   static_assert(D + 1 <= DM_ROWF, "staged row holds y^ and n^");
   constexpr int NT = mm_nt<D>(), NCP = 16 * NT;
   constexpr int BP = DM_SB * NT * 64;              // B pieces (16 B) per stage
@@ -85,6 +95,11 @@ void knn_dense_kernel(
   static_assert(BP % 64 == 0 && RP % 64 == 0, "whole wave-instructions per stream");
   constexpr int PW = (SP / 64 + DM_W - 1) / DM_W;  // wave-instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char stage[2][SP * 16];
+  __shared__ int s_qn[DEFER ? DM_PB : 1], s_q[DEFER ? DM_PB * DQ_L : 1];
+  if constexpr (DEFER) {
+    for (int e = threadIdx.x; e < DM_PB; e += DM_T) s_qn[e] = 0;
+    // (the first stage's barrier orders these stores before any queue use)
+  }
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int RS = gridDim.y;
@@ -105,10 +120,18 @@ void knn_dense_kernel(
     nn[g] = kn_feat<D>(X, pe, cen, y);
 #pragma unroll
     for (int q = 0; q < D; ++q) m2y[g][q] = -2.0f * y[q];
-    const double v = key_val(sel_v[pe]);
-    cin[g] = kn_cut_below(v, Bd);
-    cout[g] = kn_cut_above(v, Bd);
+    if constexpr (DEFER) {
+      cin[g] = kn_cut_below(__longlong_as_double((long long)sel_v[pe]), Bd);
+      cout[g] = kn_cut_above(__longlong_as_double(sel_jcut[pe]), Bd);
+    } else {
+      const double v = key_val(sel_v[pe]);
+      cin[g] = kn_cut_below(v, Bd);
+      cout[g] = kn_cut_above(v, Bd);
+    }
   }
+  uint32_t nin[DM_G];   // DEFER: certain members counted per lane
+#pragma unroll
+  for (int g = 0; g < DM_G; ++g) nin[g] = 0u;
   f32x4 acc[DM_G][NT];
 #pragma unroll
   for (int g = 0; g < DM_G; ++g)
@@ -185,7 +208,37 @@ void knn_dense_kernel(
 #pragma unroll
         for (int u = 0; u < 8; ++u)
           a[g][u] = ((inm >> (8 * g + u)) & 1u) ? (_Float16)1.0f : (_Float16)0.0f;
-      if (__builtin_amdgcn_ballot_w64(openm != 0u) != 0ull) {
+      if constexpr (DEFER) {
+#pragma unroll
+        for (int g = 0; g < DM_G; ++g) nin[g] += __builtin_popcount((inm >> (8 * g)) & 0xFFu);
+      }
+      if (DEFER && __builtin_amdgcn_ballot_w64(openm != 0u) != 0ull) {
+        // queue the open pairs (their a stays 0): one LDS atomic per lane
+        // reserves its slots
+#pragma unroll
+        for (int g = 0; g < DM_G; ++g) {
+          const int64_t pn = p0 + 16 * g + (lane & 15);
+          const int pl = (wv * DM_G + g) * 16 + (lane & 15);
+          const int64_t jb = 32 * (sb + k) + 8 * kq;
+          uint32_t om = (openm >> (8 * g)) & 0xFFu;
+          if (jb + 8 > N) om &= N > jb ? (1u << (uint32_t)(N - jb)) - 1u : 0u;
+          if (pn >= N) om = 0u;
+          if (om) {
+            int slot = atomicAdd(&s_qn[pl], __builtin_popcount(om));
+            while (om) {
+              const int j = (int)jb + __builtin_ctz(om);
+              om &= om - 1u;
+              if (slot < DQ_L) {
+                s_q[pl * DQ_L + slot] = j;
+              } else {
+                const int gs = atomicAdd(&qcnt[pn], 1);
+                if (gs < KN_QCAP) qidx[pn * KN_QCAP + gs] = j;
+              }
+              ++slot;
+            }
+          }
+        }
+      } else if (!DEFER && __builtin_amdgcn_ballot_w64(openm != 0u) != 0ull) {
         // rare: settle the open pairs in fp64 (rank-0 row excluded)
 #pragma unroll
         for (int g = 0; g < DM_G; ++g) {
@@ -219,4 +272,139 @@ void knn_dense_kernel(
     }
   }
   if (since > 0 || first) flush();
+  if constexpr (DEFER) {
+#pragma unroll
+    for (int g = 0; g < DM_G; ++g) {
+      uint32_t c = nin[g];
+      c += __shfl_xor(c, 16, 64);
+      c += __shfl_xor(c, 32, 64);
+      const int64_t pn = p0 + 16 * g + (lane & 15);
+      if (lane < 16 && pn < N && c) atomicAdd(&cbelow[pn], (int)c);
+    }
+    __syncthreads();   // every wave's LDS queue entries are in
+    for (int pl = threadIdx.x; pl < DM_PB; pl += DM_T) {
+      const int64_t pn = (int64_t)blockIdx.x * DM_PB + pl;
+      const int m = s_qn[pl] < DQ_L ? s_qn[pl] : DQ_L;
+      if (pn >= N || m == 0) continue;
+      const int base = atomicAdd(&qcnt[pn], m);
+      for (int i = 0; i < m; ++i)
+        if (base + i < KN_QCAP) qidx[pn * KN_QCAP + base + i] = s_q[pl * DQ_L + i];
+    }
+  }
+}
+
+// The deferred collect's settle step, one wave per particle: the queued open
+// pairs get their exact fp64 keys; those below T_lo join the certain-below
+// count, those in [T_lo, T_hi) are ranked in (key, index) order, and rank
+// nq - 1 - #below is the selected neighbour (as in knn_select_kernel's
+// steps 3-4).  The members among the queue (below T_lo, or ranked at most
+// the selected one; the rank-0 row excluded) sum their features F_j,f in
+// fp64 (in index order, fixed) into extra[f][n], which
+// mm_finish_kernel adds to the limb sums of the certain members.  A particle flagged by the
+// select, with an overflowing queue or with the rank outside the kept set
+// counts into nfail (the host then reruns the fit with the in-kernel collect).
+template <int D>
+__global__ __launch_bounds__(256) void knn_resolve_kernel(
+    const double* __restrict__ X, const double* __restrict__ w, int64_t N, int64_t nq,
+    const int* __restrict__ need, unsigned long long* __restrict__ sel_v,
+    long long* __restrict__ sel_jcut, long long* __restrict__ sel_rank0,
+    const int* __restrict__ qcnt, const int* __restrict__ qidx,
+    const int* __restrict__ cbelow, double* __restrict__ extra, int* __restrict__ nfail) {
+  constexpr int E = KN_QCAP / 64;
+  __shared__ double s_key[4][KN_QCAP];
+  __shared__ int s_idx[4][KN_QCAP], s_ord[4][KN_QCAP];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 4 + wv;
+  const bool live = n < N;
+  const int64_t ne = live ? n : N - 1;
+  const int cnt = qcnt[ne];
+  bool ok = live && !need[ne] && cnt <= KN_QCAP;
+  const double tlo = __longlong_as_double((long long)sel_v[ne]);
+  const double thi = __longlong_as_double(sel_jcut[ne]);
+  double xn[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) xn[q] = X[ne * D + q];
+  double key[E], s64[E];
+  int jj[E];
+  int nbelow = 0, nkeep = 0, r0 = 0x7FFFFFFF;
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int q = lane + 64 * i;
+    jj[i] = (ok && q < cnt) ? qidx[ne * KN_QCAP + q] : -1;
+    s64[i] = INFINITY;
+    key[i] = INFINITY;
+    if (jj[i] >= 0) {
+      s64[i] = dist2<D>(X, jj[i], xn);
+      if (s64[i] == 0.0) r0 = min(r0, jj[i]);
+      if (s64[i] < tlo) ++nbelow;
+      else if (s64[i] < thi) { key[i] = s64[i]; ++nkeep; }
+    }
+    if (q < KN_QCAP) { s_key[wv][q] = key[i]; s_idx[wv][q] = jj[i]; }
+  }
+  __syncthreads();
+  int less[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) less[i] = 0;
+  if (ok)
+    for (int f = 0; f < cnt; ++f) {
+      const double kf = s_key[wv][f];
+      const int jf = s_idx[wv][f];
+#pragma unroll
+      for (int i = 0; i < E; ++i) less[i] += (kf < key[i]) || (kf == key[i] && jf < jj[i]);
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    nbelow += __shfl_xor(nbelow, o, 64);
+    nkeep += __shfl_xor(nkeep, o, 64);
+    r0 = min(r0, __shfl_xor(r0, o, 64));
+  }
+  const long long rr = nq - 1 - ((long long)cbelow[ne] + nbelow);
+  if (!(rr >= 0 && rr < nkeep)) ok = false;
+  const long long r0l = r0 == 0x7FFFFFFF ? (long long)N : (long long)r0;
+  bool mem[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const bool kept = key[i] < INFINITY;
+    mem[i] = ok && jj[i] >= 0 && (long long)jj[i] != r0l &&
+             (s64[i] < tlo || (kept && less[i] <= rr));
+    if (ok && kept && less[i] == rr) {
+      sel_v[n] = (unsigned long long)__double_as_longlong(s64[i]);
+      sel_jcut[n] = (long long)jj[i] + 1;
+      sel_rank0[n] = r0l;
+    }
+  }
+  if (live && !ok && lane == 0) atomicAdd(nfail, 1);
+  // members in index order (a deterministic summation order: the queue's
+  // order comes from atomics)
+  __syncthreads();                       // the ranking's LDS reads are done
+#pragma unroll
+  for (int i = 0; i < E; ++i) s_idx[wv][lane + 64 * i] = mem[i] ? jj[i] : 0x7FFFFFFF;
+  __syncthreads();
+  int pos[E], nmem = 0;
+#pragma unroll
+  for (int i = 0; i < E; ++i) { pos[i] = 0; nmem += mem[i] ? 1 : 0; }
+  if (ok)
+    for (int f = 0; f < cnt; ++f) {
+      const int jf = s_idx[wv][f];
+#pragma unroll
+      for (int i = 0; i < E; ++i) pos[i] += jf < jj[i] ? 1 : 0;
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nmem += __shfl_xor(nmem, o, 64);
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+    if (mem[i]) s_ord[wv][pos[i]] = jj[i];
+  __syncthreads();
+  // members' features in fp64: lane f < NM owns feature f
+  constexpr int NM = local_nm<D>();
+  double acc = 0.0;
+  if (ok && lane < NM)
+    for (int q = 0; q < nmem; ++q) {
+      const int j = s_ord[wv][q];
+      double y[D];
+#pragma unroll
+      for (int a = 0; a < D; ++a) y[a] = X[(int64_t)j * D + a] - X[a];
+      acc += mm_feature<D>(lane, w[j], y);
+    }
+  if (ok && lane < NM) extra[(int64_t)lane * N + n] = acc;
 }

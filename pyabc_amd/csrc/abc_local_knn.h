@@ -49,6 +49,7 @@ constexpr int KN_CAP = 192;  // list entries per particle (LDS: 4 blocks per CU)
 constexpr int KN_MARGIN = 32;
 constexpr int KN_PF = 4;     // row-tile groups in flight per sweep (kn_sweep)
 constexpr int KN_MIN_N = 4 * KN_SK;
+constexpr int KN_QCAP = 256; // open pairs per particle queued by the deferred collect
 typedef float knf4 __attribute__((ext_vector_type(4)));
 
 template <int D> constexpr int kn_kb() { return (D + 2 + 3) / 4; }
@@ -241,7 +242,7 @@ template <int D>
 __global__ __launch_bounds__(256) void knn_select_kernel(
     const double* __restrict__ X, const double* __restrict__ w, int64_t N, int64_t nq,
     const double* __restrict__ cen, const float* __restrict__ img,
-    const double* __restrict__ R2p, int list_ok,
+    const double* __restrict__ R2p, int list_ok, int defer,
     unsigned long long* __restrict__ sel_v, long long* __restrict__ sel_jcut,
     long long* __restrict__ sel_rank0, int* __restrict__ need, int* __restrict__ done,
     double* __restrict__ lmom, int* __restrict__ counts /* [nfail, ndone] */) {
@@ -460,6 +461,21 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     }
   }
   __syncthreads();
+  if (defer) {
+    // deferred collect (dense k): the moments sweep classifies every pair
+    // against [T_lo, T_hi) itself and queues the open ones
+    // (knn_dense_kernel<D, true>, knn_resolve_kernel); the bracket leaves
+    // here as two doubles, -inf for a particle whose window missed the rank
+    // or whose bin would not fit the queue
+    if (tid < KN_PB && p0 + tid < N) {
+      const int p = tid;
+      const bool bad = s_fail[p] || s_rank[p] + KN_MARGIN > KN_QCAP;
+      sel_v[p0 + p] = (unsigned long long)__double_as_longlong(bad ? -INFINITY : s_tlo[p]);
+      sel_jcut[p0 + p] = (long long)__double_as_longlong(bad ? -INFINITY : s_thi[p]);
+      need[p0 + p] = bad ? 1 : 0;
+    }
+    return;
+  }
   // list mode per particle: every neighbour fits the list
   if (tid < KN_PB)
     s_lm[tid] = (list_ok && kn_list_capable<D>() && !s_fail[tid] &&
