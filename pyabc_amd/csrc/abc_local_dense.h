@@ -213,28 +213,21 @@ void knn_dense_kernel(
         for (int g = 0; g < DM_G; ++g) nin[g] += __builtin_popcount((inm >> (8 * g)) & 0xFFu);
       }
       if (DEFER && __builtin_amdgcn_ballot_w64(openm != 0u) != 0ull) {
-        // queue the open pairs (their a stays 0): one LDS atomic per lane
-        // reserves its slots
+        // queue the open pairs (their a stays 0)
 #pragma unroll
         for (int g = 0; g < DM_G; ++g) {
           const int64_t pn = p0 + 16 * g + (lane & 15);
           const int pl = (wv * DM_G + g) * 16 + (lane & 15);
-          const int64_t jb = 32 * (sb + k) + 8 * kq;
-          uint32_t om = (openm >> (8 * g)) & 0xFFu;
-          if (jb + 8 > N) om &= N > jb ? (1u << (uint32_t)(N - jb)) - 1u : 0u;
-          if (pn >= N) om = 0u;
-          if (om) {
-            int slot = atomicAdd(&s_qn[pl], __builtin_popcount(om));
-            while (om) {
-              const int j = (int)jb + __builtin_ctz(om);
-              om &= om - 1u;
-              if (slot < DQ_L) {
-                s_q[pl * DQ_L + slot] = j;
-              } else {
-                const int gs = atomicAdd(&qcnt[pn], 1);
-                if (gs < KN_QCAP) qidx[pn * KN_QCAP + gs] = j;
-              }
-              ++slot;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int64_t j = 32 * (sb + k) + 8 * kq + u;
+            if (!((openm >> (8 * g + u)) & 1u) || j >= N || pn >= N) continue;
+            const int slot = atomicAdd(&s_qn[pl], 1);
+            if (slot < DQ_L) {
+              s_q[pl * DQ_L + slot] = (int)j;
+            } else {
+              const int gs = atomicAdd(&qcnt[pn], 1);
+              if (gs < KN_QCAP) qidx[pn * KN_QCAP + gs] = (int)j;
             }
           }
         }
@@ -298,9 +291,10 @@ void knn_dense_kernel(
 // count, those in [T_lo, T_hi) are ranked in (key, index) order, and rank
 // nq - 1 - #below is the selected neighbour (as in knn_select_kernel's
 // steps 3-4).  The members among the queue (below T_lo, or ranked at most
-// the selected one; the rank-0 row excluded) sum their features F_j,f in
-// fp64 (in index order, fixed) into extra[f][n], which
-// mm_finish_kernel adds to the limb sums of the certain members.  A particle flagged by the
+// the selected one; the rank-0 row excluded) add their limbs L_l(F_j,f) into
+// part's chunk 0: integers, so the sums are exactly the ones the MFMA would
+// have formed with those rows' membership set, in any order (deterministic
+// although the queue's order comes from atomics).  A particle flagged by the
 // select, with an overflowing queue or with the rank outside the kept set
 // counts into nfail (the host then reruns the fit with the in-kernel collect).
 template <int D>
@@ -309,10 +303,13 @@ __global__ __launch_bounds__(256) void knn_resolve_kernel(
     const int* __restrict__ need, unsigned long long* __restrict__ sel_v,
     long long* __restrict__ sel_jcut, long long* __restrict__ sel_rank0,
     const int* __restrict__ qcnt, const int* __restrict__ qidx,
-    const int* __restrict__ cbelow, double* __restrict__ extra, int* __restrict__ nfail) {
+    const int* __restrict__ cbelow, const double* __restrict__ bnd,
+    double* __restrict__ part, int* __restrict__ nfail) {
   constexpr int E = KN_QCAP / 64;
+  constexpr int NC = mm_nc<D>();
+  constexpr int CPL = (NC + 63) / 64;
   __shared__ double s_key[4][KN_QCAP];
-  __shared__ int s_idx[4][KN_QCAP], s_ord[4][KN_QCAP];
+  __shared__ int s_idx[4][KN_QCAP];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t n = (int64_t)blockIdx.x * 4 + wv;
   const bool live = n < N;
@@ -373,38 +370,41 @@ __global__ __launch_bounds__(256) void knn_resolve_kernel(
       sel_rank0[n] = r0l;
     }
   }
-  if (live && !ok && lane == 0) atomicAdd(nfail, 1);
-  // members in index order (a deterministic summation order: the queue's
-  // order comes from atomics)
-  __syncthreads();                       // the ranking's LDS reads are done
+  if (live && !ok) {
+    if (lane == 0) atomicAdd(nfail, 1);
+    return;
+  }
+  if (!live) return;
+  // members' limbs: lane owns columns lane + 64 h
+  int ef[CPL];
+  double acc[CPL];
 #pragma unroll
-  for (int i = 0; i < E; ++i) s_idx[wv][lane + 64 * i] = mem[i] ? jj[i] : 0x7FFFFFFF;
-  __syncthreads();
-  int pos[E], nmem = 0;
+  for (int h = 0; h < CPL; ++h) {
+    const int c = lane + 64 * h;
+    ef[h] = c < NC ? mm_fexp<D>(c / ML_NL, bnd) : 0;
+    acc[h] = 0.0;
+  }
 #pragma unroll
-  for (int i = 0; i < E; ++i) { pos[i] = 0; nmem += mem[i] ? 1 : 0; }
-  if (ok)
-    for (int f = 0; f < cnt; ++f) {
-      const int jf = s_idx[wv][f];
-#pragma unroll
-      for (int i = 0; i < E; ++i) pos[i] += jf < jj[i] ? 1 : 0;
-    }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) nmem += __shfl_xor(nmem, o, 64);
-#pragma unroll
-  for (int i = 0; i < E; ++i)
-    if (mem[i]) s_ord[wv][pos[i]] = jj[i];
-  __syncthreads();
-  // members' features in fp64: lane f < NM owns feature f
-  constexpr int NM = local_nm<D>();
-  double acc = 0.0;
-  if (ok && lane < NM)
-    for (int q = 0; q < nmem; ++q) {
-      const int j = s_ord[wv][q];
+  for (int i = 0; i < E; ++i) {
+    unsigned long long m = __builtin_amdgcn_ballot_w64(mem[i]);
+    while (m) {
+      const int src = __builtin_ctzll(m);
+      m &= m - 1;
+      const int j = __shfl(jj[i], src, 64);
       double y[D];
 #pragma unroll
       for (int a = 0; a < D; ++a) y[a] = X[(int64_t)j * D + a] - X[a];
-      acc += mm_feature<D>(lane, w[j], y);
+      const double lw = w[j];
+#pragma unroll
+      for (int h = 0; h < CPL; ++h) {
+        const int c = lane + 64 * h;
+        if (c < NC) acc[h] += mm_limb(mm_feature<D>(c / ML_NL, lw, y), ef[h], c % ML_NL);
+      }
     }
-  if (ok && lane < NM) extra[(int64_t)lane * N + n] = acc;
+  }
+#pragma unroll
+  for (int h = 0; h < CPL; ++h) {
+    const int c = lane + 64 * h;
+    if (c < NC) part[(int64_t)c * N + n] += acc[h];
+  }
 }

@@ -646,3 +646,30 @@ def test_local_fit_knn_keys_at_the_fp32_bound(dev, d, k, jitter):
     covs, inv, dets, chol, lnorm = gpu.local_fit(gpu.as_dev(X), gpu.as_dev(w), k, 1.0, 1e-3)
     np.testing.assert_allclose(covs.cpu().numpy(), ref["covs"], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(dets.cpu().numpy(), ref["dets"], rtol=1e-8)
+
+
+@pytest.mark.parametrize("N,d,k,grid", [(12000, 5, 3000, None), (6000, 3, 1500, 5),
+                                         (4096, 2, 1024, None)])
+def test_local_fit_deferred_collect(dev, N, d, k, grid):
+    """Dense k at d <= 5 runs the deferred collect: the count sweep's bracket
+    goes to the moments sweep, which queues the open pairs in an order set by
+    atomics; the resolve kernel selects among them and sums the queued
+    members in index order.  The fit must equal the oracle's and be
+    bit-identical between runs (every rank of a multi-GPU run fits the same
+    population itself).  The {0..4}^3 grid holds hundreds of exact ties at
+    the k-th distance: the queue overflows and the fit falls back to the
+    select's own collect sweep."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(N + d + k)
+    if grid is None:
+        X = rng.normal(size=(N, d))
+    else:
+        X = rng.integers(0, grid, size=(N, d)).astype(float)
+    w = np.exp(0.3 * rng.standard_normal(N))
+    w /= w.sum()
+    ref = oracle.local_fit(X, w, k=k, k_fraction=None)
+    Xd, wd = gpu.as_dev(X), gpu.as_dev(w)
+    covs = [gpu.local_fit(Xd, wd, k, 1.0, 1e-3)[0].cpu().numpy() for _ in range(3)]
+    np.testing.assert_allclose(covs[0], ref["covs"], rtol=1e-9, atol=1e-12)
+    for c in covs[1:]:
+        np.testing.assert_array_equal(c, covs[0])
