@@ -42,6 +42,10 @@
 // A particle whose window misses the rank or whose list overflows is
 // flagged (need[n] = 1) and re-selected by local_select_kernel (fp64 radix
 // passes, exact for any data).
+// Dense k (defer = 1, the moments run on knn_dense_kernel): the kernel stops
+// after step 2 and leaves [T_lo, T_hi) in sel_v / sel_jcut; the moments
+// sweep does step 3 on its own keys and knn_resolve_kernel step 4
+// (abc_local_dense.h), one N^2 sweep fewer.
 constexpr int KN_PB = 16;    // particles per block
 constexpr int KN_SK = 512;   // sample rows
 constexpr int KN_NB = 520;   // window bins
