@@ -1047,7 +1047,8 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const double* __restrict
                                                         const double* __restrict__ part,
                                                         int RS, const double* __restrict__ bnd,
                                                         double* __restrict__ out,
-                                                        int* __restrict__ flag) {
+                                                        int* __restrict__ flag,
+                                                        const double* __restrict__ extra) {
   constexpr int NM = local_nm<D>(), NCP = 16 * mm_nt<D>();
   const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (n >= N) return;
@@ -1060,6 +1061,7 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const double* __restrict
       for (int y = 0; y < RS; ++y) c += part[((int64_t)y * NCP + f * ML_NL + l) * N + n];
       v += ldexp(c, e - 11 * (l + 1));
     }
+    if (extra) v += extra[(int64_t)f * N + n];   // deferred collect (ABC_DEFER_V2)
     S[f] = v;
     // last-limb rounding per member + the limb sum's own rounding
     E[f] = (double)nq * ldexp(1.0, e - 11 * ML_NL - 1) + 4.0 * MM_EPS * fabs(v);
@@ -1258,10 +1260,11 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
         hipLaunchKernelGGL((knn_resolve_kernel<D>), dim3((unsigned)ceil_div(N, 4)), dim3(256), 0, s,
                            X, w, N, nq, (const int*)knn_need, sel_v, sel_ties, sel_rank0,
                            (const int*)qcnt, (const int*)qidx, (const int*)cbelow,
-                           (const double*)bnd, part16, flag + 1);
+                           (const double*)bnd, part16, part, flag + 1);
         ABC_LAUNCHED();
         hipLaunchKernelGGL((mm_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
-                           X, N, nq, (const double*)part16, RS16, (const double*)bnd, cenm, flag);
+                           X, N, nq, (const double*)part16, RS16, (const double*)bnd, cenm, flag,
+                           (const double*)(ABC_DEFER_V2 ? part : nullptr));
         ABC_LAUNCHED();
         int h_f[2] = {0, 0};
         ABC_HIP(hipMemcpyAsync(h_f, flag, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1304,7 +1307,8 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
     }
     if (!finished) {
       hipLaunchKernelGGL((mm_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
-                         X, N, nq, (const double*)part16, RS16, (const double*)bnd, cenm, flag);
+                         X, N, nq, (const double*)part16, RS16, (const double*)bnd, cenm, flag,
+                         (const double*)nullptr);
       ABC_LAUNCHED();
       ABC_HIP(hipMemcpyAsync(&h_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s));
       ABC_HIP(hipStreamSynchronize(s));

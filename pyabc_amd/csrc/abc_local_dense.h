@@ -75,6 +75,12 @@ __global__ __launch_bounds__(256) void knn_rows_kernel(const double* __restrict_
 // queue per block (DQ_L per particle), flushed to the global queue at the
 // end with one atomic per particle; a full LDS queue spills by global atomics.
 constexpr int DQ_L = 16;
+#ifndef ABC_DEFER_V2
+// build-time A/B (unmeasured): one LDS queue atomic per lane instead of per
+// open pair, and the resolve's queued members summed as NM fp64 features in
+// index order (added by mm_finish_kernel) instead of 110 limb columns
+#define ABC_DEFER_V2 0
+#endif
 template <int D, bool DEFER>
 __global__ __launch_bounds__(DM_T)
 #if ABC_DM_WPE
@@ -213,6 +219,33 @@ void knn_dense_kernel(
         for (int g = 0; g < DM_G; ++g) nin[g] += __builtin_popcount((inm >> (8 * g)) & 0xFFu);
       }
       if (DEFER && __builtin_amdgcn_ballot_w64(openm != 0u) != 0ull) {
+#if ABC_DEFER_V2
+        // queue the open pairs (their a stays 0): one LDS atomic per lane
+        // reserves its slots
+#pragma unroll
+        for (int g = 0; g < DM_G; ++g) {
+          const int64_t pn = p0 + 16 * g + (lane & 15);
+          const int pl = (wv * DM_G + g) * 16 + (lane & 15);
+          const int64_t jb = 32 * (sb + k) + 8 * kq;
+          uint32_t om = (openm >> (8 * g)) & 0xFFu;
+          if (jb + 8 > N) om &= N > jb ? (1u << (uint32_t)(N - jb)) - 1u : 0u;
+          if (pn >= N) om = 0u;
+          if (om) {
+            int slot = atomicAdd(&s_qn[pl], __builtin_popcount(om));
+            while (om) {
+              const int j = (int)jb + __builtin_ctz(om);
+              om &= om - 1u;
+              if (slot < DQ_L) {
+                s_q[pl * DQ_L + slot] = j;
+              } else {
+                const int gs = atomicAdd(&qcnt[pn], 1);
+                if (gs < KN_QCAP) qidx[pn * KN_QCAP + gs] = j;
+              }
+              ++slot;
+            }
+          }
+        }
+#else
         // queue the open pairs (their a stays 0)
 #pragma unroll
         for (int g = 0; g < DM_G; ++g) {
@@ -231,6 +264,7 @@ void knn_dense_kernel(
             }
           }
         }
+#endif
       } else if (!DEFER && __builtin_amdgcn_ballot_w64(openm != 0u) != 0ull) {
         // rare: settle the open pairs in fp64 (rank-0 row excluded)
 #pragma unroll
@@ -304,12 +338,15 @@ __global__ __launch_bounds__(256) void knn_resolve_kernel(
     long long* __restrict__ sel_jcut, long long* __restrict__ sel_rank0,
     const int* __restrict__ qcnt, const int* __restrict__ qidx,
     const int* __restrict__ cbelow, const double* __restrict__ bnd,
-    double* __restrict__ part, int* __restrict__ nfail) {
+    double* __restrict__ part, double* __restrict__ extra, int* __restrict__ nfail) {
   constexpr int E = KN_QCAP / 64;
   constexpr int NC = mm_nc<D>();
   constexpr int CPL = (NC + 63) / 64;
   __shared__ double s_key[4][KN_QCAP];
   __shared__ int s_idx[4][KN_QCAP];
+#if ABC_DEFER_V2
+  __shared__ int s_ord[4][KN_QCAP];
+#endif
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t n = (int64_t)blockIdx.x * 4 + wv;
   const bool live = n < N;
@@ -370,6 +407,43 @@ __global__ __launch_bounds__(256) void knn_resolve_kernel(
       sel_rank0[n] = r0l;
     }
   }
+#if ABC_DEFER_V2
+  if (live && !ok && lane == 0) atomicAdd(nfail, 1);
+  // members in index order (a deterministic summation order: the queue's
+  // order comes from atomics), their NM features summed in fp64 into extra
+  // (mm_finish_kernel adds it to the limb sums)
+  __syncthreads();                       // the ranking's LDS reads are done
+#pragma unroll
+  for (int i = 0; i < E; ++i) s_idx[wv][lane + 64 * i] = mem[i] ? jj[i] : 0x7FFFFFFF;
+  __syncthreads();
+  int pos[E], nmem = 0;
+#pragma unroll
+  for (int i = 0; i < E; ++i) { pos[i] = 0; nmem += mem[i] ? 1 : 0; }
+  if (ok)
+    for (int f = 0; f < cnt; ++f) {
+      const int jf = s_idx[wv][f];
+#pragma unroll
+      for (int i = 0; i < E; ++i) pos[i] += jf < jj[i] ? 1 : 0;
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nmem += __shfl_xor(nmem, o, 64);
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+    if (mem[i]) s_ord[wv][pos[i]] = jj[i];
+  __syncthreads();
+  constexpr int NM = local_nm<D>();
+  double sum = 0.0;
+  if (ok && lane < NM)
+    for (int q = 0; q < nmem; ++q) {
+      const int j = s_ord[wv][q];
+      double y[D];
+#pragma unroll
+      for (int a = 0; a < D; ++a) y[a] = X[(int64_t)j * D + a] - X[a];
+      sum += mm_feature<D>(lane, w[j], y);
+    }
+  if (ok && lane < NM) extra[(int64_t)lane * N + n] = sum;
+  (void)bnd; (void)part;
+#else
   if (live && !ok) {
     if (lane == 0) atomicAdd(nfail, 1);
     return;
@@ -407,4 +481,5 @@ __global__ __launch_bounds__(256) void knn_resolve_kernel(
     const int c = lane + 64 * h;
     if (c < NC) part[(int64_t)c * N + n] += acc[h];
   }
+#endif
 }
