@@ -33,6 +33,13 @@ def test_size_queries_are_pure_host():
         63 * 64 * 3 * 8
     assert nat.query("abc_mvn_logpdf_workspace", 4096, 4096, 10, 0) > 0
     assert nat.query("abc_sort_pairs_workspace", 10 ** 6) > 32 * 10 ** 6
+    # LocalTransition fit: d <= 5 carries the deferred collect's queue (256
+    # row indices per particle) beside the dense moments' buffers
+    n = 10 ** 5
+    for d in (1, 5):
+        assert nat.query("abc_local_fit_workspace", n, d) > n * 256 * 4
+    assert nat.query("abc_local_fit_workspace", 2 * n, 5) > \
+        nat.query("abc_local_fit_workspace", n, 5)
 
 
 def test_invalid_arguments_raise_without_device():
