@@ -11,7 +11,10 @@ on the device; nothing is read from the host inside the timed region except
 the per-round accept counts.  `--pop 100000` runs configs[1] ("c2", the
 one-GPU config); both are reported in DESIGN.md.
 
-Multi-GPU (torch.distributed.run, one rank per GPU, nccl = RCCL): candidates
+Multi-GPU (one rank per GPU, nccl = RCCL): `python bench.py --gpus N` starts
+its N rank processes itself (`spawn_ranks`, the parent never touches the
+GPU); under `torch.distributed.run` (WORLD_SIZE set) each process is one
+rank.  Candidates
 are sharded by global index, each rank weights its own accepted rows against
 the replicated population, the accepted rows are all-gathered ("scaling":
 "strong": the population -- total work -- is fixed as N grows).  The c3
@@ -62,7 +65,94 @@ def parse():
                     help="BatchedGPUSampler.filter_below (default: the sampler's)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: functional multi-rank runs on one GPU (tests)")
+    ap.add_argument("--launcher-check", action="store_true",
+                    help="rendezvous over gloo on the CPU, exchange one value per "
+                         "rank and print the rank count; no GPU (tests the launcher)")
     return ap.parse_args()
+
+
+def launcher_check():
+    import torch
+    import torch.distributed as dist
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if os.environ.get("BENCH_LAUNCHER_FAIL_RANK") == str(rank):
+        sys.exit(3)     # the launcher test's failing rank
+    if ws > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([float(rank), 1.0], dtype=torch.float64)
+    if ws > 1:
+        dist.all_reduce(t)
+    got = [None] * ws
+    if ws > 1:
+        dist.all_gather_object(got, (rank, int(os.environ.get("LOCAL_RANK", "0")), os.getpid()))
+        dist.destroy_process_group()
+    else:
+        got = [(0, 0, os.getpid())]
+    if rank == 0:
+        print(json.dumps({"launcher_check": True, "n_gpus": ws,
+                          "rank_sum": t[0].item(), "ranks": t[1].item(),
+                          "local_ranks": [g[1] for g in got],
+                          "distinct_pids": len({g[2] for g in got})}), flush=True)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv=None):
+    """`python bench.py --gpus N` with no WORLD_SIZE in the environment: start
+    N rank processes of this script (RANK = LOCAL_RANK = i, WORLD_SIZE = N,
+    MASTER_ADDR 127.0.0.1, a free MASTER_PORT) and wait for all of them -- the
+    process fan-out of the reference's MulticoreEvalParallelSampler
+    (multicore_evaluation_parallel.py:92-150), one process per GPU.  This
+    parent never touches the GPU (no torch import); the children are started
+    as new processes, never exec'd over it.  Returns the first non-zero child
+    exit code (a failed rank kills the others), else 0."""
+    import signal
+    import subprocess
+    argv = list(sys.argv[1:] if argv is None else argv)
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                   MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                   MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)]
+                                      + argv, env=env, start_new_session=True))
+    rc = 0
+    live = set(range(n))
+    try:
+        while live:
+            for r in sorted(live):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                live.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench: rank {r} exited with {code}; stopping the others",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        try:
+                            os.killpg(procs[q].pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        raise
+    for p in procs:
+        p.wait()
+    return rc
 
 
 def setup_dist(backend="nccl"):
@@ -243,6 +333,10 @@ def measured_traffic(args, n_pop):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.launcher_check:
+        return launcher_check()
     import torch
     rank, ws = setup_dist(args.dist_backend)
     if ws != args.gpus and rank == 0:
@@ -345,9 +439,12 @@ def main():
     avg_m = k_pairs / max(k_n, 1) / n_pop if k_n else 0
     algo_bytes = ((n_pop + avg_m) * kb * 64 + avg_m * 8) if kb else None
     out = None
+    if ws > 1:
+        # every rank is done with the GPU; rank 0 alone times the host leg
+        torch.distributed.destroy_process_group()
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and ws == 1:
+        if not args.no_cpu_baseline:
             hist = abc.history
             df, w = hist.get_distribution(0, hist.max_t)
             cores = max(1, min(args.cpu_cores, os.cpu_count() or 1))
@@ -424,8 +521,6 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
-    if ws > 1:
-        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

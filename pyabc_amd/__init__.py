@@ -9,7 +9,8 @@ import logging
 import os
 
 from .parameters import Parameter
-from .random_variables import Distribution, RV, RVBase
+from .random_variables import (Distribution, RV, RVBase, RVDecorator,
+                               LowerBoundDecorator)
 from .distance import (Distance, NoDistance, IdentityFakeDistance,
                        AcceptAllDistance, SimpleFunctionDistance,
                        PNormDistance, AdaptivePNormDistance, to_distance,
@@ -30,10 +31,11 @@ from .acceptor import (Acceptor, SimpleFunctionAcceptor, UniformAcceptor,
                        StochasticAcceptor, pdf_norm_from_kernel,
                        pdf_norm_max_found, ScaledPDFNorm)
 from . import distance, epsilon, acceptor, storage
-from .model import (Model, SimpleModel, ModelResult, VectorizedModel,
-                    LinearGaussianModel)
+from .model import (Model, SimpleModel, ModelResult, IntegratedModel,
+                    VectorizedModel, LinearGaussianModel)
 from .transition import (Transition, MultivariateNormalTransition,
-                         LocalTransition, NotEnoughParticles)
+                         LocalTransition, DiscreteRandomWalkTransition,
+                         NotEnoughParticles)
 from .population import Particle, Population
 from .populationstrategy import (ConstantPopulationSize, PopulationStrategy,
                                  AdaptivePopulationSize, ListPopulationSize)

@@ -51,7 +51,6 @@
 // underflows 2^-60 relative to max w (all pairs beyond ~11 kernel widths),
 // are recomputed in fp64 from the whitened population Y and log2 weights lw
 // stored after the fragments (rescue list; empty in practice).
-#include <stdlib.h>
 #include "abc_common.h"
 
 namespace abc {
@@ -313,10 +312,7 @@ template <int KB, int CT, bool PASS1>
 __global__ __launch_bounds__(256) void mvn_x3_kernel(
     const half8* __restrict__ A, const half8* __restrict__ Bi, int64_t MT,
     int64_t NT, int nchunk, int64_t tiles_per_chunk, int64_t ngroups, int koff,
-    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad,
-    int mode) {
-  // mode (timing experiments only; results are wrong unless 0):
-  // 1 = pass 1 only, 2 = pass 2 only
+    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t bid = blockIdx.x;
@@ -349,7 +345,7 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
   // ---- pass 1: exact s_hi (offset slot still 0) -> column max -> o.
   // Block-0 fragments through a ring of 4 registers (prefetch distance 4).
   float o[CT];
-  if (PASS1 && t_begin < t_end && mode != 2) {
+  if (PASS1 && t_begin < t_end) {
     float mx[CT];
 #pragma unroll
     for (int c = 0; c < CT; ++c) mx[c] = -INFINITY;
@@ -382,10 +378,6 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
     for (int c = 0; c < CT; ++c) o[c] = O_MIN;
   }
 
-  if (mode == 1) {
-    if (lane < 16) part_l[(int64_t)chunk * Mpad + ct0 * 16 + lane] = o[0];
-    return;
-  }
   // ---- pass 2: full limb-split GEMM, exp2, sums.  Two register buffers of
   // population fragments (prefetch distance 2).  Work runs as a stream of
   // (tile, c) units: the MFMA chain of unit u is issued next to the
@@ -679,15 +671,6 @@ size_t plan_x3_ws(const PlanX3& p) {
   return off + 256;
 }
 
-int debug_mode() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("ABC_X3_DEBUG_MODE");
-    m = e ? atoi(e) : 0;
-  }
-  return m;
-}
-
 template <int KB, int CT>
 void launch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
                double* po, double* pl, bool pass1, hipStream_t s) {
@@ -695,13 +678,11 @@ void launch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
   if (pass1)
     hipLaunchKernelGGL((mvn_x3_kernel<KB, CT, true>), dim3((unsigned)blocks),
                        dim3(256), 0, s, A, B, p.MT, p.NT, p.nchunk,
-                       p.tiles_per_chunk, p.groups, koff, po, pl, p.Mpad,
-                       debug_mode());
+                       p.tiles_per_chunk, p.groups, koff, po, pl, p.Mpad);
   else
     hipLaunchKernelGGL((mvn_x3_kernel<KB, CT, false>), dim3((unsigned)blocks),
                        dim3(256), 0, s, A, B, p.MT, p.NT, p.nchunk,
-                       p.tiles_per_chunk, p.groups, koff, po, pl, p.Mpad,
-                       debug_mode());
+                       p.tiles_per_chunk, p.groups, koff, po, pl, p.Mpad);
 }
 
 int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,

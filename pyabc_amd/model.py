@@ -55,6 +55,22 @@ class Model:
         return result
 
 
+class IntegratedModel(Model):
+    """A model that simulates and decides acceptance in one call, so it can
+    stop a simulation early once eps is out of reach (the role of
+    pyabc/model.py:273-328).  Subclasses implement ``integrated_simulate``
+    and return ``ModelResult(accepted=False)`` for a rejection, or
+    ``ModelResult(accepted=True, distance=..., sum_stats=...)``.  Runs on the
+    per-candidate path (it is not a ``VectorizedModel``)."""
+
+    def integrated_simulate(self, pars, eps: float) -> ModelResult:
+        raise NotImplementedError()
+
+    def accept(self, t, pars, sum_stats_calculator, distance_calculator,
+               eps_calculator, acceptor, x_0):
+        return self.integrated_simulate(pars, eps_calculator(t))
+
+
 class SimpleModel(Model):
     def __init__(self, sample_function, name=None):
         if name is None:

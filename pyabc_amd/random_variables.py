@@ -17,8 +17,10 @@ device prior kinds of include/abcgpu.h:
   and the draws stay keyed by the global candidate index.
 
 The HOST kind assumes the density is positive inside the support interval
-(true of scipy's continuous families); a prior whose density vanishes
-inside its support is re-drawn by the reference and is not covered.
+(true of scipy's continuous families).  Discrete distributions outside the
+device families and non-frozen scipy objects have no batched form
+(``device_spec`` is None): such priors run the per-candidate loop, which
+re-draws until the prior density is positive as the reference does.
 """
 import logging
 from abc import ABC, abstractmethod
@@ -117,15 +119,28 @@ class RV(RVBase):
     # -- batched-sampler description -----------------------------------------
     @property
     def is_discrete(self):
-        return not hasattr(self.distribution.dist, "pdf")
+        import scipy.stats
+        dist = getattr(self.distribution, "dist", self.distribution)
+        return (isinstance(dist, scipy.stats.rv_discrete)
+                or not hasattr(dist, "pdf"))
 
     def device_spec(self):
         """(kind, [4 params]) for the device kernels: a device family, or
-        ABC_PRIOR_HOST with (lo, hi, centre) of the support interval."""
+        ABC_PRIOR_HOST with (lo, hi, centre) of the support interval; None
+        when the component has no batched form.  That is the case for a
+        discrete distribution outside the device families (its pmf vanishes
+        between the support's points, where the reference re-draws,
+        smc.py:649-662, and the support box cannot) and for anything that is
+        not a frozen continuous scipy distribution (e.g. ``rv_discrete(values=
+        ...)``, a bare distribution object)."""
+        import scipy.stats
         from ._native import PRIOR_KINDS
         fam = self._device_family_params()
         if fam is not None:
             return PRIOR_KINDS[self.name], fam
+        if (not isinstance(self.distribution, scipy.stats._distn_infrastructure.rv_frozen)
+                or self.is_discrete):
+            return None
         lo, hi = (float(v) for v in self.distribution.support())
         if np.isfinite(lo) and np.isfinite(hi):
             c = 0.5 * (lo + hi)
@@ -169,6 +184,85 @@ class RV(RVBase):
     def host_ppf(self, u):
         return np.asarray(self.distribution.ppf(np.asarray(u, np.float64)),
                           dtype=np.float64)
+
+
+class RVDecorator(RVBase):
+    """Wraps a prior component (``self.component``) and forwards to it;
+    subclasses override what they change (pyabc random_variables.py:199-260).
+    ``repr`` is ``[<decorator_repr()>]<component repr>``.  Decorated
+    components have no batched form: priors that use them run the
+    per-candidate loop."""
+
+    def __init__(self, component: RVBase):
+        self.component = component
+
+    def rvs(self, *args, **kwargs):
+        return self.component.rvs(*args, **kwargs)
+
+    def pmf(self, x, *args, **kwargs):
+        return self.component.pmf(x, *args, **kwargs)
+
+    def pdf(self, x, *args, **kwargs):
+        return self.component.pdf(x, *args, **kwargs)
+
+    def cdf(self, x, *args, **kwargs):
+        return self.component.cdf(x, *args, **kwargs)
+
+    def copy(self):
+        return type(self)(self.component.copy())
+
+    def decorator_repr(self) -> str:
+        return "Decorator"
+
+    def __repr__(self):
+        return f"[{self.decorator_repr()}]{self.component!r}"
+
+
+class LowerBoundDecorator(RVDecorator):
+    """The component conditioned on X > lower_bound (pyabc
+    random_variables.py:263-325): rejection draws (at most MAX_TRIES, then
+    None), densities and cdf renormalised by the mass above the bound."""
+
+    MAX_TRIES = 10000
+
+    def __init__(self, component: RVBase, lower_bound: float):
+        if component.cdf(lower_bound) == 1:
+            raise Exception("LowerBoundDecorator: Conditioning on a set of "
+                            "measure zero.")
+        super().__init__(component)
+        self.lower_bound = lower_bound
+
+    def copy(self):
+        return type(self)(self.component.copy(), self.lower_bound)
+
+    def decorator_repr(self):
+        return f"Lower: X > {self.lower_bound:2f}"
+
+    def _mass_above(self):
+        return 1 - self.component.cdf(self.lower_bound)
+
+    def rvs(self, *args, **kwargs):
+        tries = 0
+        while tries < self.MAX_TRIES:
+            tries += 1
+            x = self.component.rvs()
+            if not x <= self.lower_bound:     # NaN passes, as in the reference
+                return x
+        return None
+
+    def pdf(self, x, *args, **kwargs):
+        return 0. if x <= self.lower_bound else \
+            self.component.pdf(x) / self._mass_above()
+
+    def pmf(self, x, *args, **kwargs):
+        return 0. if x <= self.lower_bound else \
+            self.component.pmf(x) / self._mass_above()
+
+    def cdf(self, x, *args, **kwargs):
+        if x <= self.lower_bound:
+            return 0.
+        below = self.component.cdf(self.lower_bound)
+        return (self.component.cdf(x) - below) / (1 - below)
 
 
 class Distribution(ParameterStructure):
@@ -217,9 +311,10 @@ class Distribution(ParameterStructure):
         kinds, params = [], []
         for name in self.get_parameter_names():
             rv = self[name]
-            if not hasattr(rv, "device_spec"):
+            spec = rv.device_spec() if hasattr(rv, "device_spec") else None
+            if spec is None:
                 return None
-            kind, par = rv.device_spec()
+            kind, par = spec
             kinds.append(kind)
             params.extend(par)
         return np.asarray(kinds, dtype=np.int32), np.asarray(params, np.float64)
@@ -231,7 +326,8 @@ class Distribution(ParameterStructure):
         out = []
         for col, name in enumerate(self.get_parameter_names()):
             rv = self[name]
-            if hasattr(rv, "device_spec") and rv.device_spec()[0] == PRIOR_KINDS["host"]:
+            spec = rv.device_spec() if hasattr(rv, "device_spec") else None
+            if spec is not None and spec[0] == PRIOR_KINDS["host"]:
                 out.append((col, rv))
         return out
 

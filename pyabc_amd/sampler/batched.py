@@ -132,8 +132,12 @@ class BatchedGPUSampler(Sampler):
                  max_attempts=10000, check_max_eval=False, fused=True,
                  max_fused_batch_size=1 << 31, filter_below=0.0,
                  filter_min_stats=5, record_budget_bytes=1 << 31,
-                 record_device_budget_bytes=None):
+                 record_device_budget_bytes=None, allow_per_candidate=True):
         super().__init__()
+        # a generation without a batched form (plain closure, non-vectorised
+        # model, discrete host prior, ...) runs the per-candidate loop with a
+        # warning; False makes it a TypeError instead
+        self.allow_per_candidate = allow_per_candidate
         self.check_max_eval = check_max_eval
         self.batch_size = batch_size
         self.max_batch_size = max_batch_size
@@ -375,8 +379,13 @@ class BatchedGPUSampler(Sampler):
         batch of one).  With several ranks rank 0 runs the loop and the
         sample is broadcast, so every rank holds the same population."""
         why = getattr(simulate_one, "why_not", "")
-        logger.info("BatchedGPUSampler: per-candidate loop (%s)",
-                    why or type(simulate_one).__name__)
+        if not self.allow_per_candidate:
+            raise TypeError("BatchedGPUSampler: this generation has no batched "
+                            "form (" + (why or type(simulate_one).__name__)
+                            + ") and allow_per_candidate=False")
+        logger.warning("BatchedGPUSampler: per-candidate loop, orders of "
+                       "magnitude slower than the batched path (%s)",
+                       why or type(simulate_one).__name__)
         rank, ws = dd.world()
         res = None
         if rank == 0:
@@ -694,8 +703,10 @@ class BatchedGPUSampler(Sampler):
         the staged path's proposals through the fused kernel's propose_one
         (ancestor table, support box computed once per launch; the same bits
         as gpu.propose).  None when the transition has no proposal arrays."""
-        key = (id(spec), seed, gen)
-        if getattr(self, "_prop_key", None) == key:
+        # keyed on the spec object itself (held here, so its id cannot be
+        # reused by a later run's spec while the entry lives)
+        key = (seed, gen)
+        if getattr(self, "_prop_spec", None) is spec and self._prop_key == key:
             return self._prop_round
         arrays = None
         if spec.transition is not None:
@@ -709,7 +720,7 @@ class BatchedGPUSampler(Sampler):
                                 spec.prior_params, torch.zeros(1, dtype=torch.int32, device=dev),
                                 z, z, z, z, 2.0, seed, gen, self.max_attempts,
                                 **(arrays or {}))
-        self._prop_key, self._prop_round = key, fr
+        self._prop_spec, self._prop_key, self._prop_round = spec, key, fr
         return fr
 
     def _propose(self, spec, B, seed, gen, lo, d):

@@ -98,7 +98,9 @@ class GenerationSpec:
         prior = abc.parameter_priors[0]
         spec = prior.device_spec() if hasattr(prior, "device_spec") else None
         if spec is None:
-            why.append("prior component that is not a scipy-backed RV")
+            why.append("prior component without a batched form (not a scipy "
+                       "RV, or a discrete / non-frozen scipy distribution "
+                       "outside the device families)")
         # components without a device sampler: host-scipy density / draws
         self.host_prior = prior.host_components() if spec is not None else []
         self.why_not = "; ".join(why)
@@ -159,8 +161,12 @@ class ModelPerturbationKernel:
         return 0 if row.size == 1 else int(np.random.choice(row.size, p=row))
 
     def pmf(self, n: int, m: int) -> float:
+        # the reference accepts n == nr_of_models (mass 0) and raises beyond
+        # (random_variables.py:527-531)
+        if not 0 <= n <= self.nr_of_models:
+            raise Exception("n and m have to be between 0 and nr_of_models - 1")
         row = self._row(int(m))
-        return float(row[n]) if 0 <= n < row.size else 0.0
+        return float(row[n]) if n < row.size else 0.0
 
 
 class ABCSMC:

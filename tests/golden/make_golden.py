@@ -323,6 +323,57 @@ def gen_e2e_samples(seeds=(0, 1, 2, 3)):
     np.savez_compressed(os.path.join(HERE, "e2e_reference_samples.npz"), **out)
 
 
+def gen_e2e_large(seeds=(0, 1, 2), pop=10_000, n_procs=8):
+    """Final populations of reference runs at N = 1e4 (MulticoreEval on this
+    container's cores): the c1 model (1-D, x_0 = 2, 8 generations, as
+    gen_e2e) and the 10-D conjugate model (x_0 = 1, QuantileEpsilon(0.5), 4
+    generations).  Targets of the N = 1e4 KS / moment tests
+    (tests/test_gpu_e2e.py), whose thresholds are the reference's
+    test_abc_smc_algorithm.py:354-394.  Samples stored as float32 (the KS
+    statistic needs no more), weights as float64."""
+    from pyabc.sampler import MulticoreEvalParallelSampler
+    out = {}
+    d = 10
+    nm = [f"p{k}" for k in range(d)]
+    keys = [f"y{k}" for k in range(d)]
+    for s in seeds:
+        np.random.seed(s)
+        t0 = time.time()
+
+        def model1(p):
+            return {"y": p["x"] + 0.5 * np.random.randn()}
+        abc = pyabc.ABCSMC(model1, pyabc.Distribution(x=pyabc.RV("norm", 0, 1)),
+                           pyabc.PNormDistance(), population_size=pop,
+                           sampler=MulticoreEvalParallelSampler(n_procs=n_procs))
+        abc.new("sqlite://", {"y": 2.0})
+        h = abc.run(max_nr_populations=8)
+        df, w = h.get_distribution(0, h.max_t)
+        out[f"c1_seed{s}__x"] = df["x"].values.astype(np.float32)
+        out[f"c1_seed{s}__w"] = w
+        out[f"c1_seed{s}__eps"] = h.get_all_populations()["epsilon"].values
+        print("large c1", s, float((df["x"].values * w).sum()),
+              round(time.time() - t0, 1), "s", flush=True)
+    for s in seeds:
+        np.random.seed(s)
+        t0 = time.time()
+
+        def model10(p):
+            return {keys[k]: p[nm[k]] + 0.5 * np.random.randn() for k in range(d)}
+        prior = pyabc.Distribution(**{n: pyabc.RV("norm", 0, 1) for n in nm})
+        abc = pyabc.ABCSMC(model10, prior, pyabc.PNormDistance(),
+                           population_size=pop, eps=QuantileEpsilon(alpha=0.5),
+                           sampler=MulticoreEvalParallelSampler(n_procs=n_procs))
+        abc.new("sqlite://", {k: 1.0 for k in keys})
+        h = abc.run(max_nr_populations=4)
+        df, w = h.get_distribution(0, h.max_t)
+        out[f"d10_seed{s}__X"] = df[nm].values.astype(np.float32)
+        out[f"d10_seed{s}__w"] = w
+        out[f"d10_seed{s}__eps"] = h.get_all_populations()["epsilon"].values
+        print("large d10", s, (df[nm].values * w[:, None]).sum(0).mean(),
+              out[f"d10_seed{s}__eps"], round(time.time() - t0, 1), "s", flush=True)
+    np.savez_compressed(os.path.join(HERE, "e2e_reference_large.npz"), **out)
+
+
 def gen_cv(seeds=tuple(range(24))):
     """Bootstrapped KDE CV (pyabc/cv/bootstrap.py:44-110) and the population
     size predicted from it (transition/predict_population_size.py).
@@ -589,6 +640,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if "--e2e10" in sys.argv:
         gen_e2e10()
+        sys.exit(0)
+    if "--e2e-large" in sys.argv:
+        gen_e2e_large()
         sys.exit(0)
     if "--e2e-samples" in sys.argv:
         gen_e2e_samples()

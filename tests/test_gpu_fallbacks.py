@@ -206,3 +206,69 @@ def test_local_transition_wide_generations():
         ref = np.exp(lw - lw.max())
         ref /= ref.sum()
         np.testing.assert_allclose(w, ref, rtol=1e-8, atol=0)
+
+
+def test_discrete_prior_per_candidate_loop():
+    """A poisson prior has no batched form (its pmf vanishes between the
+    integers, where the reference re-draws, smc.py:649-662): the generation
+    runs the per-candidate loop with DiscreteRandomWalkTransition, so every
+    particle is an integer with positive prior mass and positive weight, and
+    allow_per_candidate=False turns the fallback into a TypeError."""
+    import pyabc_amd as pa
+    np.random.seed(21)
+    prior = pa.Distribution(k=pa.RV("poisson", 3))
+    assert prior.device_spec() is None
+    assert pa.Distribution(k=pa.RV("rv_discrete", values=([0, 1], [.5, .5]))) \
+        .device_spec() is None
+
+    def model(p):
+        return {"y": p["k"] + 0.5 * np.random.randn()}
+    sampler = pa.BatchedGPUSampler()
+    abc = pa.ABCSMC(model, prior, pa.PNormDistance(), population_size=200,
+                    transitions=pa.DiscreteRandomWalkTransition(n_steps=2),
+                    sampler=sampler)
+    abc.new("sqlite://", {"y": 4.0})
+    h = abc.run(max_nr_populations=3)
+    assert h.max_t == 2
+    assert sampler.last_stats.get("per_candidate")
+    for t in range(h.max_t + 1):
+        df, w = h.get_distribution(0, t)
+        k = df["k"].to_numpy()
+        assert np.array_equal(k, np.rint(k)) and (k >= 0).all()
+        assert (w > 0).all() and abs(w.sum() - 1) < 1e-12
+    strict = pa.BatchedGPUSampler(allow_per_candidate=False)
+    abc2 = pa.ABCSMC(model, prior, pa.PNormDistance(), population_size=20,
+                     transitions=pa.DiscreteRandomWalkTransition(), sampler=strict)
+    abc2.new("sqlite://", {"y": 4.0})
+    with pytest.raises(TypeError, match="allow_per_candidate"):
+        abc2.run(max_nr_populations=1)
+
+
+def test_sampler_reused_across_runs():
+    """One BatchedGPUSampler (fixed seed) drives two ABCSMC runs in a row; the
+    staged path's cached proposal round must belong to the current run: the
+    second run equals the same run on a fresh sampler, bit for bit."""
+    import pyabc_amd as pa
+    names, keys = ["a", "b"], ["y0", "y1"]
+
+    def sim(theta, seed, gen, idx0):
+        g = torch.Generator(device=theta.device)
+        g.manual_seed((seed * 1000003 + gen * 7919 + idx0) % (2 ** 63))
+        return theta + 0.5 * torch.randn(theta.shape, generator=g,
+                                          dtype=theta.dtype, device=theta.device)
+
+    def run(sampler, scale):
+        prior = pa.Distribution(a=pa.RV("norm", 0, scale), b=pa.RV("norm", 0, scale))
+        abc = pa.ABCSMC(pa.VectorizedModel(sim, keys), prior, pa.PNormDistance(p=2),
+                        population_size=2000, sampler=sampler,
+                        eps=pa.QuantileEpsilon(alpha=0.5))
+        abc.new("sqlite://", {"y0": 1.0, "y1": 0.5})
+        h = abc.run(max_nr_populations=3)
+        return [h.get_distribution(0, t) for t in range(h.max_t + 1)]
+    shared = pa.BatchedGPUSampler(seed=9)
+    run(shared, 1.0)
+    second = run(shared, 3.0)
+    fresh = run(pa.BatchedGPUSampler(seed=9), 3.0)
+    for (df1, w1), (df2, w2) in zip(second, fresh):
+        np.testing.assert_array_equal(df1[names].to_numpy(), df2[names].to_numpy())
+        np.testing.assert_array_equal(w1, w2)

@@ -3,9 +3,12 @@
 BIT-IDENTICAL populations, weights, epsilons and evaluation counts to the
 single-rank run (draws keyed by the global candidate index,
 first-n-accepted cutoff in global order, x3 density summation order
-independent of the sharding).  The RCCL (nccl) path runs the same code; it
-is exercised by bench.py on the 8-GPU node.
+independent of the sharding).  The RCCL (nccl) path runs the same code: a
+plain `python bench.py --gpus N` starts N ranks itself (bench.spawn_ranks),
+so the driver's scaling run measures it; here bench.py's self-launched
+multi-rank path runs with gloo on the one GPU (test_bench_spawned_ranks).
 """
+import json
 import os
 import socket
 import subprocess
@@ -82,3 +85,24 @@ def test_sharded_adaptive_population_size(tmp_path):
     assert len(set(ref["sizes"])) > 1          # the size did adapt
     for k in ("theta", "w", "eps", "samples", "sizes"):
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def test_bench_spawned_ranks():
+    """`python bench.py --gpus 2` with no WORLD_SIZE: bench.py starts its two
+    rank processes itself; rank 0 prints one line with n_gpus = 2 and a CPU
+    baseline (timed after the ranks left the GPU)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--dist-backend", "gloo", "--pop", "20000", "--steps", "2",
+                        "--warmup", "1", "--cpu-baseline-seconds", "2",
+                        "--cpu-cores", "2"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 2
+    assert out["config"]["dist_backend"] == "gloo"
+    assert out["value"] > 0
+    assert out["cpu_baseline"] is not None and out["cpu_baseline"]["value"] > 0

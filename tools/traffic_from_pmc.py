@@ -3,6 +3,14 @@
     python tools/traffic_from_pmc.py <pmc_dir_root> <kernel-substring> \
         <population> <d> <out.json>
 
+The substring must select ONE instantiation (e.g. "mvn_x3_kernel<3, 8, false>",
+the main c3 launch; "mvn_x3_kernel<3, 8, true>" is the small unhinted rescue
+pass, ~1% of the bytes): dispatches are grouped by their full kernel name and
+the tool refuses a substring that matches more than one name, so launches of
+different shapes are never averaged together.  Only dispatches at least 10%
+of the largest matching one's FETCH_SIZE are kept (the same instantiation
+also runs small rescue subsets).
+
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction
 (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of
 16-B-per-lane streaming reads (the x3 kernel's fragment loads are 16 B per
@@ -17,25 +25,38 @@ import sys
 from collections import defaultdict
 
 
-def main():
-    root, pat, pop, d, out = sys.argv[1:6]
-    vals = defaultdict(list)
+def collect(root, pat):
+    by_name = defaultdict(lambda: defaultdict(dict))   # name -> counter -> dispatch -> v
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"),
                        recursive=True):
         for r in csv.DictReader(open(f)):
-            if pat in r["Kernel_Name"] and r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    fetch = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
-    write = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
-    res = {"kernel": pat, "population": int(pop), "candidates": int(pop),
-           "d": int(d), "fetch_size_kib": fetch, "write_size_kib": write,
-           "fetch_correction": 2.0,
-           "traffic_bytes": 2.0 * fetch * 1024 + write * 1024,
-           "dispatches": len(vals["FETCH_SIZE"]),
-           "note": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate "
-                   "runs of `bench.py --steps 3 --warmup 1`; FETCH doubled "
-                   "(gfx950 16 B/lane streaming-read correction); includes "
-                   "Infinity-Cache hits"}
+            c = r["Counter_Name"]
+            if pat in r["Kernel_Name"] and c in ("FETCH_SIZE", "WRITE_SIZE"):
+                key = (f, r.get("Dispatch_Id") or r.get("Correlation_Id"))
+                by_name[r["Kernel_Name"]][c][key] = (
+                    by_name[r["Kernel_Name"]][c].get(key, 0.0) + float(r["Counter_Value"]))
+    return by_name
+
+
+def main():
+    root, pat, pop, d, out = sys.argv[1:6]
+    by_name = collect(root, pat)
+    if len(by_name) != 1:
+        sys.exit(f"substring {pat!r} matches {len(by_name)} kernel names: "
+                 + "; ".join(n[:120] for n in by_name))
+    name, vals = next(iter(by_name.items()))
+    res = {"kernel": pat, "kernel_name": name[:200], "population": int(pop),
+           "candidates": int(pop), "d": int(d), "fetch_correction": 2.0}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        v = list(vals[c].values())
+        big = [x for x in v if x >= 0.1 * max(v)]
+        res[c.lower() + "_kib"] = sum(big) / len(big)
+        res[c.lower() + "_dispatches"] = len(big)
+        res[c.lower() + "_dispatches_dropped"] = len(v) - len(big)
+    res["traffic_bytes"] = 2.0 * res["fetch_size_kib"] * 1024 + res["write_size_kib"] * 1024
+    res["note"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate runs; "
+                   "one kernel instantiation; FETCH doubled (gfx950 16 B/lane "
+                   "streaming-read correction); includes Infinity-Cache hits")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
