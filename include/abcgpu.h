@@ -305,6 +305,22 @@ int abc_candidates_propose(const abc_candidate_spec* spec, int64_t idx0, int64_t
                            double* theta, double* prior_logpdf, int64_t* ancestor,
                            int32_t* attempts, void* ws, size_t ws_bytes, void* stream);
 
+/* Accept tail of a user simulator's round: PNormDistance of every row of
+ * x [B x S] to x0 with weights*factors wf (pyabc/distance/distance.py:79-105,
+ * the arithmetic of abc_pnorm per row) and the UniformAcceptor test d <= eps
+ * (acceptor/acceptor.py:235-244) in one pass; rows whose attempts exceed
+ * max_attempts (nullable) are rejected (abc_mask_gave_up).  Writes the
+ * positions of the first `cap` accepted rows (increasing) to idx and the
+ * number accepted (uncapped) to *count (device int64); no distance array.
+ * Replaces, for VectorizedModels without a fused simulator, the staged
+ * abc_pnorm + abc_mask_gave_up + abc_accept_compact of one round
+ * (the per-candidate accept of pyabc/model.py:163-218 via smc.py:664-724).
+ * Workspace: abc_candidates_workspace(B) bytes. */
+int abc_pnorm_accept(const double* x, int64_t B, int S, const double* x0,
+                     const double* wf, double p, double eps, const int32_t* attempts,
+                     int max_attempts, int64_t cap, int64_t* idx, int64_t* count,
+                     void* ws, size_t ws_bytes, void* stream);
+
 /* Gather rows: out[i, :] = in[idx[i], :] (row width `cols` doubles). */
 int abc_gather_rows(const double* in, const int64_t* idx, int64_t n, int cols,
                     double* out, void* stream);

@@ -402,6 +402,114 @@ __global__ __launch_bounds__(256) void fused_propose_kernel(
   }
 }
 
+// ---- the accept tail of user simulators ---------------------------------------
+// A VectorizedModel without a fused simulator hands the sampler its sum stats
+// x [B x S]; one pass over them computes PNormDistance (distance.py:79-105)
+// and the UniformAcceptor test d <= eps (acceptor.py:235-244) and leaves only
+// the accept bits + per-tile counts of the fused round, whose scan and
+// bits_write turn them into the positions of the first `cap` accepted: no
+// distance array is written and re-read.  The arithmetic per row is
+// pnorm_row_kernel's (S <= 32: thread per row, k order) or pnorm_wave_kernel's
+// (wide rows: lane-strided partials then the wave tree), so the decision is
+// the one dist <= eps of abc_pnorm's value would give, and the kept rows'
+// distances recomputed by abc_pnorm are those bits.  A proposal that gave up
+// on the prior support (attempts > max_attempts) is never accepted, as
+// abc_mask_gave_up's NaN.
+constexpr int PA_ROWS = 8;    // rows in flight per wave (wide path)
+template <bool WIDE>
+__global__ __launch_bounds__(FR_T) void pnorm_accept_kernel(
+    const double* __restrict__ x, int64_t B, int S, const double* __restrict__ x0,
+    const double* __restrict__ wf, double p, double eps, const int32_t* __restrict__ att,
+    int max_attempts, uint64_t* __restrict__ bits, int64_t* __restrict__ tile_cnt) {
+  __shared__ uint32_t tbits[FR_TILE / 32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t tile0 = (int64_t)blockIdx.x * FR_TILE;
+  if (tid < FR_TILE / 32) tbits[tid] = 0u;
+  __syncthreads();
+  const bool inf = isinf(p);
+  auto finish = [&](double t) {
+    return inf ? t : ((p == 1.0) ? t : (p == 2.0 ? sqrt(t) : pow(t, 1.0 / p)));
+  };
+  auto ok = [&](int64_t b) { return att == nullptr || att[b] <= max_attempts; };
+  if (!WIDE) {
+#pragma unroll 1
+    for (int it = 0; it < FR_CPT; ++it) {
+      const int loc = it * FR_T + tid;
+      const int64_t b = tile0 + loc;
+      if (b >= B) break;
+      const double* xr = x + b * S;
+      double s = 0.0;
+      if (inf) {
+        for (int k = 0; k < S; ++k) s = fmax(s, fabs(wf[k] * (xr[k] - x0[k])));
+      } else {
+        for (int k = 0; k < S; ++k) s += pterm(fabs(wf[k] * (xr[k] - x0[k])), p);
+      }
+      if (finish(s) <= eps && ok(b)) atomicOr(&tbits[loc >> 5], 1u << (loc & 31));
+    }
+  } else {
+    // wave w takes rows w * PA_ROWS + 4 PA_ROWS i of the tile
+#pragma unroll 1
+    for (int r0 = wave * PA_ROWS; r0 < FR_TILE; r0 += 4 * PA_ROWS) {
+      const int64_t b0 = tile0 + r0;
+      if (b0 >= B) break;  // wave-uniform
+      double sr[PA_ROWS];
+#pragma unroll
+      for (int r = 0; r < PA_ROWS; ++r) sr[r] = 0.0;
+      for (int k = lane; k < S; k += 64) {
+        const double wk = wf[k], ck = x0[k];
+        double v[PA_ROWS];
+#pragma unroll
+        for (int r = 0; r < PA_ROWS; ++r) v[r] = b0 + r < B ? x[(b0 + r) * S + k] : ck;
+#pragma unroll
+        for (int r = 0; r < PA_ROWS; ++r) {
+          const double a = fabs(wk * (v[r] - ck));
+          sr[r] = inf ? fmax(sr[r], a) : sr[r] + pterm(a, p);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < PA_ROWS; ++r) {
+        const double t = inf ? wave_max(sr[r]) : wave_sum(sr[r]);
+        const int loc = r0 + r;
+        if (lane == 0 && b0 + r < B && finish(t) <= eps && ok(b0 + r))
+          atomicOr(&tbits[loc >> 5], 1u << (loc & 31));
+      }
+    }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    int c = 0;
+    if (lane < FR_WORDS) {
+      const uint64_t w = (uint64_t)tbits[2 * lane] | ((uint64_t)tbits[2 * lane + 1] << 32);
+      const int64_t word = tile0 / 64 + lane;
+      if (word * 64 < B) bits[word] = w;
+      c = __popcll(w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0) tile_cnt[blockIdx.x] = c;
+  }
+}
+
+// accept bits + tile counts -> exclusive tile offsets, *count, and the first
+// cap positions (the fused round's compaction)
+int compact_accept_bits(const uint64_t* bits, int64_t* tcnt, int64_t nt, int64_t* bsum,
+                        int64_t B, int64_t cap, int64_t* idx, int64_t* count, hipStream_t s) {
+  const int64_t nb = ceil_div(nt, SC_N);
+  hipLaunchKernelGGL(scan_partial, dim3((unsigned)nb), dim3(SC_T), 0, s, tcnt, nt, bsum);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(scan_top, dim3(1), dim3(SC_T), 0, s, bsum, nb, count);
+  ABC_LAUNCHED();
+  hipLaunchKernelGGL(scan_apply, dim3((unsigned)nb), dim3(SC_T), 0, s, tcnt, nt, bsum);
+  ABC_LAUNCHED();
+  if (cap > 0) {
+    const int64_t nwords = ceil_div(B, 64);
+    hipLaunchKernelGGL(bits_write_kernel, dim3((unsigned)ceil_div(nwords, 256)), dim3(256), 0,
+                       s, bits, nwords, tcnt, cap, idx);
+    ABC_LAUNCHED();
+  }
+  return ABC_OK;
+}
+
 // ---- ancestor table (abc_candidate.h) ---------------------------------------
 __global__ __launch_bounds__(256) void anc_records_kernel(const double* __restrict__ X,
                                                           const double* __restrict__ cdf,
@@ -631,20 +739,42 @@ extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0
                        rec_x);
   profile_stop(s, ABC_PROF_CANDIDATES);
   ABC_LAUNCHED();
-  const int64_t nb = ceil_div(nt, SC_N);
-  hipLaunchKernelGGL(scan_partial, dim3((unsigned)nb), dim3(SC_T), 0, s, tcnt, nt, bsum);
-  ABC_LAUNCHED();
-  hipLaunchKernelGGL(scan_top, dim3(1), dim3(SC_T), 0, s, bsum, nb, count);
-  ABC_LAUNCHED();
-  hipLaunchKernelGGL(scan_apply, dim3((unsigned)nb), dim3(SC_T), 0, s, tcnt, nt, bsum);
-  ABC_LAUNCHED();
-  if (cap > 0) {
-    const int64_t nwords = ceil_div(B, 64);
-    hipLaunchKernelGGL(bits_write_kernel, dim3((unsigned)ceil_div(nwords, 256)), dim3(256), 0,
-                       s, bits, nwords, tcnt, cap, idx);
-    ABC_LAUNCHED();
+  return compact_accept_bits(bits, tcnt, nt, bsum, B, cap, idx, count, s);
+}
+
+extern "C" int abc_pnorm_accept(const double* x, int64_t B, int S, const double* x0,
+                                const double* wf, double p, double eps,
+                                const int32_t* attempts, int max_attempts, int64_t cap,
+                                int64_t* idx, int64_t* count, void* ws, size_t ws_bytes,
+                                void* stream) {
+  ABC_CHECK_ARG(S >= 1 && B >= 0 && p >= 1.0 && cap >= 0, "pnorm_accept: bad S/B/p/cap");
+  ABC_CHECK_ARG(B < (1ll << 40), "pnorm_accept: B too large");
+  ABC_CHECK_ARG(count && (cap == 0 || idx), "pnorm_accept: null pointer");
+  if (ws_bytes < abc_candidates_workspace(B))
+    return set_error(ABC_ERR_WORKSPACE, "pnorm_accept: workspace too small");
+  hipStream_t s = as_stream(stream);
+  if (B == 0) {
+    ABC_HIP(hipMemsetAsync(count, 0, sizeof(int64_t), s));
+    return ABC_OK;
   }
-  return ABC_OK;
+  ABC_CHECK_ARG(x && x0 && wf, "pnorm_accept: null pointer");
+  const int64_t nt = ceil_div(B, FR_TILE);
+  ABC_CHECK_ARG(nt < (1ll << 31), "pnorm_accept: too many tiles");
+  Carver c(ws, ws_bytes);
+  uint64_t* bits = c.take<uint64_t>((size_t)nt * FR_WORDS);
+  int64_t* tcnt = c.take<int64_t>((size_t)nt);
+  c.take<double>(128);
+  int64_t* bsum = c.take<int64_t>((size_t)ceil_div(nt, SC_N));
+  if (!c.ok) return set_error(ABC_ERR_WORKSPACE, "pnorm_accept: workspace");
+  // the same row / wave split as abc_pnorm (the same bits per row)
+  if (S <= 32)
+    hipLaunchKernelGGL(pnorm_accept_kernel<false>, dim3((unsigned)nt), dim3(FR_T), 0, s, x, B,
+                       S, x0, wf, p, eps, attempts, max_attempts, bits, tcnt);
+  else
+    hipLaunchKernelGGL(pnorm_accept_kernel<true>, dim3((unsigned)nt), dim3(FR_T), 0, s, x, B,
+                       S, x0, wf, p, eps, attempts, max_attempts, bits, tcnt);
+  ABC_LAUNCHED();
+  return compact_accept_bits(bits, tcnt, nt, bsum, B, cap, idx, count, s);
 }
 
 extern "C" size_t abc_candidates_propose_workspace() { return 128 * sizeof(double) + 256; }

@@ -79,8 +79,25 @@ class PNormDistance(Distance):
     def device_call(self, xmat, x0vec, t, keys, out=None):
         """Distances of B simulations (device [B, S], columns in ``keys``
         order) to x_0 (device [S])."""
-        wf = gpu.as_dev(self.weight_vector(t, keys), device=xmat.device)
-        return gpu.pnorm(xmat, x0vec, wf, float(self.p), out=out)
+        return gpu.pnorm(xmat, x0vec, self._device_weights(t, keys, xmat.device),
+                         float(self.p), out=out)
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state["_dev_wf_cache"] = {}     # device tensors stay per process
+        return state
+
+    def _device_weights(self, t, keys, device):
+        """weight_vector(t, keys) on the device, uploaded only when it changed
+        (a pageable host-to-device copy synchronises the stream: once per
+        round of the staged sampler otherwise)."""
+        wv = np.ascontiguousarray(self.weight_vector(t, keys), dtype=np.float64)
+        key = (wv.tobytes(), str(device))
+        cache = self.__dict__.setdefault("_dev_wf_cache", {})
+        if key not in cache:
+            cache.clear()
+            cache[key] = gpu.as_dev(wv, device=device)
+        return cache[key]
 
     def fused_pnorm(self, t, keys, device):
         """(wf device [S], p) for the fused candidate kernel, or None when a
@@ -90,7 +107,7 @@ class PNormDistance(Distance):
                 cls.__call__ is not PNormDistance.__call__ or \
                 cls.weight_vector is not PNormDistance.weight_vector:
             return None
-        return gpu.as_dev(self.weight_vector(t, keys), device=device), float(self.p)
+        return self._device_weights(t, keys, device), float(self.p)
 
     # -- reference per-particle interface ----------------------------------
     def __call__(self, x: dict, x_0: dict, t: int = None, par: dict = None):

@@ -263,6 +263,25 @@ def pnorm(x, x0, wf, pval, out=None):
     return out
 
 
+def pnorm_accept(x, x0, wf, pval, eps, cap, att=None, max_attempts=0):
+    """Accept tail of one staged round (abc_pnorm_accept): the positions of
+    the first `cap` rows of x [B, S] whose p-norm distance to x0 is <= eps
+    (and whose proposal did not give up), and the number accepted [1] int64,
+    without a distance array.  x must be contiguous float64."""
+    B, S = x.shape
+    if x.dtype != F64 or not x.is_contiguous():
+        x = x.to(F64).contiguous()
+    cap = int(min(max(cap, 0), B))
+    idx = torch.empty(max(cap, 1), dtype=I64, device=x.device)
+    cnt = torch.empty(1, dtype=I64, device=x.device)
+    nb = nat.query("abc_candidates_workspace", int(B))
+    ws = workspace(nb, "candidates")
+    nat.call("abc_pnorm_accept", p(x), int(B), int(S), p(x0), p(wf), float(pval),
+             float(eps), p(att), int(max_attempts), cap, p(idx), p(cnt), p(ws),
+             ws.numel(), stream_ptr())
+    return idx, cnt
+
+
 def prior_uniforms(att, k, seed, generation, idx0, B=None):
     """Uniforms in (0, 1) of the candidates' prior streams for dimension k
     (abc_prior_uniforms): the source of an ABC_PRIOR_HOST coordinate's draw."""

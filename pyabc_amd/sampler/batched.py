@@ -145,7 +145,7 @@ class BatchedGPUSampler(Sampler):
         # sum stats, distance, ancestor, the user simulator's output): at
         # low acceptance rounds of 2^22 candidates meant hundreds of rounds
         # (one host read each) per generation
-        self.staged_round_bytes = 1 << 32
+        self.staged_round_bytes = 1 << 34
         self.seed = seed
         self.max_attempts = max_attempts
         # fused candidate rounds (abc_candidates_round): one kernel per round,
@@ -217,6 +217,13 @@ class BatchedGPUSampler(Sampler):
         acc_theta, acc_lp, acc_d, acc_x, acc_anc, acc_w = [], [], [], [], [], []
         rec_x = []
         stochastic = getattr(spec, "stochastic", None) is not None and not all_accepted
+        # the accept tail (abc_pnorm_accept): a p-norm distance and the
+        # uniform acceptor decided in one pass over the user simulator's
+        # rows, no distance array; the kept rows' distances afterwards
+        pnorm_tail = None
+        if not (stochastic or all_accepted or spec.distance is None) and \
+                hasattr(spec.distance, "fused_pnorm"):
+            pnorm_tail = spec.distance.fused_pnorm(spec.t, spec.sum_stat_keys, dev)
         # StochasticAcceptor + record_rejected: keep every evaluated
         # candidate's (theta, density, key, ancestor) for the temperature
         rec_extra = [] if (stochastic and record) else None
@@ -243,7 +250,20 @@ class BatchedGPUSampler(Sampler):
                 # the candidates' own prior-stream uniforms
                 host_prior_draw(theta, att, spec.host_prior, seed, gen, lo)
             x = spec.model.simulate_batch(theta, seed, gen, lo)
-            if all_accepted or spec.distance is None:
+            dist = None
+            if pnorm_tail is not None:
+                if x.dtype != gpu.F64 or not x.is_contiguous():
+                    x = x.to(gpu.F64).contiguous()
+                kk = min(n - n_acc, B)
+                idx, cnt = gpu.pnorm_accept(x, spec.x0vec, *pnorm_tail, spec.eps,
+                                            kk, att=att, max_attempts=self.max_attempts)
+                if ws == 1:
+                    both = gpu.torch.cat([cnt.view(1), idx[kk - 1:kk]]).cpu()
+                    cnt_local = int(both[0])
+                    pos_hint = int(both[1])
+                else:
+                    cnt_local = cnt
+            elif all_accepted or spec.distance is None:
                 dist = gpu.torch.full((B,), np.inf, dtype=gpu.F64, device=dev)
                 idx = gpu.torch.arange(B, dtype=gpu.I64, device=dev)
                 cnt_local = B
@@ -308,9 +328,16 @@ class BatchedGPUSampler(Sampler):
             rec_rows = int(rec_all[rank])
             if k_mine:
                 sel = idx[:k_mine]
-                cols = [theta, lp, dist, x] + ([anc] if anc is not None else []) \
-                    + ([accw] if stochastic else [])
-                got = gpu.gather_rows_batch(cols, sel)   # one launch
+                if dist is None:
+                    # the tail kept no distances: the kept rows' ones, the
+                    # same per-row arithmetic (abc_pnorm)
+                    cols = [theta, lp, x] + ([anc] if anc is not None else [])
+                    got = gpu.gather_rows_batch(cols, sel)
+                    got.insert(2, gpu.pnorm(got[2], spec.x0vec, *pnorm_tail))
+                else:
+                    cols = [theta, lp, dist, x] + ([anc] if anc is not None else []) \
+                        + ([accw] if stochastic else [])
+                    got = gpu.gather_rows_batch(cols, sel)   # one launch
                 acc_theta.append(got[0])
                 acc_lp.append(got[1])
                 acc_d.append(got[2])

@@ -76,17 +76,25 @@ class _Distance:
         return torch.from_numpy(oracle.pnorm(x.numpy(), x0.numpy()))
 
 
+class _TailDistance(_Distance):
+    """A p-norm distance with the fused form: the staged loop then decides
+    acceptance in the accept tail (gpu.pnorm_accept)."""
+
+    def fused_pnorm(self, t, keys, device):
+        return torch.ones(D, dtype=torch.float64), 2.0
+
+
 class _Spec:
     batched_capable = True
 
-    def __init__(self, eps):
+    def __init__(self, eps, tail=False):
         pop = _Population()
         self.t = GEN
         self.param_names = [f"p{k}" for k in range(D)]
         self.sum_stat_keys = [f"y{k}" for k in range(D)]
         self.transition = _Transition(pop)
         self.model = _Model()
-        self.distance = _Distance()
+        self.distance = _TailDistance() if tail else _Distance()
         self.x0vec = torch.ones(D, dtype=torch.float64)
         self.eps = eps
         self.weight_scale = 1.0
@@ -112,6 +120,18 @@ def _install_cpu_doubles(monkeypatch_like):
         w = torch.exp(lp - lt) * scale
         return w if acc_w is None else w * acc_w
 
+    def pnorm(x, x0, wf, pv):
+        return torch.from_numpy(oracle.pnorm(x.numpy(), x0.numpy()))
+
+    def pnorm_accept(x, x0, wf, pv, eps, cap, att=None, max_attempts=0):
+        acc = np.nonzero(oracle.pnorm(x.numpy(), x0.numpy()) <= eps)[0]
+        idx = torch.zeros(max(int(cap), 1), dtype=torch.int64)
+        k = min(int(cap), len(acc))
+        idx[:k] = torch.from_numpy(acc[:k])
+        return idx, torch.tensor([len(acc)])
+
+    monkeypatch_like(g, "pnorm", pnorm)
+    monkeypatch_like(g, "pnorm_accept", pnorm_accept)
     monkeypatch_like(g, "require_device", lambda: torch.device("cpu"))
     monkeypatch_like(g, "accept_compact", accept_compact)
     monkeypatch_like(g, "gather_rows", gather_rows)
@@ -159,12 +179,14 @@ class _FusedRound:
 
 
 def _run(n, eps, batch, record, fused=False):
+    """fused: False (staged distance + compaction), True (fused rounds) or
+    "tail" (staged rounds with the accept tail)."""
     from pyabc_amd.sampler import BatchedGPUSampler
-    s = BatchedGPUSampler(batch_size=batch, seed=SEED, fused=fused)
-    if fused:
+    s = BatchedGPUSampler(batch_size=batch, seed=SEED, fused=fused is True)
+    if fused is True:
         s._fused_round = lambda spec, seed, gen, dev: _FusedRound(spec)
     s.sample_factory.record_rejected = record
-    sample = s.sample_until_n_accepted(n, _Spec(eps))
+    sample = s.sample_until_n_accepted(n, _Spec(eps, tail=fused == "tail"))
     c = sample._cols
     rec = sample._recorded
     return dict(theta=c.theta.numpy(), w=c.weights.numpy(),
@@ -200,7 +222,7 @@ def _worker(rank, ws, port, out_dir, n, eps, batch, record, fused=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("fused", [False, True, "tail"])
 @pytest.mark.parametrize("n,batch,record,ws", [(300, 256, True, 2), (37, 64, False, 2),
                                                (1, 128, True, 2), (300, 128, True, 4),
                                                (5, 64, True, 4)])
@@ -214,7 +236,7 @@ def test_sharded_sampler_matches_single_rank(monkeypatch, n, batch, record, ws, 
     _install_cpu_doubles(monkeypatch.setattr)
     ref = _run(n, eps, batch * ws, record, fused)  # 1 rank, same global round size
     if fused:
-        staged = _run(n, eps, batch * ws, record, False)
+        staged = _run(n, eps, batch * ws, record, False)   # fused / tail == staged
         for k in ("theta", "w", "d", "x", "n_eval", "rec"):
             np.testing.assert_array_equal(ref[k], staged[k], err_msg=k)
     with tempfile.TemporaryDirectory() as tmp:

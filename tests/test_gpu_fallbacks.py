@@ -272,3 +272,40 @@ def test_sampler_reused_across_runs():
     for (df1, w1), (df2, w2) in zip(second, fresh):
         np.testing.assert_array_equal(df1[names].to_numpy(), df2[names].to_numpy())
         np.testing.assert_array_equal(w1, w2)
+
+
+def test_user_model_accept_tail_equals_staged():
+    """A user VectorizedModel's rounds decide acceptance in the accept tail
+    (abc_pnorm_accept); a PNormDistance subclass without the fused form
+    takes the staged distance + compaction instead.  Both runs give the same
+    populations, weights, epsilons and evaluation counts bit for bit."""
+    import pyabc_amd as pa
+    names, keys = [f"p{k}" for k in range(4)], [f"y{k}" for k in range(4)]
+
+    class Staged(pa.PNormDistance):
+        def weight_vector(self, t, k):          # same values, no fused form
+            return super().weight_vector(t, k)
+
+    def sim(theta, seed, gen, idx0):
+        g = torch.Generator(device=theta.device)
+        g.manual_seed((seed * 1000003 + gen * 7919 + idx0) % (2 ** 63))
+        return theta + 0.5 * torch.randn(theta.shape, generator=g, dtype=theta.dtype,
+                                          device=theta.device)
+
+    def run(dist):
+        prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
+        sampler = pa.BatchedGPUSampler(seed=17)
+        abc = pa.ABCSMC(pa.VectorizedModel(sim, keys), prior, dist, population_size=3000,
+                        sampler=sampler, eps=pa.QuantileEpsilon(alpha=0.5))
+        abc.new("sqlite://", {k: 0.7 for k in keys})
+        h = abc.run(max_nr_populations=5)
+        pops = h.get_all_populations()
+        return [h.get_distribution(0, t) for t in range(h.max_t + 1)], pops
+    a, pa_ = run(pa.PNormDistance(p=2))
+    b, pb_ = run(Staged(p=2))
+    assert len(a) == len(b) == 5
+    for (df1, w1), (df2, w2) in zip(a, b):
+        np.testing.assert_array_equal(df1[names].to_numpy(), df2[names].to_numpy())
+        np.testing.assert_array_equal(w1, w2)
+    np.testing.assert_array_equal(pa_["epsilon"].to_numpy(), pb_["epsilon"].to_numpy())
+    np.testing.assert_array_equal(pa_["samples"].to_numpy(), pb_["samples"].to_numpy())

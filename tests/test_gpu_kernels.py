@@ -551,6 +551,34 @@ def test_accept_compact(dev):
         np.testing.assert_array_equal(idx.cpu().numpy()[:n], ref)
 
 
+@pytest.mark.parametrize("S", [3, 10, 32, 33, 100])
+def test_pnorm_accept_tail(dev, S):
+    """abc_pnorm_accept (the user-simulator accept tail): the first cap
+    accepted positions and the count equal abc_pnorm + abc_mask_gave_up +
+    abc_accept_compact on the same rows, bit for bit, for p in {1, 2, 3,
+    inf}, ragged B, exact eps ties, gave-up proposals and cap < count."""
+    import torch
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(S)
+    for B in (1, 2047, 2049, 100_003):
+        x = T(rng.normal(size=(B, S)))
+        x0 = T(rng.normal(size=S))
+        wf = T(rng.uniform(0.2, 2.0, size=S))
+        att = torch.as_tensor(np.where(rng.uniform(size=B) < 0.05, 11, 1),
+                              dtype=torch.int32, device=x.device)
+        for pv in (1.0, 2.0, 3.0, np.inf):
+            d = gpu.pnorm(x, x0, wf, pv)
+            eps = float(d.cpu().numpy()[B // 2])          # an exact tie
+            gpu.mask_gave_up(d, att, 10)
+            ref_idx, ref_cnt = gpu.accept_compact(d, eps)
+            n = int(ref_cnt.cpu())
+            for cap in (B, max(n // 2, 1)):
+                idx, cnt = gpu.pnorm_accept(x, x0, wf, pv, eps, cap, att=att, max_attempts=10)
+                assert int(cnt.cpu()) == n
+                k = min(cap, n)
+                np.testing.assert_array_equal(idx.cpu().numpy()[:k], ref_idx.cpu().numpy()[:k])
+
+
 def test_step_golden(dev):
     """Fixed-input generation step (tests/golden/step.npz): distances,
     accept mask and importance weights against the reference."""

@@ -7,6 +7,8 @@ export TMPDIR=/tmp PYTHONPATH=$PWD
 O=gpurun_out/r04a
 W=/tmp/r04w
 mkdir -p $O $W
+timeout -k 5 60 ./tools/probes/mfma_mix > $O/mfma_mix.txt 2>&1 || { echo "mfma probe failed"; cat $O/mfma_mix.txt; exit 1; }
+cat $O/mfma_mix.txt
 timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
 ARGS="--steps 3 --warmup 1 --no-cpu-baseline"
