@@ -344,9 +344,12 @@ int abc_importance_weights(const double* prior_logpdf,
                            double* w, void* stream);
 
 /* ---- QuantileEpsilon (epsilon.py:202-228 -> weighted_statistics.py:27-43)
- * Stable LSD radix sort of fp64 keys carrying fp64 values, then
- * q = interp(alpha, cumsum(w) - w/2, sorted keys) with w normalised by its
- * sum.  Result written to *q (device double). */
+ * abc_weighted_quantile: q = interp(alpha, (cumsum(w) - w/2) / sum(w),
+ * points sorted ascending, ties by index), found by a weighted MSD select
+ * (fixed-point bin weights, a few hundred points sorted around the knots;
+ * abc_quantile.hip), written to *q (device double).  Weights >= 0.
+ * abc_sort_pairs_f64: stable LSD radix sort of fp64 keys carrying fp64
+ * values. */
 size_t abc_sort_pairs_workspace(int64_t N);
 int abc_sort_pairs_f64(const double* keys, const double* vals, int64_t N,
                        double* keys_out, double* vals_out, void* ws,

@@ -35,6 +35,12 @@ constexpr int DM_PB = DM_W * DM_G * 16;    // particles per block
 #endif
 constexpr int DM_SB = ABC_DM_SB;           // 32-row steps per LDS stage
 constexpr int DM_ROWF = 8;                 // floats per staged row: y^ (D <= 7), n^
+// rows image: per 32-row step 32 rows of DM_ROWF floats with 4 pad floats
+// after every 8 rows, so the 4 lane groups (rows 8 kq + u) read 4 different
+// bank quads of the staged copy (unpadded, the rows lay 64 words apart: one
+// bank quad, a 4-way conflict on every row read)
+constexpr int DM_RSTEP = 32 * DM_ROWF + 16;     // floats per 32-row step
+__host__ __device__ constexpr int dm_row_off(int r) { return r * DM_ROWF + (r >> 3) * 4; }
 
 __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(
@@ -50,6 +56,7 @@ __global__ __launch_bounds__(256) void knn_rows_kernel(const double* __restrict_
                                                        float* __restrict__ rows) {
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= nrows) return;
+  float* dst = rows + (j >> 5) * DM_RSTEP + dm_row_off((int)(j & 31));
   float f[DM_ROWF];
 #pragma unroll
   for (int k = 0; k < DM_ROWF; ++k) f[k] = 0.0f;
@@ -63,7 +70,7 @@ __global__ __launch_bounds__(256) void knn_rows_kernel(const double* __restrict_
     f[D] = INFINITY;
   }
 #pragma unroll
-  for (int k = 0; k < DM_ROWF; ++k) rows[j * DM_ROWF + k] = f[k];
+  for (int k = 0; k < DM_ROWF; ++k) dst[k] = f[k];
 }
 
 // DEFER (the deferred collect, see knn_select_kernel): sel_v / sel_jcut hold
@@ -96,10 +103,10 @@ void knn_dense_kernel(
   static_assert(D + 1 <= DM_ROWF, "staged row holds y^ and n^");
   constexpr int NT = mm_nt<D>(), NCP = 16 * NT;
   constexpr int BP = DM_SB * NT * 64;              // B pieces (16 B) per stage
-  constexpr int RP = DM_SB * 32 * DM_ROWF / 4;     // row pieces per stage
+  constexpr int RP = DM_SB * DM_RSTEP / 4;         // row pieces per stage
   constexpr int SP = BP + RP;
-  static_assert(BP % 64 == 0 && RP % 64 == 0, "whole wave-instructions per stream");
-  constexpr int PW = (SP / 64 + DM_W - 1) / DM_W;  // wave-instructions per wave per stage
+  static_assert(BP % 64 == 0 && DM_RSTEP % 4 == 0, "B stream: whole wave-instructions");
+  constexpr int PW = ((SP + 63) / 64 + DM_W - 1) / DM_W;  // wave-instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char stage[2][SP * 16];
   __shared__ int s_qn[DEFER ? DM_PB : 1], s_q[DEFER ? DM_PB * DQ_L : 1];
   if constexpr (DEFER) {
@@ -168,12 +175,12 @@ void knn_dense_kernel(
   // padded by DM_SB steps past nsteps, so a partial last stage loads safely)
   auto issue = [&](int buf, int64_t sb) {
     const char* bsrc = reinterpret_cast<const char*>(img + sb * NT * 64);
-    const char* rsrc = reinterpret_cast<const char*>(rows + sb * 32 * DM_ROWF);
+    const char* rsrc = reinterpret_cast<const char*>(rows + sb * DM_RSTEP);
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
       const int wi = wv * PW + i;              // wave-instruction index (uniform)
-      if (wi * 64 < SP) {
-        const int e = wi * 64 + lane;
+      const int e = wi * 64 + lane;
+      if (e < SP) {                            // the rows' last instruction is partial
         const char* src = e < BP ? bsrc + (size_t)e * 16 : rsrc + (size_t)(e - BP) * 16;
         glds16(src, &stage[buf][(size_t)wi * 64 * 16]);
       }
@@ -194,7 +201,7 @@ void knn_dense_kernel(
       // otherwise be loaded up front and cost the occupancy)
 #pragma unroll 2
       for (int u = 0; u < 8; ++u) {
-        const float* rf = rs + (k * 32 + 8 * kq + u) * DM_ROWF;
+        const float* rf = rs + k * DM_RSTEP + dm_row_off(8 * kq + u);
         const f32x4 r0 = *reinterpret_cast<const f32x4*>(rf);
         const f32x4 r1 = *reinterpret_cast<const f32x4*>(rf + 4);
         float y[8] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};

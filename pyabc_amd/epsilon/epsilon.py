@@ -1,7 +1,7 @@
 """Epsilon schedules (pyabc/epsilon/epsilon.py:12-243).
 
 QuantileEpsilon._update evaluates the weighted quantile on the GPU
-(abc_weighted_quantile: stable radix sort + scan + np.interp semantics).
+(abc_weighted_quantile: weighted MSD select + np.interp semantics).
 Weighted distances arrive either as the reference's DataFrame
 (columns ``distance``, ``w``) or as a ``WeightedDistances`` object carrying
 device tensors from the batched sampler (no host round trip).

@@ -374,6 +374,45 @@ def test_weighted_quantile_golden(dev):
                                           rel=1e-12), (name, a)
 
 
+@pytest.mark.parametrize("case", ["normal", "skewed_w", "heavy_ties", "one_value",
+                                  "two_spikes", "zero_w", "big", "discrete", "tiny"])
+def test_weighted_quantile_select(dev, case):
+    """The weighted MSD select (abc_quantile.hip) against the oracle's stable
+    sort + cumsum + interp (weighted_statistics.py:27-43): continuous data,
+    skewed weights, ties by the thousand (the final block's refinement), one
+    value for every point (the run summary), two spikes straddling the
+    quantile, zero weights, N = 2e6, integer-valued distances, N <= 3; alpha
+    at 0, 1, at a knot and between knots.  1e-12 relative."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(hash(case) % 2 ** 32)
+    N = {"big": 2_000_000, "tiny": 3}.get(case, 200_003)
+    pts = rng.gamma(2.0, 1.5, N)
+    w = rng.uniform(0.5, 1.5, N)
+    if case == "skewed_w":
+        w = np.exp(3.0 * rng.standard_normal(N))
+    elif case == "heavy_ties":
+        pts[rng.uniform(size=N) < 0.3] = 2.5
+    elif case == "one_value":
+        pts[:] = 1.25
+    elif case == "two_spikes":
+        pts = np.where(rng.uniform(size=N) < 0.5, 1.0, np.nextafter(1.0, 2.0))
+    elif case == "zero_w":
+        w[rng.uniform(size=N) < 0.4] = 0.0
+    elif case == "discrete":
+        pts = rng.integers(0, 40, N).astype(np.float64)
+    w = w / w.sum()
+    order = np.argsort(pts, kind="stable")
+    knot = float(((np.cumsum(w[order]) - 0.5 * w[order]))[N // 3])
+    for a in (0.0, 0.1, 0.5, knot, 0.9, 1.0):
+        q = float(gpu.weighted_quantile(T(pts), T(w), a).cpu())
+        ref = oracle.weighted_quantile(pts, w, a, kind="stable")
+        assert q == pytest.approx(ref, rel=1e-12, abs=1e-300), (case, a, q, ref)
+    # deterministic: the same bits twice
+    q1 = gpu.weighted_quantile(T(pts), T(w), 0.5).cpu().numpy()
+    q2 = gpu.weighted_quantile(T(pts), T(w), 0.5).cpu().numpy()
+    assert q1.tobytes() == q2.tobytes()
+
+
 def test_sort_pairs(dev):
     from pyabc_amd import gpu
     rng = np.random.default_rng(1)

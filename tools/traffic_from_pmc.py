@@ -3,9 +3,10 @@
     python tools/traffic_from_pmc.py <pmc_dir_root> <kernel-substring> \
         <population> <d> <out.json>
 
-The substring must select ONE instantiation (e.g. "mvn_x3_kernel<3, 8, false>",
-the main c3 launch; "mvn_x3_kernel<3, 8, true>" is the small unhinted rescue
-pass, ~1% of the bytes): dispatches are grouped by their full kernel name and
+The substring must select ONE instantiation (rocprofv3 reports this kernel
+by its mangled name: "mvn_x3_kernelILi3ELi8ELb0E" is the main c3 launch,
+"mvn_x3_kernelILi3ELi8ELb1E" the small unhinted rescue pass, ~1% of the
+bytes): dispatches are grouped by their full kernel name and
 the tool refuses a substring that matches more than one name, so launches of
 different shapes are never averaged together.  Only dispatches at least 10%
 of the largest matching one's FETCH_SIZE are kept (the same instantiation
