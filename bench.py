@@ -398,15 +398,18 @@ def main():
     avg_ms = k_ms / k_n if k_n else float("nan")
     achieved = k_flops / (k_ms * 1e-3) / 1e12 if k_n else float("nan")
     peak = F64_MFMA_PEAK_TFLOPS if args.precision == "f64" else F32_MFMA_PEAK_TFLOPS
-    kpad = {"x3": 32 * (math.ceil((args.dim + 7) / 32)
-                        + math.ceil((5 * args.dim + 4) / 32)),
+    # executed K per pair: the K80 layout (two 16x16x32 + one 16x16x16 f16
+    # MFMAs) for whitened rank <= 11, else 32-slot blocks
+    kpad = {"x3": (80 if args.dim <= 11 else
+                   32 * (math.ceil((args.dim + 7) / 32) + math.ceil((5 * args.dim + 4) / 32))),
             "f64": 4 * math.ceil((args.dim + 1) / 4),
             "f32": 4 * math.ceil((args.dim + 1) / 4)}[args.precision]
     executed = 2.0 * kpad * k_pairs / (k_ms * 1e-3) / 1e12 if k_n else float("nan")
     exec_peak = {"x3": F16_MFMA_PEAK_TFLOPS, "f64": F64_MFMA_PEAK_TFLOPS,
                  "f32": F32_MFMA_PEAK_TFLOPS}[args.precision]
-    kname = {"x3": "mvn_x3_kernel (f16 MFMA, 3-limb split operands, exact-grid "
-                   "f32 accumulation + exp2 + sum)",
+    kname = {"x3": ("mvn_x3k80_kernel (f16 MFMA, K = 80: 2 x 16x16x32 + 16x16x16; "
+                    if args.dim <= 11 else "mvn_x3_kernel (f16 MFMA, ")
+                   + "3-limb split operands, exact-grid f32 accumulation + exp2 + sum)",
              "f64": "mvn_lse_kernel<double> (f64 MFMA cross term + exp2 + LSE)",
              "f32": "mvn_lse_kernel<float> (f32 MFMA cross term + exp2 + LSE)"}
     traffic, traffic_src = measured_traffic(args, n_pop)
@@ -434,10 +437,9 @@ def main():
                       "transform); PMC in profiles/r03_fused_pmc_skewed_w.txt"),
             "candidates_per_generation": timed_cands}
     # unique bytes one launch must move: the population and candidate
-    # operand images (KB blocks of 32 f16 per row) + the fp64 result
-    kb = kpad // 32 if args.precision == "x3" else None
+    # operand images (kpad f16 per row) + the fp64 result
     avg_m = k_pairs / max(k_n, 1) / n_pop if k_n else 0
-    algo_bytes = ((n_pop + avg_m) * kb * 64 + avg_m * 8) if kb else None
+    algo_bytes = ((n_pop + avg_m) * kpad * 2 + avg_m * 8) if args.precision == "x3" else None
     out = None
     if ws > 1:
         # every rank is done with the GPU; rank 0 alone times the host leg

@@ -347,7 +347,10 @@ int abc_importance_weights(const double* prior_logpdf,
  * abc_weighted_quantile: q = interp(alpha, (cumsum(w) - w/2) / sum(w),
  * points sorted ascending, ties by index), found by a weighted MSD select
  * (fixed-point bin weights, a few hundred points sorted around the knots;
- * abc_quantile.hip), written to *q (device double).  Weights >= 0.
+ * abc_quantile.hip), written to *q (device double).  Weights >= 0.  When
+ * the knots lie in more than 2048 points of one 2^-24 slice of the key span
+ * (ties by the thousand) it writes NaN: the caller then runs
+ * abc_weighted_quantile_sorted (full stable radix sort, always decided).
  * abc_sort_pairs_f64: stable LSD radix sort of fp64 keys carrying fp64
  * values. */
 size_t abc_sort_pairs_workspace(int64_t N);
@@ -358,6 +361,10 @@ size_t abc_weighted_quantile_workspace(int64_t N);
 int abc_weighted_quantile(const double* points, const double* w, int64_t N,
                           double alpha, double* q, void* ws, size_t ws_bytes,
                           void* stream);
+size_t abc_weighted_quantile_sorted_workspace(int64_t N);
+int abc_weighted_quantile_sorted(const double* points, const double* w, int64_t N,
+                                 double alpha, double* q, void* ws, size_t ws_bytes,
+                                 void* stream);
 
 /* ---- AdaptivePNormDistance._update scales (distance.py:263-307,
  * scale.py:38-65) over recorded sum stats X [R x S] (row-major):

@@ -66,6 +66,8 @@ SIGNATURES = {
     "abc_sort_pairs_f64": (I32, [P, P, I64, P, P, P, SZ, P]),
     "abc_weighted_quantile_workspace": (SZ, [I64]),
     "abc_weighted_quantile": (I32, [P, P, I64, D, P, P, SZ, P]),
+    "abc_weighted_quantile_sorted_workspace": (SZ, [I64]),
+    "abc_weighted_quantile_sorted": (I32, [P, P, I64, D, P, P, SZ, P]),
     "abc_column_stats_workspace": (SZ, [I64, I32]),
     "abc_column_std": (I32, [P, I64, I32, P, P, SZ, P]),
     "abc_column_mad": (I32, [P, I64, I32, P, P, SZ, P]),

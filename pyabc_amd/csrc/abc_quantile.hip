@@ -30,10 +30,9 @@
 //      weights from the sum below, xp and np.interp's rules
 //      (quantile_pick semantics: clamps, exact knot hit, NaN fallbacks).
 // A segment that still holds more than WQ_CAP points after level 2 (ties by
-// the thousand within 2^-24 of the key span) is refined by the final block
-// itself over the whole input (slow, exact); a run of one key value is
-// summarised (its weight, its first / last member by index, its sorted
-// neighbours) instead of sorted.
+// the thousand at the knots, e.g. discrete distances) is not decided here:
+// *q = NaN, and the host (gpu.weighted_quantile's readers) reruns the exact
+// sort-based abc_weighted_quantile_sorted on the same inputs.
 #include "abc_common.h"
 
 namespace abc {
@@ -349,155 +348,40 @@ __device__ __forceinline__ bool kless(u64 ka, int ia, u64 kb, int ib) {
 }
 
 __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
-    const double* __restrict__ x, const double* __restrict__ w, int64_t N, double alpha,
-    const WqPart* __restrict__ part, int nblk, const WqDesc* __restrict__ desc,
+    int64_t N, double alpha, const WqDesc* __restrict__ desc,
     const u64* __restrict__ gkey, const int* __restrict__ gidx, const double* __restrict__ gw,
-    const unsigned int* __restrict__ list_n, const double* __restrict__ psum, int nsum,
-    double* __restrict__ q) {
-  // the slow path's histograms (refinement) and the list (sort, knots)
-  // share one LDS buffer: the list is filled after the last refinement
-  constexpr size_t HIST_B = (size_t)WQ_NB * (4 + 8 + 8 + 8);
-  constexpr size_t LIST_B = (size_t)WQ_CAP * (8 + 4 + 8 + sizeof(Knot));
-  __shared__ __attribute__((aligned(16))) char lds[HIST_B > LIST_B ? HIST_B : LIST_B];
-  u64* hw = reinterpret_cast<u64*>(lds);
-  u64* pw = hw + WQ_NB;
-  long long* pc = reinterpret_cast<long long*>(pw + WQ_NB);
-  unsigned int* hc = reinterpret_cast<unsigned int*>(pc + WQ_NB);
-  Knot* kn = reinterpret_cast<Knot*>(lds);
-  u64* skey = reinterpret_cast<u64*>(kn + WQ_CAP);
-  double* sw = reinterpret_cast<double*>(skey + WQ_CAP);
-  int* sidx = reinterpret_cast<int*>(sw + WQ_CAP);
+    const double* __restrict__ psum, int nsum, double* __restrict__ q) {
+  __shared__ u64 skey[WQ_CAP];
+  __shared__ int sidx[WQ_CAP];
+  __shared__ double sw[WQ_CAP];
+  __shared__ Knot kn[WQ_CAP];
   __shared__ double dsh[WQ_T / 64];
-  __shared__ u64 ush[WQ_T / 64];
-  __shared__ unsigned int s_n;
   const int t = threadIdx.x;
-  auto dadd = [](double a, double b) { return a + b; };
-  WqDesc D = *desc;
+  const WqDesc D = *desc;
+  if (!D.ok) {   // the knots sit in more than WQ_CAP points (ties): not decided
+    if (t == 0) *q = NAN;
+    return;
+  }
   double below = 0.0, total = 0.0;
   for (int b = 0; b < nsum; ++b) { below += psum[2 * b]; total += psum[2 * b + 1]; }
-  int m = 0;
-  if (D.ok) {
-    m = (int)D.count;
-    for (int i = t; i < m; i += WQ_T) { skey[i] = gkey[i]; sidx[i] = gidx[i]; sw[i] = gw[i]; }
-  } else {
-    // ---- slow path: refine over the whole input in this block until the
-    // segment fits or is a single key value
-    const Range R = wq_global_range(part, nblk, N);
-    const double tot_fx = __longlong_as_double(*(const long long*)(list_n + 2));
-    const double target = alpha * tot_fx;
-    const double margin = (double)N + ldexp(tot_fx, -48) + 4096.0;
-    for (int lev = 0; lev < 8 && !(D.count <= WQ_CAP) && D.lo < D.hi; ++lev) {
-      for (int b = t; b < WQ_NB; b += WQ_T) { hc[b] = 0u; hw[b] = 0ull; }
-      __syncthreads();
-      const int sh = span_shift(D.lo, D.hi);
-      for (int64_t i = t; i < N; i += WQ_T) {
-        const u64 k = qkey(x[i]);
-        if (k < D.lo || k > D.hi) continue;
-        const int bin = (int)((k - D.lo) >> sh);
-        atomicAdd(&hc[bin], 1u);
-        atomicAdd(&hw[bin], wfix(w[i], R.S));
-      }
-      __syncthreads();
-      Pick pk;
-      wq_pick_bins(hc, hw, pw, pc, D.base_w, target, margin, pk, ush);
-      WqDesc E;
-      seg_keys(D.lo, D.hi, sh, pk.b1, pk.b2, E.lo, E.hi);
-      E.base_w = pw[pk.b1];
-      E.below = D.below + pc[pk.b1];
-      long long c = 0;
-      for (int b = pk.b1; b <= pk.b2; ++b) c += hc[b];
-      E.count = c;
-      E.ok = c <= WQ_CAP;
-      E.done = 0;
-      __syncthreads();
-      D = E;
-    }
-    // fp64 sum below the final segment (fixed order)
-    double bl = 0.0;
-    for (int64_t i = t; i < N; i += WQ_T)
-      if (qkey(x[i]) < D.lo) bl += wval(w[i]);
-    below = block_reduce(bl, dsh, dadd);
-    if (D.count <= WQ_CAP) {
-      if (t == 0) s_n = 0u;
-      __syncthreads();
-      for (int64_t i = t; i < N; i += WQ_T) {
-        const u64 k = qkey(x[i]);
-        if (k >= D.lo && k <= D.hi) {
-          const unsigned int pos = atomicAdd(&s_n, 1u);
-          skey[pos] = k; sidx[pos] = (int)i; sw[pos] = wval(w[i]);
-        }
-      }
-      __syncthreads();
-      m = (int)s_n;
-    } else {
-      // one key value v = D.lo with more than WQ_CAP members: its weight, its
-      // first and last member by index, and its neighbours in sorted order
-      const u64 v = D.lo;
-      double wr = 0.0;
-      long long fi = LLONG_MAX, la = -1;
-      u64 pk_ = 0ull; long long pi = -1;   // previous: max (key, idx) below v
-      u64 nk = ~0ull; long long ni = LLONG_MAX;  // next: min (key, idx) above v
-      for (int64_t i = t; i < N; i += WQ_T) {
-        const u64 k = qkey(x[i]);
-        if (k == v) {
-          wr += wval(w[i]);
-          fi = i < fi ? i : fi;
-          la = i > la ? i : la;
-        } else if (k < v) {
-          if (pi < 0 || k > pk_ || (k == pk_ && i > pi)) { pk_ = k; pi = i; }
-        } else if (k < nk || (k == nk && i < ni)) { nk = k; ni = i; }
-      }
-      wr = block_reduce(wr, dsh, dadd);
-      __shared__ long long s_fi, s_la, s_pi, s_ni;
-      __shared__ u64 s_pk, s_nk;
-      if (t == 0) { s_fi = LLONG_MAX; s_la = -1; s_pi = -1; s_ni = LLONG_MAX; s_pk = 0ull; s_nk = ~0ull; }
-      __syncthreads();
-      atomicMin(&s_fi, fi);
-      atomicMax(&s_la, la);
-      __syncthreads();
-      // previous / next by a lexicographic (key, idx) reduction in two steps
-      if (pi >= 0) atomicMax(&s_pk, pk_);
-      if (ni < LLONG_MAX) atomicMin(&s_nk, nk);
-      __syncthreads();
-      if (pi >= 0 && pk_ == s_pk) atomicMax(&s_pi, pi);
-      if (ni < LLONG_MAX && nk == s_nk) atomicMin(&s_ni, ni);
-      __syncthreads();
-      if (t == 0) {
-        const double vv = qval(v);
-        const double wf = wval(w[s_fi]), wl = wval(w[s_la]);
-        Knot k4[4];
-        int c = 0;
-        const bool has_prev = s_pi >= 0, has_next = s_ni < LLONG_MAX;
-        if (has_prev) k4[c++] = Knot{(below - 0.5 * wval(w[s_pi])) / total, qval(s_pk)};
-        k4[c++] = Knot{(below + 0.5 * wf) / total, vv};
-        k4[c++] = Knot{(below + wr - 0.5 * wl) / total, vv};
-        if (has_next) k4[c++] = Knot{(below + wr + 0.5 * wval(w[s_ni])) / total, qval(s_nk)};
-        // neighbours are the true global first / last knots only when
-        // nothing lies beyond them: at_start / at_end as the run's position
-        const bool at_start = !has_prev || (D.below == 1);
-        const bool at_end = !has_next || (D.below + D.count + 1 == N);
-        bool ok;
-        double r = interp_rules(alpha, k4[0], k4[c - 1], at_start, at_end, k4, c, ok);
-        *q = ok ? r : NAN;
-      }
-      return;
-    }
-  }
-  __syncthreads();
-  // ---- sort (key, index) pairs with their weights: bitonic over M = next
-  // power of two >= m, padding (~0, INT_MAX)
+  const int m = (int)D.count;
   int M = 1;
   while (M < m) M <<= 1;
-  for (int i = m + t; i < M; i += WQ_T) { skey[i] = ~0ull; sidx[i] = 0x7FFFFFFF; sw[i] = 0.0; }
+  for (int i = t; i < M; i += WQ_T) {
+    const bool in = i < m;
+    skey[i] = in ? gkey[i] : ~0ull;
+    sidx[i] = in ? gidx[i] : 0x7FFFFFFF;
+    sw[i] = in ? gw[i] : 0.0;
+  }
   __syncthreads();
+  // bitonic sort by (key, index): the stable order of the reference's sort
   for (int size = 2; size <= M; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int i = t; i < M; i += WQ_T) {
         const int jx = i ^ stride;
         if (jx > i) {
           const bool asc = (i & size) == 0;
-          const bool gt = kless(skey[jx], sidx[jx], skey[i], sidx[i]);
-          if (gt == asc) {
+          if (kless(skey[jx], sidx[jx], skey[i], sidx[i]) == asc) {
             const u64 a = skey[i]; skey[i] = skey[jx]; skey[jx] = a;
             const int b = sidx[i]; sidx[i] = sidx[jx]; sidx[jx] = b;
             const double c = sw[i]; sw[i] = sw[jx]; sw[jx] = c;
@@ -507,25 +391,23 @@ __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
       __syncthreads();
     }
   }
-  // ---- cumulative weights: below + inclusive prefix (fixed-order block scan:
-  // each thread a run of consecutive elements, then the thread sums)
+  // cumulative weights: the fp64 sum below + an inclusive prefix in a fixed
+  // order (each thread a run of consecutive elements, then the thread sums)
   {
     const int per = (m + WQ_T - 1) / WQ_T;
     const int i0 = t * per;
-    double s = 0.0;
-    for (int k = 0; k < per && i0 + k < m; ++k) s += sw[i0 + k];
-    // exclusive scan of the thread sums (wave shuffles + LDS)
+    double sum = 0.0;
+    for (int k = 0; k < per && i0 + k < m; ++k) sum += sw[i0 + k];
     const int lane = t & 63, wv = t >> 6;
-    double inc = s;
+    double inc = sum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const double a = __shfl_up(inc, o, 64);
       if (lane >= o) inc += a;
     }
-    __syncthreads();
     if (lane == 63) dsh[wv] = inc;
     __syncthreads();
-    double run = below + (inc - s);
+    double run = below + (inc - sum);
     for (int i = 0; i < wv; ++i) run += dsh[i];
     for (int k = 0; k < per && i0 + k < m; ++k) {
       run += sw[i0 + k];
@@ -536,8 +418,7 @@ __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
   if (t == 0) {
     bool ok = m > 0;
     double r = NAN;
-    if (ok)
-      r = interp_rules(alpha, kn[0], kn[m - 1], D.below == 0, D.below + m == N, kn, m, ok);
+    if (ok) r = interp_rules(alpha, kn[0], kn[m - 1], D.below == 0, D.below + m == N, kn, m, ok);
     *q = ok ? r : NAN;
   }
 }
@@ -605,8 +486,8 @@ extern "C" int abc_weighted_quantile(const double* points, const double* w, int6
   hipLaunchKernelGGL(wq_gather_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk,
                      (const WqDesc*)(desc + 1), lkey, lidx, lw, list_n, psum);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_final_kernel, dim3(1), dim3(WQ_T), 0, s, points, w, N, alpha, part, nb,
-                     (const WqDesc*)(desc + 1), lkey, lidx, lw, list_n, psum, nb, q);
+  hipLaunchKernelGGL(wq_final_kernel, dim3(1), dim3(WQ_T), 0, s, N, alpha,
+                     (const WqDesc*)(desc + 1), lkey, lidx, lw, psum, nb, q);
   ABC_LAUNCHED();
   return ABC_OK;
 }

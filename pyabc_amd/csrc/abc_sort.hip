@@ -1,7 +1,9 @@
-// Stable segmented LSD radix sort of fp64 keys (abc_sort_pairs_f64);
-// AdaptivePNormDistance's per-column std (two-pass) here and its median
-// absolute deviation by radix select (abc_select.hip).  QuantileEpsilon's
-// weighted quantile is a weighted MSD select (abc_quantile.hip).
+// Stable segmented LSD radix sort of fp64 keys (abc_sort_pairs_f64) and the
+// sort-based weighted quantile (abc_weighted_quantile_sorted: the exact
+// fallback of the weighted MSD select of abc_quantile.hip, for inputs whose
+// knots sit in ties by the thousand); AdaptivePNormDistance's per-column std
+// (two-pass) here and its median absolute deviation by radix select
+// (abc_select.hip).
 //
 // Reference:
 //   weighted_quantile   pyabc/weighted_statistics.py:27-43 (argsort, cumsum,
@@ -301,6 +303,38 @@ __global__ void from_keys_kernel(const uint64_t* __restrict__ k, int64_t n,
   if (i < n) out[i] = key2f(k[i]);
 }
 
+// ---- weighted quantile ----------------------------------------------------
+// xp_k = (cs_k - w_k/2) / total; np.interp(alpha, xp, sorted points)
+// (numpy compiled_base.c arr_interp: j = #(xp <= x) - 1, edges clamp, exact
+// knot hit -> fp[j], NaN fallback from the right knot).
+__global__ void quantile_pick_kernel(const uint64_t* __restrict__ keys,
+                                     const double* __restrict__ w,
+                                     const double* __restrict__ cs, int64_t n,
+                                     double alpha, double* __restrict__ q) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const double total = cs[n - 1];
+  auto xp = [&](int64_t k) { return (cs[k] - 0.5 * w[k]) / total; };
+  auto fp = [&](int64_t k) { return key2f(keys[k]); };
+  if (alpha > xp(n - 1)) { *q = fp(n - 1); return; }
+  if (alpha < xp(0)) { *q = fp(0); return; }
+  int64_t lo = 0, hi = n;  // first index with xp > alpha
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (xp(mid) > alpha) hi = mid; else lo = mid + 1;
+  }
+  const int64_t j = lo - 1;
+  if (j == n - 1) { *q = fp(j); return; }
+  const double xj = xp(j), xj1 = xp(j + 1), yj = fp(j), yj1 = fp(j + 1);
+  if (xj == alpha) { *q = yj; return; }
+  const double slope = (yj1 - yj) / (xj1 - xj);
+  double r = slope * (alpha - xj) + yj;
+  if (isnan(r)) {
+    r = slope * (alpha - xj1) + yj1;
+    if (isnan(r) && yj == yj1) r = yj;
+  }
+  *q = r;
+}
+
 // ---- column std (np.std, two-pass) -------------------------------------------
 constexpr int CS_BLOCKS = 256;
 __global__ __launch_bounds__(256) void colsum_kernel(const double* __restrict__ X,
@@ -380,6 +414,40 @@ extern "C" int abc_sort_pairs_f64(const double* keys, const double* vals,
   hipLaunchKernelGGL(from_keys_kernel, dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s, b.k0, N, keys_out);
   ABC_LAUNCHED();
   ABC_HIP(hipMemcpyAsync(vals_out, b.v0, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
+  return ABC_OK;
+}
+
+extern "C" size_t abc_weighted_quantile_sorted_workspace(int64_t N) {
+  size_t off = sort_ws_bytes(1, N, true);
+  size_only<double>(off, (size_t)(N > 0 ? N : 1));  // cumsum
+  off += abc_scan_workspace(N) + 256;
+  return off + 256;
+}
+
+extern "C" int abc_weighted_quantile_sorted(const double* points, const double* w,
+                                     int64_t N, double alpha, double* q,
+                                     void* ws, size_t ws_bytes, void* stream) {
+  ABC_CHECK_ARG(N >= 1, "quantile: N < 1");
+  ABC_CHECK_ARG(points && w && q && ws, "quantile: null pointer");
+  if (ws_bytes < abc_weighted_quantile_sorted_workspace(N))
+    return set_error(ABC_ERR_WORKSPACE, "quantile: workspace too small");
+  hipStream_t s = as_stream(stream);
+  Carver cv(ws, ws_bytes);
+  SortBufs b;
+  if (!carve_sort(cv, 1, N, true, b)) return set_error(ABC_ERR_WORKSPACE, "quantile: carve");
+  double* cs = cv.take<double>((size_t)N);
+  size_t scan_bytes = abc_scan_workspace(N);
+  void* scan_ws = cv.take<char>(scan_bytes);
+  if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "quantile: carve");
+  hipLaunchKernelGGL(to_keys_kernel, dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s, points, N, b.k0);
+  ABC_LAUNCHED();
+  ABC_HIP(hipMemcpyAsync(b.v0, w, sizeof(double) * N, hipMemcpyDeviceToDevice, s));
+  int rc = run_sort(b, 1, N, s);
+  if (rc) return rc;
+  rc = abc_inclusive_scan_f64(b.v0, cs, N, scan_ws, scan_bytes, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(quantile_pick_kernel, dim3(1), dim3(64), 0, s, b.k0, b.v0, cs, N, alpha, q);
+  ABC_LAUNCHED();
   return ABC_OK;
 }
 

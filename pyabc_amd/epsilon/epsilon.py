@@ -109,18 +109,25 @@ class QuantileEpsilon(Epsilon):
         # the kernel normalises w by its sum (epsilon.py:215-219)
         q = gpu.weighted_quantile(d, w, self.alpha)
         # read back lazily: __call__(t) is the first consumer
-        self._look_up[t] = _PendingEps(gpu.HostFuture(q), self.quantile_multiplier)
+        self._look_up[t] = _PendingEps(gpu.HostFuture(q), self.quantile_multiplier,
+                                       (d, w, self.alpha))
 
 
 class _PendingEps:
-    """Quantile of the device kernel, resolved to a float on first use."""
+    """Quantile of the device kernel, resolved to a float on first use (an
+    undecided select reruns on the sort-based kernel, gpu.resolve_quantile)."""
 
-    def __init__(self, fut, multiplier):
+    def __init__(self, fut, multiplier, inputs=None):
         self._fut = fut
         self._mult = multiplier
+        self._inputs = inputs
 
     def value(self):
-        return float(self._fut.get()[0]) * self._mult
+        v = self._fut.get()[0]
+        if self._inputs is not None:
+            v = gpu.resolve_quantile(v, *self._inputs)
+            self._inputs = None
+        return float(v) * self._mult
 
     def __float__(self):
         return self.value()

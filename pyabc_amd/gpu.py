@@ -464,14 +464,27 @@ def sort_pairs(keys, vals):
     return ko, vo
 
 
-def weighted_quantile(points, w, alpha):
+def weighted_quantile(points, w, alpha, sorted_path=False):
+    """Weighted quantile on the device (weighted_statistics.py:27-43) -> q [1]
+    (device).  The weighted MSD select (abc_weighted_quantile) leaves NaN when
+    the knots sit in ties by the thousand; resolve_quantile reruns those on the
+    sort-based kernel (sorted_path=True)."""
     N = points.numel()
     q = torch.empty(1, dtype=F64, device=points.device)
-    nb = nat.query("abc_weighted_quantile_workspace", N)
+    name = "abc_weighted_quantile_sorted" if sorted_path else "abc_weighted_quantile"
+    nb = nat.query(name + "_workspace", N)
     ws = workspace(nb, "sort")
-    nat.call("abc_weighted_quantile", p(points), p(w), N, float(alpha), p(q),
-             p(ws), ws.numel(), stream_ptr())
+    nat.call(name, p(points), p(w), N, float(alpha), p(q), p(ws), ws.numel(), stream_ptr())
     return q
+
+
+def resolve_quantile(q_host, points, w, alpha):
+    """The host value of a weighted_quantile result: a NaN from the select
+    (undecided, not a NaN input) is recomputed on the sort-based path."""
+    v = float(q_host)
+    if v != v:
+        v = float(weighted_quantile(points, w, alpha, sorted_path=True).cpu()[0])
+    return v
 
 
 def column_std(X):
