@@ -1585,7 +1585,7 @@ int launch_pdf(const double* x, int64_t M, const double* X, const double* w,
 
 }  // namespace
 
-// 16 < d <= 64: runtime-d kernels (abc_local_wide.hip)
+// d > 16: runtime-d kernels (abc_local_wide.hip)
 size_t local_wide_fit_workspace(int64_t N, int d);
 int local_wide_fit(const double* X, const double* w, int64_t N, int d, int64_t nq,
                    double scaling, double eps, double* covs, double* invs, double* dets,
@@ -1639,7 +1639,7 @@ extern "C" int abc_local_fit(const double* X, const double* w, int64_t N,
                              double* covs, double* inv_covs, double* dets,
                              double* chol, double* log_norm, void* ws,
                              size_t ws_bytes, void* stream) {
-  ABC_CHECK_ARG(N >= 1 && d >= 1 && d <= 64 && k >= 1, "local_fit: bad N/d/k (d <= 64)");
+  ABC_CHECK_ARG(N >= 1 && d >= 1 && k >= 1, "local_fit: bad N/d/k");
   ABC_CHECK_ARG(N < (1ll << 31), "local_fit: N >= 2^31");
   ABC_CHECK_ARG(ws && ws_bytes >= abc_local_fit_workspace(N, d), "local_fit: workspace");
   ABC_CHECK_ARG(X && w && covs && inv_covs && dets && chol && log_norm, "local_fit: null pointer");
@@ -1672,7 +1672,7 @@ extern "C" int abc_local_logpdf(const double* x, int64_t M, const double* X,
                                 const double* inv_covs,
                                 const double* log_norm, double* out,
                                 void* ws, size_t ws_bytes, void* stream) {
-  ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= 64, "local_logpdf: bad M/N/d (d <= 64)");
+  ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1, "local_logpdf: bad M/N/d");
   if (M == 0) return ABC_OK;
   hipStream_t s = as_stream(stream);
   if (d > 16) {

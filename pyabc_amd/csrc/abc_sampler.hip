@@ -44,6 +44,60 @@ __global__ __launch_bounds__(256) void propose_kernel(
   if (att_out) att_out[b] = att;
 }
 
+// d > 64 (the register kernels hold theta in d registers): theta is
+// accumulated in its output row, the support box of the d coordinates sits in
+// dynamic LDS; the streams, the per-coordinate fma order and the re-draw loop
+// are propose_one's (abc_candidate.h), the ancestor the cdf search's.
+template <int MODE>
+__global__ __launch_bounds__(256) void propose_wide_kernel(
+    ProposalArgs A, int64_t idx0, int64_t B, double* __restrict__ theta,
+    double* __restrict__ lp_out, int64_t* __restrict__ anc_out,
+    int32_t* __restrict__ att_out) {
+  extern __shared__ double box[];   // [d][lo, hi]
+  const int d = A.d;
+  for (int k = threadIdx.x >> 6; k < d; k += blockDim.x >> 6)
+    support_bounds_wave(A.kind[k], A.params + 4 * k, box + 2 * k);
+  __syncthreads();
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t g = (uint64_t)(idx0 + b);
+  double* th = theta + b * d;
+  int64_t j = -1;
+  int used = A.max_attempts + 1;
+  const double total = MODE != PROP_PRIOR ? A.cdf[A.N - 1] : 0.0;
+  for (int att = 0; att < A.max_attempts; ++att) {
+    const uint32_t s0 = (uint32_t)att * SLOTS_PER_ATTEMPT;
+    if (MODE == PROP_PRIOR) {
+      for (int k = 0; k < d; ++k)
+        th[k] = prior_draw1(A.kind[k], A.params + 4 * k, g, s0 + SLOT_PRIOR + 512u * k, A.gen,
+                            A.seed);
+    } else {
+      u32x4 r = philox(g, s0 + SLOT_ANCESTOR, A.gen, A.seed);
+      const double target = uniform53(r.x, r.y) * total;
+      j = ancestor_search(A.cdf, A.guide, A.N, total, target);
+      const double* Lj = MODE == PROP_LOCAL ? A.L + j * d * d : A.L;
+      for (int k = 0; k < d; ++k) th[k] = 0.0;
+      for (int q = 0; q < d; q += 2) {
+        if ((q & 3) == 0) r = philox(g, s0 + SLOT_PERTURB + (uint32_t)(q >> 2), A.gen, A.seed);
+        double n0, n1;
+        box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1);
+        const bool two = q + 1 < d;
+        for (int k = q; k < d; ++k) {
+          th[k] = fma(Lj[k * d + q], n0, th[k]);
+          if (two && k >= q + 1) th[k] = fma(Lj[k * d + q + 1], n1, th[k]);
+        }
+      }
+      for (int k = 0; k < d; ++k) th[k] = A.X[j * d + k] + th[k];
+    }
+    bool ok = true;
+    for (int k = 0; k < d; ++k) ok = ok & (box[2 * k] <= th[k]) & (th[k] <= box[2 * k + 1]);
+    if (ok) { used = att + 1; break; }
+  }
+  lp_out[b] = used <= A.max_attempts ? prior_logpdf(A.kind, A.params, d, th) : -INFINITY;
+  if (anc_out) anc_out[b] = j;
+  if (att_out) att_out[b] = used;
+}
+
 template <bool PPL>
 void launch_propose(int d, dim3 grid, hipStream_t s, const double* X,
                     const double* cdf, const int32_t* guide, int64_t N, const double* L,
@@ -51,6 +105,16 @@ void launch_propose(int d, dim3 grid, hipStream_t s, const double* X,
                     uint32_t gen, int64_t idx0, int64_t B, int max_attempts,
                     double* theta, double* lp, int64_t* anc, int32_t* att) {
   const ProposalArgs A{X, cdf, guide, N, L, kind, params, d, max_attempts, seed, gen};
+  if (d > 64) {
+    const size_t lds = sizeof(double) * 2 * (size_t)d;
+    if (X == nullptr)
+      hipLaunchKernelGGL((propose_wide_kernel<PROP_PRIOR>), grid, dim3(256), lds, s, A, idx0, B,
+                         theta, lp, anc, att);
+    else
+      hipLaunchKernelGGL((propose_wide_kernel<PPL ? PROP_LOCAL : PROP_MVN>), grid, dim3(256),
+                         lds, s, A, idx0, B, theta, lp, anc, att);
+    return;
+  }
 #define ABC_PROPOSE_CASE(DD)                                                        \
   case DD:                                                                          \
     if (X == nullptr)                                                               \
@@ -272,7 +336,7 @@ extern "C" int abc_propose(const double* X, const double* cdf,
                            int max_attempts, double* theta,
                            double* prior_logpdf, int64_t* ancestor,
                            int32_t* attempts, void* stream) {
-  ABC_CHECK_ARG(d >= 1 && d <= 64 && B >= 0 && max_attempts >= 1, "propose: bad d/B");
+  ABC_CHECK_ARG(d >= 1 && d <= 4096 && B >= 0 && max_attempts >= 1, "propose: bad d/B");
   ABC_CHECK_ARG(max_attempts < (1 << 15), "propose: max_attempts too large");
   if (B == 0) return ABC_OK;
   ABC_CHECK_ARG(theta && prior_logpdf && prior_kind && prior_params, "propose: null pointer");
@@ -293,7 +357,7 @@ extern "C" int abc_local_propose(const double* X, const double* cdf,
                                  int max_attempts, double* theta,
                                  double* prior_logpdf, int64_t* ancestor,
                                  int32_t* attempts, void* stream) {
-  ABC_CHECK_ARG(d >= 1 && d <= 64 && B >= 0 && max_attempts >= 1, "local_propose: bad d/B");
+  ABC_CHECK_ARG(d >= 1 && d <= 4096 && B >= 0 && max_attempts >= 1, "local_propose: bad d/B");
   ABC_CHECK_ARG(max_attempts < (1 << 15), "local_propose: max_attempts too large");
   if (B == 0) return ABC_OK;
   ABC_CHECK_ARG(X && cdf && chol && N >= 1 && theta && prior_logpdf && prior_kind &&

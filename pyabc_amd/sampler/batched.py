@@ -127,6 +127,7 @@ class BatchedGPUSampler(Sampler):
     """
 
     FUSED_MAX_STATS = 256     # abc_candidates_round: S <= SIM_SMAX
+    FUSED_MAX_DIM = 64        # abc_candidates_round / _propose: d <= 64
 
     def __init__(self, batch_size=None, max_batch_size=None, seed=None,
                  max_attempts=10000, check_max_eval=False, fused=True,
@@ -438,7 +439,7 @@ class BatchedGPUSampler(Sampler):
         """gpu.CandidateRound of this generation, or None when some piece has
         no fused form (custom simulator / distance, stochastic acceptor)."""
         if not self.fused or getattr(spec, "stochastic", None) is not None \
-                or spec.distance is None:
+                or spec.distance is None or len(spec.param_names) > self.FUSED_MAX_DIM:
             return None
         if spec.transition is None and getattr(spec, "host_prior", None):
             return None     # t = 0 draws of host-leg coordinates: staged path
@@ -732,6 +733,8 @@ class BatchedGPUSampler(Sampler):
         as gpu.propose).  None when the transition has no proposal arrays."""
         # keyed on the spec object itself (held here, so its id cannot be
         # reused by a later run's spec while the entry lives)
+        if len(spec.param_names) > self.FUSED_MAX_DIM:
+            return None     # d > 64: the transition's own (wide) proposal kernel
         key = (seed, gen)
         if getattr(self, "_prop_spec", None) is spec and self._prop_key == key:
             return self._prop_round

@@ -9,8 +9,10 @@ Reference: pyabc/transition/local_transition.py:13-145.
   rvs      :141-145 j ~ Cat(w), theta ~ N(X_j, cov_j)
 Device kernels: abc_local_fit (exact radix-select k-NN + moments + small
 fp64 linear algebra), abc_local_logpdf, abc_local_propose.  d <= 16 on the
-templated kernels; 16 < d <= 64 on runtime-d kernels (abc_local_wide.hip,
-slower, same results); the reference has no cap, d > 64 raises.
+templated kernels; d > 16 on runtime-d kernels (abc_local_wide.hip, slower,
+same results; above d = 64 the per-particle matrices live in the workspace
+and proposals come from the wide propose kernel); no cap on d, as in the
+reference.
 """
 import numpy as np
 import pandas as pd
@@ -23,7 +25,6 @@ from .exceptions import NotEnoughParticles
 class LocalTransition(Transition):
     EPS = 1e-3
     MIN_K = 10
-    MAX_DIM = 64
 
     def __init__(self, k=None, k_fraction=1 / 4, scaling=1):
         if k_fraction is not None:
@@ -70,9 +71,6 @@ class LocalTransition(Transition):
 
     def _fit_device_arrays(self, Xd, wd):
         N, d = Xd.shape
-        if d > self.MAX_DIM:
-            raise NotImplementedError(
-                f"LocalTransition GPU kernels support d <= {self.MAX_DIM}, got {d}")
         covs, inv, dets, chol, lnorm = gpu.local_fit(Xd, wd, self.k,
                                                      self.scaling, self.EPS)
         self._dev_X, self._dev_w = Xd, wd

@@ -137,12 +137,14 @@ def test_plain_model_per_candidate_loop():
     assert not sample.ok and s2.nr_evaluations_ == 40
 
 
-@pytest.mark.parametrize("d,N,k", [(20, 1500, None), (17, 700, 40), (33, 400, None)])
+@pytest.mark.parametrize("d,N,k", [(20, 1500, None), (17, 700, 40), (33, 400, None),
+                                   (80, 400, None), (72, 300, 90)])
 def test_local_transition_wide_vs_oracle(d, N, k):
     """LocalTransition above d = 16 (the reference has no dimension cap,
     local_transition.py:77-96): the runtime-d fit, density and proposal
     against the oracle -- covariances, inverses, determinants and densities
-    to 1e-9 relative, proposals replayed to 1e-12."""
+    to 1e-9 relative, proposals replayed to 1e-12.  d = 72, 80: the BIG path
+    (per-particle matrices in the workspace, the wide propose kernel)."""
     import pyabc_amd as pa
     rng = np.random.default_rng(d + N)
     A = rng.normal(size=(d, d)) / np.sqrt(d)
@@ -309,3 +311,32 @@ def test_user_model_accept_tail_equals_staged():
         np.testing.assert_array_equal(w1, w2)
     np.testing.assert_array_equal(pa_["epsilon"].to_numpy(), pb_["epsilon"].to_numpy())
     np.testing.assert_array_equal(pa_["samples"].to_numpy(), pb_["samples"].to_numpy())
+
+
+def test_local_transition_d80_generations():
+    """ABCSMC with LocalTransition at d = 80 (> 64: staged rounds with the
+    wide propose kernel, the BIG fit and density): every generation's
+    weights equal the oracle's prior / LocalTransition density of the
+    previous population (1e-8 relative)."""
+    import pyabc_amd as pa
+    d = 80
+    names = [f"p{q:02d}" for q in range(d)]
+    keys = [f"y{q:02d}" for q in range(d)]
+    model = pa.LinearGaussianModel(names, keys, src=list(range(d)), sigma=[0.5] * d)
+    prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.PNormDistance(p=2), population_size=600,
+                    transitions=pa.LocalTransition(k=100, k_fraction=None),
+                    sampler=pa.BatchedGPUSampler(seed=13),
+                    eps=pa.QuantileEpsilon(alpha=0.5))
+    abc.new("sqlite://", {k: 0.3 for k in keys})
+    h = abc.run(max_nr_populations=3)
+    assert h.max_t == 2
+    for t in range(1, h.max_t + 1):
+        dfp, wp = h.get_distribution(0, t - 1)
+        df, w = h.get_distribution(0, t)
+        Xp, x = dfp[names].to_numpy(), df[names].to_numpy()
+        fit = oracle.local_fit(Xp, wp, k=100, k_fraction=None)
+        lw = stats.norm.logpdf(x).sum(1) - np.log(oracle.local_pdf(x, Xp, fit))
+        ref = np.exp(lw - lw.max())
+        ref /= ref.sum()
+        np.testing.assert_allclose(w, ref, rtol=1e-8, atol=0)
