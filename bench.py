@@ -312,10 +312,11 @@ def cpu_baseline(args, population, cov, budget_s, cores):
     return cand_rate, pdf_rate, n_c, n_p
 
 
-def measured_traffic(args, n_pop):
+def measured_traffic(args, n_pop, kernel):
     """HBM bytes per launch of the dominant kernel from the committed
     rocprofv3 --pmc passes (profiles/*_x3_traffic_*.json, written by
-    tools/traffic_from_pmc.py) when they were taken on this workload."""
+    tools/traffic_from_pmc.py) when they were taken on this workload and on
+    the kernel the library runs now (`kernel`: its mangled-name stem)."""
     import glob
     if args.precision != "x3":
         return None, None
@@ -326,7 +327,8 @@ def measured_traffic(args, n_pop):
             t = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if t.get("population") == n_pop and t.get("d") == args.dim:
+        if (t.get("population") == n_pop and t.get("d") == args.dim
+                and kernel + "I" in t.get("kernel_name", "")):
             return t["traffic_bytes"], os.path.relpath(f, ROOT)
     return None, None
 
@@ -398,21 +400,22 @@ def main():
     avg_ms = k_ms / k_n if k_n else float("nan")
     achieved = k_flops / (k_ms * 1e-3) / 1e12 if k_n else float("nan")
     peak = F64_MFMA_PEAK_TFLOPS if args.precision == "f64" else F32_MFMA_PEAK_TFLOPS
-    # executed K per pair: the K80 layout (two 16x16x32 + one 16x16x16 f16
-    # MFMAs) for whitened rank <= 11, else 32-slot blocks
-    kpad = {"x3": (80 if args.dim <= 11 else
-                   32 * (math.ceil((args.dim + 7) / 32) + math.ceil((5 * args.dim + 4) / 32))),
+    # executed K per pair and the kernel, as the library reports them
+    from pyabc_amd import gpu
+    x3_kernel, x3_k = gpu.mvn_x3_layout(args.dim) if args.precision == "x3" else (0, 0)
+    kpad = {"x3": x3_k,
             "f64": 4 * math.ceil((args.dim + 1) / 4),
             "f32": 4 * math.ceil((args.dim + 1) / 4)}[args.precision]
     executed = 2.0 * kpad * k_pairs / (k_ms * 1e-3) / 1e12 if k_n else float("nan")
     exec_peak = {"x3": F16_MFMA_PEAK_TFLOPS, "f64": F64_MFMA_PEAK_TFLOPS,
                  "f32": F32_MFMA_PEAK_TFLOPS}[args.precision]
     kname = {"x3": ("mvn_x3k80_kernel (f16 MFMA, K = 80: 2 x 16x16x32 + 16x16x16; "
-                    if args.dim <= 11 else "mvn_x3_kernel (f16 MFMA, ")
+                    if x3_kernel == 1 else f"mvn_x3_kernel (f16 MFMA, K = {x3_k}; ")
                    + "3-limb split operands, exact-grid f32 accumulation + exp2 + sum)",
              "f64": "mvn_lse_kernel<double> (f64 MFMA cross term + exp2 + LSE)",
              "f32": "mvn_lse_kernel<float> (f32 MFMA cross term + exp2 + LSE)"}
-    traffic, traffic_src = measured_traffic(args, n_pop)
+    traffic, traffic_src = measured_traffic(
+        args, n_pop, "mvn_x3k80_kernel" if x3_kernel == 1 else "mvn_x3_kernel")
     # per-stage split of the timed region (HIP events on the launch streams)
     c_ms, c_n = timer.channels["candidates"]
     r_ms, r_n = timer.channels["regen"]

@@ -29,10 +29,7 @@ constexpr int FR_T = 256;                // threads per block
 constexpr int FR_CPT = 8;                // candidates per thread and tile
 constexpr int FR_TILE = FR_T * FR_CPT;   // candidates per block
 constexpr int FR_WORDS = FR_TILE / 64;   // 64-bit accept words per tile
-#ifndef ABC_FR_CG
-#define ABC_FR_CG 2
-#endif
-constexpr int FR_CG = ABC_FR_CG;         // lazy early reject: candidates in flight per thread
+constexpr int FR_CG = 2;                 // lazy early reject: candidates in flight per thread
 
 struct RoundArgs {
   ProposalArgs P;

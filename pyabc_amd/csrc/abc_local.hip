@@ -734,18 +734,6 @@ inline int moments_chunks(int64_t N) {
 // local variance: a particle that fails it sends the whole fit back to the
 // VALU kernel (a device flag read by the host; never seen on the tests'
 // populations).
-#ifndef ABC_LOCAL_SELECT_FP64
-#define ABC_LOCAL_SELECT_FP64 0   // build-time A/B: 1 keeps the fp64 select kernel
-#endif
-#ifndef ABC_LOCAL_DENSE_OLD
-#define ABC_LOCAL_DENSE_OLD 0     // build-time A/B: 1 keeps mm_moments_kernel after the k-NN select
-#endif
-#ifndef ABC_KNN_NO_DEFER
-#define ABC_KNN_NO_DEFER 0        // build-time A/B: 1 keeps the select's own collect sweep at dense k
-#endif
-#ifndef ABC_LOCAL_MOMENTS_VALU
-#define ABC_LOCAL_MOMENTS_VALU 0   // build-time A/B: 1 keeps the VALU kernel for all k
-#endif
 constexpr int ML_NL = 5;
 template <int D> constexpr int mm_nc() { return local_nm<D>() * ML_NL; }
 template <int D> constexpr int mm_nt() { return (mm_nc<D>() + 15) / 16; }
@@ -1142,14 +1130,14 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   constexpr int NM = local_nm<D>();
   // k-NN selection on fp32 MFMA keys (abc_local_knn.h) for N >= KN_MIN_N;
   // small k sums the moments in the same kernel (list mode)
-  const bool knn = N >= KN_MIN_N && !(ABC_LOCAL_SELECT_FP64);
+  const bool knn = N >= KN_MIN_N;
   const bool list_ok = knn && kn_list_capable<D>() && nq + KN_MARGIN <= KN_CAP;
   // dense neighbourhoods (k > N / 16, d <= 5; above, the kernel's registers
   // spill): the moments on f16 MFMA
-  bool dense = D <= 5 && N >= 64 && nq * 16 > N && !(ABC_LOCAL_MOMENTS_VALU);
+  bool dense = D <= 5 && N >= 64 && nq * 16 > N;
   // dense k after the k-NN select's count sweep: the moments sweep does the
   // collect (deferred collect, abc_local_dense.h) -- one sweep less
-  const bool defer = knn && !list_ok && dense && !(ABC_LOCAL_DENSE_OLD) && !(ABC_KNN_NO_DEFER);
+  const bool defer = knn && !list_ok && dense;
   int* done = nullptr;
   double* lmom = nullptr;
   double* cen = nullptr;
@@ -1191,16 +1179,6 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
                          sel_v, sel_ties, sel_rank0, (const int*)need);
       ABC_LAUNCHED();
     }
-#ifdef ABC_KNN_TIMING
-    ABC_HIP(hipMemcpyAsync(covs, lmom, sizeof(double) * 8 * ceil_div(N, KN_PB), hipMemcpyDeviceToDevice, s));
-    return ABC_OK;
-#endif
-#ifdef ABC_KNN_DEBUG
-    ABC_HIP(hipMemcpyAsync(covs, lmom, sizeof(double) * 16 * N, hipMemcpyDeviceToDevice, s));
-    hipLaunchKernelGGL((knn_keys_debug_kernel<D>), dim3(1), dim3(64), 0, s, X, N,
-                       (const double*)cen, (const float*)img, inv);
-    return ABC_OK;
-#endif
     if (list_ok) {
       // one 8-byte read decides whether any particle still needs a sweep
       ABC_HIP(hipMemcpyAsync(h_cnt, cnt, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1241,7 +1219,7 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
     ABC_LAUNCHED();
     int h_flag = 0;
     bool finished = false;   // mm_finish ran already (deferred collect)
-    if (knn && !(ABC_LOCAL_DENSE_OLD)) {
+    if (knn) {
       // membership from the centred fp32 keys of the k-NN select
       const int64_t nrows = (nsteps + DM_SB) * 32;
       hipLaunchKernelGGL((knn_rows_kernel<D>), dim3((unsigned)ceil_div(nrows, 256)), dim3(256), 0,

@@ -17,23 +17,11 @@
 //  * both operand streams reach LDS by global_load_lds (16 B per lane, no
 //    staging registers), double-buffered per DM_SB 32-row steps, so the
 //    wave's registers go to its 2 x 7 accumulator tiles.
-#ifndef ABC_DM_W
-#define ABC_DM_W 4
-#endif
-#ifndef ABC_DM_WPE
-#define ABC_DM_WPE 0
-#endif
-constexpr int DM_W = ABC_DM_W;             // waves per block
-#ifndef ABC_DM_G
-#define ABC_DM_G 1
-#endif
-constexpr int DM_G = ABC_DM_G;             // particle tiles per wave
+constexpr int DM_W = 4;                    // waves per block
+constexpr int DM_G = 1;                    // particle tiles per wave
 constexpr int DM_T = DM_W * 64;
 constexpr int DM_PB = DM_W * DM_G * 16;    // particles per block
-#ifndef ABC_DM_SB
-#define ABC_DM_SB 2
-#endif
-constexpr int DM_SB = ABC_DM_SB;           // 32-row steps per LDS stage
+constexpr int DM_SB = 2;                   // 32-row steps per LDS stage
 constexpr int DM_ROWF = 8;                 // floats per staged row: y^ (D <= 7), n^
 // rows image: per 32-row step 32 rows of DM_ROWF floats with 4 pad floats
 // after every 8 rows, so the 4 lane groups (rows 8 kq + u) read 4 different
@@ -89,11 +77,7 @@ constexpr int DQ_L = 16;
 #define ABC_DEFER_V2 0
 #endif
 template <int D, bool DEFER>
-__global__ __launch_bounds__(DM_T)
-#if ABC_DM_WPE
-__attribute__((amdgpu_waves_per_eu(ABC_DM_WPE)))
-#endif
-void knn_dense_kernel(
+__global__ __launch_bounds__(DM_T) void knn_dense_kernel(
     const double* __restrict__ X, const double* __restrict__ cen,
     const double* __restrict__ R2p, const float* __restrict__ rows,
     const half8* __restrict__ img, int64_t N, int64_t nsteps,

@@ -199,20 +199,12 @@ __device__ __forceinline__ void kn_sweep(const float* __restrict__ img, int nt, 
   float ld[KN_PF][KB];
   knf4 cn[KN_PF];
   auto load = [&](int t0) {
-#if defined(ABC_KNN_EXP) && ABC_KNN_EXP == 3
-    // timing experiment: no loads (the MFMA operands stay in registers)
-#pragma unroll
-    for (int i = 0; i < KN_PF; ++i)
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) ld[i][kb] = bfr[kb] + (float)(t0 & 7);
-#else
 #pragma unroll
     for (int i = 0; i < KN_PF; ++i) {
       const float* src = img + (size_t)(t0 + 4 * i) * (KB * 64);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) ld[i][kb] = src[kb * 64 + lane];
     }
-#endif
   };
   // k-block-major order: the KN_PF tiles' MFMAs of one k-block are
   // independent and issue back to back; each accumulator's next k-block
@@ -272,13 +264,6 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
   const int64_t p0 = (int64_t)blockIdx.x * KN_PB;
   const int nt = (int)((N + 15) / 16);
   const KnBound Bd = kn_bound<D>(*R2p);
-#ifdef ABC_KNN_TIMING
-  long long ts[8];
-  ts[0] = clock64();
-#define KN_TS(i) ts[i] = clock64()
-#else
-#define KN_TS(i)
-#endif
 
   // ---- particle features (B operand) and the sample's fp32 coordinates
   float bfr[KB];
@@ -383,7 +368,6 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     s_sh[p] = sh;
     s_lo[p] = lo >> sh;
   }
-  KN_TS(1);
   __syncthreads();   // sample reads done; the LDS becomes the histogram
   for (int e = tid; e < KN_PB * KN_NB; e += 256) (&u.h.bins[0][0])[e] = 0u;
   const int sh = s_sh[pl];
@@ -397,19 +381,6 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
   // follows the active lanes).  Pad rows (key +inf) can only land in a bin
   // whose upper edge is +inf, and then T_hi = +inf.
   uint32_t* const hrow = &u.h.bins[pl][0];
-#if defined(ABC_KNN_EXP) && (ABC_KNN_EXP == 2 || ABC_KNN_EXP == 3)
-  kn_sweep<KB>(img, nt, wv, lane, bfr, [&](int, const knf4& c) {
-    below += __float_as_uint(c[0] + c[1] + c[2] + c[3]) >> 30;
-  });
-#elif defined(ABC_KNN_EXP) && ABC_KNN_EXP == 1
-  kn_sweep<KB>(img, nt, wv, lane, bfr, [&](int, const knf4& c) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t top = __float_as_uint(fmaxf(c[r], 0.0f)) >> sh;
-      below += top < lor ? 1u : 0u;
-    }
-  });
-#else
   kn_sweep<KB>(img, nt, wv, lane, bfr, [&](int, const knf4& c) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -419,13 +390,11 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
       if (off < (uint32_t)KN_NB) atomicAdd(hrow + off, 1u);
     }
   });
-#endif
   below += __shfl_xor(below, 16, 64);
   below += __shfl_xor(below, 32, 64);
   if (lane < 16) atomicAdd(&s_below[pl], below);
   __syncthreads();
 
-  KN_TS(2);
   // ---- the bin holding rank nq - 1: 16 lanes per particle
   {
     const int p = tid >> 4, l = tid & 15;
@@ -501,7 +470,6 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
   }
   __syncthreads();
 
-  KN_TS(3);
   // ---- 3. collect sweep
   {
     const float clo = s_clo[pl], chi = s_chi[pl];
@@ -563,7 +531,6 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     u.list.key[p][q] = kv;
   }
   __syncthreads();
-  KN_TS(4);
   // ---- 4. select rank nq - 1 in (key, index) order among the list: wave wv
   // takes particles wv, wv + 4, ...; lane holds entries lane + 64 i in
   // registers and counts the smaller (key, index) pairs against broadcast
@@ -608,29 +575,12 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
     const int p = tid;
     const long long rr = nq - 1 - (long long)s_below[p];
     const bool bad = s_fail[p] || rr < 0 || rr >= (long long)s_cnt[p];
-#ifdef ABC_KNN_DEBUG
-    {
-      double* dg = lmom + (int64_t)(p0 + p) * 16;
-      dg[0] = s_fail[p]; dg[1] = s_nest[p]; dg[2] = s_rank[p]; dg[3] = s_cnt[p];
-      dg[4] = s_below[p]; dg[5] = s_tlo[p]; dg[6] = s_thi[p]; dg[7] = s_chi[p];
-      dg[8] = s_clo[p]; dg[9] = *R2p; dg[10] = s_lo[p]; dg[11] = s_sh[p]; dg[12] = s_lm[p];
-      dg[13] = (double)rr; dg[14] = Bd(0.0); dg[15] = 0;
-    }
-#endif
     need[p0 + p] = bad ? 1 : 0;
     done[p0 + p] = (!bad && s_lm[p]) ? 1 : 0;
     if (bad) atomicAdd(&counts[0], 1);
     else if (s_lm[p]) atomicAdd(&counts[1], 1);
     s_fail[p] = bad ? 1 : 0;
   }
-  KN_TS(5);
-#ifdef ABC_KNN_TIMING
-  if (tid == 0) {
-    for (int i = 1; i <= 5; ++i) lmom[(int64_t)blockIdx.x * 8 + i] = (double)(ts[i] - ts[i - 1]);
-    lmom[(int64_t)blockIdx.x * 8] = 0;
-  }
-  return;
-#endif
   if constexpr (kn_list_capable<D>()) {
     if (!listm) return;
     __syncthreads();
@@ -676,66 +626,9 @@ __global__ __launch_bounds__(256) void knn_select_kernel(
 #pragma unroll
       for (int t = 0; t < NM; ++t) {
         const double v = wave_sum(m[t]);
-#ifndef ABC_KNN_DEBUG
         if (lane == 0) lmom[(int64_t)t * N + n] = v;
-#endif
       }
     }
   }
 }
 
-#ifdef ABC_KNN_DEBUG
-// keys of particles 0..15 against every row, as the sweeps compute them:
-// out[0][p][j] from the count sweep's two-tile path, out[1][p][j] from the
-// collect sweep's one-tile path
-template <int D>
-__global__ __launch_bounds__(64) void knn_keys_debug_kernel(const double* __restrict__ X, int64_t N,
-                                                            const double* __restrict__ cen,
-                                                            const float* __restrict__ img,
-                                                            double* __restrict__ out) {
-  constexpr int KB = kn_kb<D>();
-  const int lane = threadIdx.x, pl = lane & 15;
-  const int64_t nt = (N + 15) / 16;
-  float bfr[KB];
-  {
-    float y[D];
-    const float nn = kn_feat<D>(X, pl, cen, y);
-    for (int kb = 0; kb < KB; ++kb) {
-      const int k = 4 * kb + (lane >> 4);
-      float v = 0.0f;
-      for (int q = 0; q < D; ++q) if (k == q) v = -2.0f * y[q];
-      if (k == D) v = 1.0f;
-      if (k == D + 1) v = nn;
-      bfr[kb] = v;
-    }
-  }
-  for (int64_t t = 0; t + 4 < nt; t += 8) {
-    float a0[KB], a1[KB];
-    for (int kb = 0; kb < KB; ++kb) {
-      a0[kb] = img[(t * KB + kb) * 64 + lane];
-      a1[kb] = img[((t + 4) * KB + kb) * 64 + lane];
-    }
-    knf4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-    for (int kb = 0; kb < KB; ++kb) {
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[kb], bfr[kb], c0, 0, 0, 0);
-      c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[kb], bfr[kb], c1, 0, 0, 0);
-    }
-    for (int r = 0; r < 4; ++r) {
-      const int64_t j0 = 16 * t + 4 * (lane >> 4) + r, j1 = j0 + 64;
-      if (j0 < N && pl < 8) out[pl * N + j0] = c0[r];
-      if (j1 < N && pl < 8) out[pl * N + j1] = c1[r];
-    }
-  }
-  for (int64_t t = 0; t < nt; ++t) {
-    float a0[KB];
-    for (int kb = 0; kb < KB; ++kb) a0[kb] = img[(t * KB + kb) * 64 + lane];
-    knf4 c0 = {0.f, 0.f, 0.f, 0.f};
-    for (int kb = 0; kb < KB; ++kb)
-      c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[kb], bfr[kb], c0, 0, 0, 0);
-    for (int r = 0; r < 4; ++r) {
-      const int64_t j = 16 * t + 4 * (lane >> 4) + r;
-      if (j < N && pl < 8) out[8 * N + pl * N + j] = c0[r];
-    }
-  }
-}
-#endif

@@ -313,7 +313,10 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
 // Image per 16-row tile: frags32 [2][64 lanes][8 halves] | frags16 [64][4].
 constexpr int K80_RMAX = 11;
 constexpr int K80_TILE_H = 2 * 64 * 8 + 64 * 4;   // halves per tile (2560 B)
-__host__ __device__ constexpr bool x3_k80(int r) { return r <= K80_RMAX; }
+// (off while the c = 0 tiles' wrong sums under -amdgpu-mfma-vgpr-form are
+// diagnosed: tools/probes/x3_k80_debug.py, tools/probes/mfma_srcc_hazard.hip)
+constexpr bool K80_ON = false;
+__host__ __device__ constexpr bool x3_k80(int r) { return K80_ON && r <= K80_RMAX; }
 __host__ __device__ constexpr int x3_tile_halves(int r) {
   return x3_k80(r) ? K80_TILE_H : (x3_kb0(r) + x3_kb12(r)) * 64 * 8;
 }
@@ -705,6 +708,12 @@ __global__ __launch_bounds__(256) void mvn_x3k80_kernel(
     f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b0[c], f32x4{0.f, 0.f, 0.f, 0.f},
                                                      0, 0, 0);
     r = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b1[c], r, 0, 0, 0);
+    // A 16x16x16 MFMA that takes the accumulator of the 16x16x32 MFMA just
+    // before it as SrcC reads a stale value unless >= 2 wait states separate
+    // them, and the compiler inserts none for this mixed-shape pair
+    // (tools/probes/mfma_srcc_hazard.hip: wrong at 0-1, exact at >= 2 on
+    // gfx950).  The s_nop is tied to r so it sits between the two; 3 here.
+    asm volatile("s_nop 2" : "+v"(r));
     return __builtin_amdgcn_mfma_f32_16x16x16f16(a2, b2[c], r, 0, 0, 0);
   };
   auto expsum = [&](const f32x4& v) {
@@ -1051,6 +1060,11 @@ size_t x3_packed_bytes(int64_t N, int r) {
 }
 
 int x3_max_rank() { return MAX_R; }
+
+extern "C" int abc_mvn_x3_layout(int r, int* kslots) {
+  if (kslots) *kslots = x3_k80(r) ? 80 : 32 * (x3_kb0(r) + x3_kb12(r));
+  return x3_k80(r) ? 1 : 0;
+}
 
 int x3_pack_population(const double* X, const double* w, int64_t N, int d,
                        const double* mu, const double* U, int r,

@@ -164,13 +164,7 @@ __global__ __launch_bounds__(SEL_T) void col_sample_kernel(
 // (heavy ties: a constant column is all window) sends the rest straight to
 // scratch, one returning global atomic per key.  The order of the compacted
 // keys is not deterministic; the selection does not depend on it.
-#ifndef ABC_BK_U
-#define ABC_BK_U 8
-#endif
-#ifndef ABC_BK_ROWS
-#define ABC_BK_ROWS 96
-#endif
-constexpr int BK_T = 256, BK_U = ABC_BK_U, BK_ROWS = ABC_BK_ROWS, BK_CAP = 4096;
+constexpr int BK_T = 256, BK_U = 8, BK_ROWS = 96, BK_CAP = 4096;
 template <bool DEV>
 __global__ __launch_bounds__(BK_T) void col_bracket_kernel(
     const double* __restrict__ X, int64_t R, int S, const double* __restrict__ med,

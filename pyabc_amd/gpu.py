@@ -183,6 +183,15 @@ def mvn_logpdf(x, packed, N, mu, U, prec, log_const, out=None, X=None, w=None,
     return out
 
 
+def mvn_x3_layout(r):
+    """(kernel, K slots per pair) the x3 density runs at whitened rank r:
+    kernel 1 = mvn_x3k80_kernel (K = 80), 0 = mvn_x3_kernel (K = 32 x blocks)."""
+    import ctypes
+    k = ctypes.c_int(0)
+    kernel = int(nat.load().abc_mvn_x3_layout(int(r), ctypes.byref(k)))
+    return kernel, int(k.value)
+
+
 def mvn_logpdf_direct(x, X, w, U, V, support_tol, log_const, out=None):
     M, d = x.shape
     N = X.shape[0]

@@ -134,6 +134,32 @@ def test_mvn_x3_rescue_and_edges(dev):
                                    rtol=1e-9)
 
 
+@pytest.mark.parametrize("d", [1, 7, 11, 12, 16, 25])
+def test_mvn_x3_layouts_vs_oracle(dev, d):
+    """Both x3 operand layouts against the fp64 oracle: the K80 layout (two
+    16x16x32 + one 16x16x16 f16 MFMAs, whitened rank <= 11) and the 32-slot
+    block layout above it (d = 12, 16, 25 = the largest x3 rank); unhinted
+    (max pre-pass) and hinted by the proposals' ancestors; 1e-6 / 2e-6."""
+    import pandas as pd
+    from pyabc_amd.transition import MultivariateNormalTransition
+    rng = np.random.default_rng(100 + d)
+    N = 5000
+    X = 0.5 + 0.7 * rng.standard_normal((N, d))
+    w = np.exp(0.7 * rng.standard_normal(N))
+    w /= w.sum()
+    cols = [f"p{k:02d}" for k in range(d)]
+    t = MultivariateNormalTransition()
+    t.fit(pd.DataFrame(X, columns=cols), w.copy())
+    assert t._prec == 2
+    th, _, anc, _ = t.propose_device(1500)
+    x = th.cpu().numpy()
+    ref = oracle.mvn_logpdf(x, X, w, t.cov)
+    lp = t.logpdf_device(th).cpu().numpy()
+    np.testing.assert_allclose(np.exp(lp - ref), 1.0, rtol=1e-6)
+    lph = t.logpdf_device(th, hint=anc).cpu().numpy()
+    np.testing.assert_allclose(np.exp(lph - ref), 1.0, rtol=2e-6)
+
+
 def test_mvn_x3_hinted_offsets(dev):
     """x3 with per-candidate offsets from a hint row (the sampler passes the
     proposal's ancestor) instead of the max pre-pass: ancestors, random rows,

@@ -29,6 +29,10 @@ def main():
                     help="lognormal importance weights, ESS/N = exp(-wsigma^2) "
                          "(c3's last generations: ~1e-2)")
     ap.add_argument("--staged", action="store_true")
+    ap.add_argument("--sort-weights", action="store_true",
+                    help="population rows in descending weight order (probe of a "
+                         "weight-sorted ancestor table: the heavy rows' records "
+                         "and guide bins contiguous)")
     ap.add_argument("--modes", nargs="+", default=["plain", "filter"],
                     choices=["plain", "filter"])
     a = ap.parse_args()
@@ -41,6 +45,9 @@ def main():
     X = (0.8 + np.sqrt(0.2) * torch.randn(N, d, generator=g, dtype=torch.float64)).to(dev)
     w = torch.exp(a.wsigma * torch.randn(N, generator=g, dtype=torch.float64)).to(dev)
     w /= w.sum()
+    if a.sort_weights:
+        order = torch.argsort(w, descending=True, stable=True)
+        X, w = X[order].contiguous(), w[order].contiguous()
     bw = (4 / (2e4 * (d + 2))) ** (1 / (d + 4))
     L = torch.eye(d, dtype=torch.float64, device=dev) * (bw * np.sqrt(0.2))
     cdf = gpu.inclusive_scan(w)

@@ -13,7 +13,8 @@ for f in $(git ls-tree --name-only $REV pyabc_amd/csrc/) $(git ls-tree --name-on
   git show $REV:$f > $T/$f
 done
 OBJS=$(ls pyabc_amd/_build/*.o | grep -v "/$SRC.o")
-/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -I include -Wno-unused-result \
+EXTRA=$(python3 -c "import pyabc_amd.build as b; print(' '.join(b.EXTRA.get('$SRC', [])))")
+/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -I include -Wno-unused-result $EXTRA \
   -c $T/pyabc_amd/csrc/$SRC -o "$OUT.$SRC.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT" $OBJS "$OUT.$SRC.o"
 rm -rf "$OUT.$SRC.o" $T

@@ -4,7 +4,7 @@ out=$1; to=$2; shift 2
 for i in $(seq 1 40); do
   /usr/local/graft/bin/gpurun --timeout $to -- "$@" > $out 2>&1
   rc=$?
-  if grep -q "status=transient" $out && grep -q "nothing was charged" $out; then
+  if [ $rc -eq 3 ] || { grep -q "status=transient" $out && grep -q "nothing was charged" $out; }; then
     echo "[gpuq] slot busy, retry $i" >> $out.retries; sleep 150; continue
   fi
   break

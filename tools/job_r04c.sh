@@ -9,16 +9,20 @@ export TMPDIR=/tmp PYTHONPATH=$PWD
 O=gpurun_out/r04c
 W=/tmp/r04cw
 mkdir -p $O $W
+# PART=tests: parity + x3 A/B; PART=rest: everything after (two gpurun calls)
+if [ "${PART:-tests}" = tests ]; then
 timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-  tests/test_gpu_kernels.py tests/test_gpu_rows.py tests/test_gpu_fused.py \
+  tests/test_gpu_kernels.py tests/test_gpu_rows.py tests/test_gpu_fused.py tests/test_gpu_fallbacks.py \
   tests/test_gpu_e2e.py::test_large_n_parity_vs_reference > $O/tests.log 2>&1 || { echo "tests failed"; tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 STEPS=8 bash tools/ab_x3.sh > $O/ab_x3.log 2>&1 || { echo "x3 ab failed"; tail -20 $O/ab_x3.log; tail -20 gpurun_out/ab_x3.log; exit 1; }
 cat $O/ab_x3.log
+exit 0
+fi
 ABCGPU_LIB=ab/libdeferv2.so timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
   tests/test_gpu_kernels.py -k "local" tests/test_gpu_rows.py::test_c5_local_fit_default_k > $O/defer_v2_tests.log 2>&1 \
   && echo "v2 tests ok" || { echo "v2 tests failed"; tail -15 $O/defer_v2_tests.log; }
-bash tools/ab_local_fit.sh ab/libbase_local.so ab/libdeferv2.so > $O/ab_local_fit.log 2>&1 || { echo "ab failed"; cat $O/ab_local_fit.log; exit 1; }
+bash tools/ab_local_fit.sh ab/libbase_local.so ab/libdeferv2.so ab/libdm_w8.so ab/libdm_sb1.so > $O/ab_local_fit.log 2>&1 || { echo "ab failed"; cat $O/ab_local_fit.log; exit 1; }
 cat $O/ab_local_fit.log
 K=/tmp/knnpmc
 args="tools/probes/c5_fit_probe.py quarter"
@@ -39,3 +43,9 @@ cat $O/traffic.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $W/cm -o run -- python3 -u tools/probes/custom_model_c2.py 20 > $O/custom20.log 2>&1 || { echo "custom probe failed"; tail -5 $O/custom20.log; exit 1; }
 find $W/cm -name "*kernel_stats.csv" -exec cp {} $O/custom_model_kernel_stats.csv \;
 grep model $O/custom20.log | cut -c1-700
+for ws in 0 2.2; do
+  for so in "" "--sort-weights"; do
+    timeout -k 10 120 python3 -u tools/bench_fused.py --wsigma $ws --rates 1e-4 --B 134217728 --reps 2 --modes plain $so > $O/fused_w${ws}${so}.log 2>&1 || { echo "bench_fused failed"; tail -5 $O/fused_w${ws}${so}.log; exit 1; }
+    echo "wsigma $ws $so: $(grep candidates $O/fused_w${ws}${so}.log)"
+  done
+done
