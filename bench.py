@@ -402,20 +402,18 @@ def main():
     peak = F64_MFMA_PEAK_TFLOPS if args.precision == "f64" else F32_MFMA_PEAK_TFLOPS
     # executed K per pair and the kernel, as the library reports them
     from pyabc_amd import gpu
-    x3_kernel, x3_k = gpu.mvn_x3_layout(args.dim) if args.precision == "x3" else (0, 0)
+    _, x3_k = gpu.mvn_x3_layout(args.dim) if args.precision == "x3" else (0, 0)
     kpad = {"x3": x3_k,
             "f64": 4 * math.ceil((args.dim + 1) / 4),
             "f32": 4 * math.ceil((args.dim + 1) / 4)}[args.precision]
     executed = 2.0 * kpad * k_pairs / (k_ms * 1e-3) / 1e12 if k_n else float("nan")
     exec_peak = {"x3": F16_MFMA_PEAK_TFLOPS, "f64": F64_MFMA_PEAK_TFLOPS,
                  "f32": F32_MFMA_PEAK_TFLOPS}[args.precision]
-    kname = {"x3": ("mvn_x3k80_kernel (f16 MFMA, K = 80: 2 x 16x16x32 + 16x16x16; "
-                    if x3_kernel == 1 else f"mvn_x3_kernel (f16 MFMA, K = {x3_k}; ")
-                   + "3-limb split operands, exact-grid f32 accumulation + exp2 + sum)",
+    kname = {"x3": (f"mvn_x3_kernel (f16 MFMA, K = {x3_k} per pair; 3-limb split "
+                    "operands, exact-grid f32 accumulation + exp2 + sum)"),
              "f64": "mvn_lse_kernel<double> (f64 MFMA cross term + exp2 + LSE)",
              "f32": "mvn_lse_kernel<float> (f32 MFMA cross term + exp2 + LSE)"}
-    traffic, traffic_src = measured_traffic(
-        args, n_pop, "mvn_x3k80_kernel" if x3_kernel == 1 else "mvn_x3_kernel")
+    traffic, traffic_src = measured_traffic(args, n_pop, "mvn_x3_kernel")
     # per-stage split of the timed region (HIP events on the launch streams)
     c_ms, c_n = timer.channels["candidates"]
     r_ms, r_n = timer.channels["regen"]

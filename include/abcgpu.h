@@ -138,7 +138,7 @@ int abc_mvn_pack_population(const double* X, const double* w, int64_t N, int d,
 size_t abc_mvn_logpdf_workspace(int64_t M, int64_t N, int r, int prec);
 /* K slots the X3 kernel executes per (candidate, population row) pair at
  * whitened rank r (the f16 MFMA work per pair is 2 K FLOP), and the kernel it
- * runs: 0 = mvn_x3_kernel (K = 32 x blocks), 1 = mvn_x3k80_kernel (K = 80).
+ * runs (0 = mvn_x3_kernel, K = 32 x MFMA blocks).
  * A layout query for reporting; no device work. */
 int abc_mvn_x3_layout(int r, int* kslots);
 int abc_mvn_logpdf(const double* x, int64_t M, int d, const void* packed,

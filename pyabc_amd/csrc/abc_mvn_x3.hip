@@ -298,175 +298,6 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
   }
 }
 
-// ---- K80 layout (r <= 11): K = 80 = two 16x16x32 blocks + one 16x16x16 ----
-// The scalars c and m need only two hi limbs (|c| <= 2^(2E), m <= 2^(2E-1):
-// top limbs on the grid 2^11 G^2 stay within 2048) and the offset o fits one
-// slot, so the exact part is r + 5 slots:
-//   slots  0..15 (MFMA block 0, its groups 0-1): class 0 (r), C0 C1, M0 M1, O
-//   slots 16..79 (block 0 groups 2-3, block 1, the x16 block): class 1 (2r),
-//                class 2 (3r), C2 C3, M2 M3                       -> 5r + 4
-// Groups 0-1 hold multiples of G^2 only and their partial sums stay below
-// 2^24 G^2, so the accumulator after them is s_hi - o EXACTLY; the lower
-// classes follow in K order and round at 2^-24 |s - o| as in the KB layout.
-// Per 16x16 tile pair: 2 + 1 MFMAs of 16 + 8 cycles' issue instead of 3 x 16
-// (tools/probes/mfma_mix.hip: 103 vs 124 cycles per unit with the exp2/sum).
-// Image per 16-row tile: frags32 [2][64 lanes][8 halves] | frags16 [64][4].
-constexpr int K80_RMAX = 11;
-constexpr int K80_TILE_H = 2 * 64 * 8 + 64 * 4;   // halves per tile (2560 B)
-// (off while the c = 0 tiles' wrong sums under -amdgpu-mfma-vgpr-form are
-// diagnosed: tools/probes/x3_k80_debug.py, tools/probes/mfma_srcc_hazard.hip)
-constexpr bool K80_ON = false;
-__host__ __device__ constexpr bool x3_k80(int r) { return K80_ON && r <= K80_RMAX; }
-__host__ __device__ constexpr int x3_tile_halves(int r) {
-  return x3_k80(r) ? K80_TILE_H : (x3_kb0(r) + x3_kb12(r)) * 64 * 8;
-}
-__host__ __device__ constexpr int x3_koff(int r) { return x3_k80(r) ? r + 4 : r + 6; }
-
-struct Limbs4 { double c[4]; };
-// grid exponent of scalar limb l: 2E - 11 - 11 l (2^11 G^2, G^2, G^2 2^-11, G^2 2^-22)
-__device__ __forceinline__ int scalar_exp4(int l, int E) { return 2 * E - 11 - 11 * l; }
-__device__ __forceinline__ Limbs4 split_scalar4(double c, int E) {
-  Limbs4 L;
-  double r = c;
-  for (int l = 0; l < 4; ++l) {
-    const int e = scalar_exp4(l, E);
-    L.c[l] = rint(ldexp(r, -e));
-    r -= ldexp(L.c[l], e);
-  }
-  return L;
-}
-
-template <int SIDE>
-__device__ __forceinline__ float slot_value80(int k, int r, int E, const Limbs3* L,
-                                              const Limbs4& S) {
-  if (k < 16) {
-    const int e0 = 2 * (E - 11);
-    if (k < r) {  // class 0: a1 b1 G^2
-      const int x = e0 >> 1;
-      return opv(L[k].a1, SIDE == 0 ? x : e0 - x);
-    }
-    const int q = k - r;
-    if (q < 4) {  // 0, 1: c hi limbs (A); 2, 3: m hi limbs (B)
-      const int l = q & 1;
-      const int e = scalar_exp4(l, E);
-      const int x = e > 4 ? 4 : e;  // limb side exponent (|limb| <= 2048)
-      const bool limb_side = (q < 2) == (SIDE == 0);
-      return limb_side ? opv(S.c[l], x) : opv(1.0, e - x);
-    }
-    if (q == 4) return SIDE == 0 ? 1.f : 0.f;  // O: B = -o (set in the kernel)
-    return 0.f;
-  }
-  const int q = k - 16;
-  if (q < 5 * r) {
-    const int cls = q / r, dim = q % r;
-    const int pa[5] = {1, 2, 1, 2, 3}, pb[5] = {2, 1, 3, 2, 1};
-    const int p = SIDE == 0 ? pa[cls] : pb[cls];
-    const int etot = 2 * (E - 11) - 11 * (pa[cls] + pb[cls] - 2);
-    const int x = etot >> 1;
-    const double limb = p == 1 ? L[dim].a1 : (p == 2 ? L[dim].a2 : L[dim].a3);
-    return opv(limb, SIDE == 0 ? x : etot - x);
-  }
-  const int e4 = q - 5 * r;
-  if (e4 < 4) {  // 0, 1: c lo limbs (A); 2, 3: m lo limbs (B)
-    const int l = 2 + (e4 & 1);
-    const int e = scalar_exp4(l, E);
-    const int x = e < -24 ? -24 : e;  // limb side
-    const bool limb_side = (e4 < 2) == (SIDE == 0);
-    return limb_side ? opv(S.c[l], x) : opv(1.0, e - x);
-  }
-  return 0.f;
-}
-
-typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-
-// pack_x3_kernel's work for the K80 layout (same whitening, flags, Y / lw,
-// hint offsets; only the slot map and the image layout differ)
-template <int SIDE, int R>
-__global__ __launch_bounds__(128) void pack_x3k80_kernel(
-    const double* __restrict__ P, const double* __restrict__ w, int64_t n,
-    int d, const double* __restrict__ mu, const double* __restrict__ U, int r_rt,
-    double log_w_shift, const Header* __restrict__ hdr,
-    _Float16* __restrict__ img, int64_t ntiles, int32_t* __restrict__ flags,
-    double* __restrict__ Y, double* __restrict__ lw, int64_t Np,
-    const int64_t* __restrict__ hint, float* __restrict__ cand_o, int koff) {
-  constexpr int RR = R > 0 ? R : K80_RMAX;
-  const int r = R > 0 ? R : r_rt;
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= ntiles * 16) return;
-  const int E = hdr->E;
-  const bool ok = hdr->ok != 0;
-  const double L2 = ldexp(1.0, 2 * E);
-  double v[RR];
-  Limbs3 L[RR];
-  double scalar = SIDE == 0 ? -L2 : 0.0;
-  bool bad = false;
-  float hint_o = O_MIN;
-#pragma unroll
-  for (int k = 0; k < RR; ++k) v[k] = 0.0;
-  if (row < n) {
-    const double h = whiten<RR>(P, row, d, mu, U, r, v);
-    if (SIDE == 0) {
-      const double wj = w[row];
-      bad = !(wj > 0.0) || !(2.0 * h <= L2);
-      const double lwj = wj > 0.0 ? (log(wj) + log_w_shift) * LOG2E : -INFINITY;
-      scalar = bad ? -L2 : fmax(lwj - h, -L2);
-#pragma unroll
-      for (int k = 0; k < RR; ++k)
-        if (k < r) Y[row * r + k] = v[k];
-      lw[row] = lwj;
-    } else {
-      bad = !ok || !(2.0 * h <= L2);
-      scalar = bad ? -L2 : -h;
-      if (hint && !bad) {
-        const int64_t j = hint[row];
-        if (j < 0 || j >= Np || !(lw[j] > -INFINITY)) {
-          bad = true;
-        } else {
-          double q = 0.0;
-#pragma unroll
-          for (int k = 0; k < RR; ++k)
-            if (k < r) { const double t = v[k] - Y[j * r + k]; q += t * t; }
-          hint_o = (float)fmax(ceil(lw[j] - 0.5 * q), (double)O_MIN);
-        }
-        scalar = bad ? -L2 : -h;
-      }
-    }
-    if (bad)
-#pragma unroll
-      for (int k = 0; k < RR; ++k) v[k] = 0.0;
-  }
-  if (flags && row < n) flags[row] = bad ? 1 : 0;
-  if (cand_o) cand_o[row] = hint_o;
-#pragma unroll
-  for (int k = 0; k < RR; ++k) L[k] = split_coord(v[k], E);
-  const Limbs4 S = split_scalar4(scalar, E);
-  const int64_t t = row >> 4;
-  const int rl = (int)(row & 15);
-  _Float16* tile = img + t * K80_TILE_H;
-  auto value = [&](int k) {
-    float val = slot_value80<SIDE>(k, r, E, L, S);
-    if (SIDE == 1 && hint && k == koff) val = -hint_o;  // B = -o (A = 1)
-    return (_Float16)val;
-  };
-  // slots 0..63: 8 groups of 8 -> frags32 [kb][lane][8]
-#pragma unroll
-  for (int g = 0; g < 8; ++g) {
-    half8 frag;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) frag[j] = value(g * 8 + j);
-    const int kb = g >> 2, lane = rl + 16 * (g & 3);
-    *reinterpret_cast<half8*>(tile + (kb * 64 + lane) * 8) = frag;
-  }
-  // slots 64..79: 4 groups of 4 -> frags16 [lane][4]
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    half4 frag;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) frag[j] = value(64 + g * 4 + j);
-    *reinterpret_cast<half4*>(tile + 2 * 64 * 8 + (rl + 16 * g) * 4) = frag;
-  }
-}
-
 // ---- the fused limb-split GEMM + exp2 + weighted sum -----------------------
 // One wave = CT candidate tiles x one population chunk; block = 4 waves; 1-D
 // grid, block b -> XCD b % 8 owns chunks {xcd, xcd + 8, ...} so that the
@@ -608,144 +439,6 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
 #pragma unroll
   for (int c = 0; c < CT; ++c) l64[c] += (double)ls[c];
   // lanes l, l^16, l^32, l^48 hold the same candidate column (same o)
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    double v = l64[c];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    const int64_t ct = ct0 + c;
-    if (lane < 16 && ct < MT) {
-      if (PASS1) part_o[(int64_t)chunk * Mpad + ct * 16 + lane] = (double)o[c];
-      part_l[(int64_t)chunk * Mpad + ct * 16 + lane] = v;
-    }
-  }
-}
-
-// mvn_x3_kernel for the K80 layout: the chain per (tile, c) unit is two
-// v_mfma_f32_16x16x32_f16 and one v_mfma_f32_16x16x16_f16; everything else
-// (XCD map, pass 1 on block 0, offsets, exp2 + sums, flushes, combine
-// partials) is mvn_x3_kernel's.
-template <int CT, bool PASS1>
-__global__ __launch_bounds__(256) void mvn_x3k80_kernel(
-    const _Float16* __restrict__ A, const _Float16* __restrict__ Bi, int64_t MT,
-    int64_t NT, int nchunk, int64_t tiles_per_chunk, int64_t ngroups, int koff,
-    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int64_t bid = blockIdx.x;
-  const int cpx = nchunk >> 3;
-  const int64_t xcd = bid & 7, jb = bid >> 3;
-  const int chunk = (int)(xcd + 8 * (jb % cpx));
-  const int64_t group = jb / cpx;
-  if (group >= ngroups) return;
-  const int64_t ct0 = (group * 4 + wave) * CT;
-  const bool off_lane = (lane >> 4) == ((koff & 31) >> 3);
-  const int off_j = koff & 7;
-  auto f32 = [&](const _Float16* base, int64_t t, int kb) {
-    return *reinterpret_cast<const half8*>(base + t * K80_TILE_H + (kb * 64 + lane) * 8);
-  };
-  auto f16 = [&](const _Float16* base, int64_t t) {
-    return *reinterpret_cast<const half4*>(base + t * K80_TILE_H + 2 * 64 * 8 + lane * 4);
-  };
-  half8 b0[CT], b1[CT];
-  half4 b2[CT];
-#pragma unroll
-  for (int c = 0; c < CT; ++c) {
-    const int64_t ct = ct0 + c < MT ? ct0 + c : MT - 1;  // clamp: dup work, never stored
-    b0[c] = f32(Bi, ct, 0);
-    b1[c] = f32(Bi, ct, 1);
-    b2[c] = f16(Bi, ct);
-  }
-  const int64_t t_begin = (int64_t)chunk * tiles_per_chunk;
-  const int64_t t_end = t_begin + tiles_per_chunk < NT ? t_begin + tiles_per_chunk : NT;
-  static_assert(X3_PAD >= 7, "pad must cover the prefetch distance");
-
-  float o[CT];
-  if (PASS1 && t_begin < t_end) {
-    float mx[CT];
-#pragma unroll
-    for (int c = 0; c < CT; ++c) mx[c] = -INFINITY;
-    half8 ring[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) ring[u] = f32(A, t_begin + u, 0);
-    for (int64_t t = t_begin; t < t_end; t += 4) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (t + u < t_end) {
-#pragma unroll
-          for (int c = 0; c < CT; ++c) {
-            const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                ring[u], b0[c], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            mx[c] = max3(max3(mx[c], acc[0], acc[1]), acc[2], acc[3]);
-          }
-        }
-        ring[u] = f32(A, t + u + 4, 0);
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < CT; ++c) {
-      float cm = fmaxf(mx[c], __shfl_xor(mx[c], 16, 64));
-      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
-      o[c] = fmaxf(ceilf(cm), O_MIN);
-      if (off_lane) b0[c][off_j] = (_Float16)(-o[c]);
-    }
-  } else {
-#pragma unroll
-    for (int c = 0; c < CT; ++c) o[c] = O_MIN;
-  }
-
-  double l64[CT];
-  float ls[CT];
-#pragma unroll
-  for (int c = 0; c < CT; ++c) { l64[c] = 0.0; ls[c] = 0.f; }
-  half8 p0[2], p1[2];
-  half4 q0, q1;
-  if (t_begin < t_end) {
-    p0[0] = f32(A, t_begin, 0); p0[1] = f32(A, t_begin, 1); q0 = f16(A, t_begin);
-    p1[0] = f32(A, t_begin + 1, 0); p1[1] = f32(A, t_begin + 1, 1); q1 = f16(A, t_begin + 1);
-  }
-  auto chain = [&](const half8 (&a)[2], const half4& a2, int c) {
-    f32x4 r = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[0], b0[c], f32x4{0.f, 0.f, 0.f, 0.f},
-                                                     0, 0, 0);
-    r = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[1], b1[c], r, 0, 0, 0);
-    // A 16x16x16 MFMA that takes the accumulator of the 16x16x32 MFMA just
-    // before it as SrcC reads a stale value unless >= 2 wait states separate
-    // them, and the compiler inserts none for this mixed-shape pair
-    // (tools/probes/mfma_srcc_hazard.hip: wrong at 0-1, exact at >= 2 on
-    // gfx950).  The s_nop is tied to r so it sits between the two; 3 here.
-    asm volatile("s_nop 2" : "+v"(r));
-    return __builtin_amdgcn_mfma_f32_16x16x16f16(a2, b2[c], r, 0, 0, 0);
-  };
-  auto expsum = [&](const f32x4& v) {
-    return (__builtin_amdgcn_exp2f(v[0]) + __builtin_amdgcn_exp2f(v[1])) +
-           (__builtin_amdgcn_exp2f(v[2]) + __builtin_amdgcn_exp2f(v[3]));
-  };
-  auto do_tile = [&](const half8 (&a)[2], const half4& a2) {
-    f32x4 prev = chain(a, a2, 0);
-#pragma unroll
-    for (int c = 1; c < CT; ++c) {
-      const f32x4 cur = chain(a, a2, c);
-      ls[c - 1] += expsum(prev);
-      prev = cur;
-    }
-    ls[CT - 1] += expsum(prev);
-  };
-  int nflush = 0;
-  for (int64_t t = t_begin; t < t_end; t += 2) {
-    do_tile(p0, q0);
-    p0[0] = f32(A, t + 2, 0); p0[1] = f32(A, t + 2, 1); q0 = f16(A, t + 2);
-    if (t + 1 < t_end) {
-      do_tile(p1, q1);
-      p1[0] = f32(A, t + 3, 0); p1[1] = f32(A, t + 3, 1); q1 = f16(A, t + 3);
-    }
-    if (++nflush == 8) {
-      nflush = 0;
-#pragma unroll
-      for (int c = 0; c < CT; ++c) { l64[c] += (double)ls[c]; ls[c] = 0.f; }
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < CT; ++c) l64[c] += (double)ls[c];
 #pragma unroll
   for (int c = 0; c < CT; ++c) {
     double v = l64[c];
@@ -908,22 +601,6 @@ void launch_pack(int r, dim3 grid, hipStream_t s, const double* P, const double*
                  _Float16* img, int64_t ntiles, int32_t* flags, double* Y,
                  double* lw, int64_t Np, const int64_t* hint, float* cand_o,
                  int koff) {
-#define ABC_PACK80_CASE(RC)                                                        \
-  case RC:                                                                         \
-    hipLaunchKernelGGL((pack_x3k80_kernel<SIDE, RC>), grid, dim3(128), 0, s, P, w, \
-                       n, d, mu, U, r, log_w_shift, hdr, img, ntiles, flags, Y, lw, \
-                       Np, hint, cand_o, koff);                                    \
-    break;
-  if (x3_k80(r)) {
-    switch (r) {
-      ABC_PACK80_CASE(1) ABC_PACK80_CASE(2) ABC_PACK80_CASE(3) ABC_PACK80_CASE(4)
-      ABC_PACK80_CASE(5) ABC_PACK80_CASE(6) ABC_PACK80_CASE(7) ABC_PACK80_CASE(8)
-      ABC_PACK80_CASE(9) ABC_PACK80_CASE(10)
-      default: ABC_PACK80_CASE(0)
-    }
-    return;
-  }
-#undef ABC_PACK80_CASE
 #define ABC_PACK_CASE(RC)                                                          \
   case RC:                                                                         \
     hipLaunchKernelGGL((pack_x3_kernel<SIDE, RC>), grid, dim3(128), 0, s, P, w, n, \
@@ -957,8 +634,6 @@ __global__ void x3_scatter_rescued(const int64_t* __restrict__ rescue, int64_t n
 
 struct PlanX3 {
   int KB0, KB, CT, nchunk;
-  bool k80;                 // the K80 layout (r <= K80_RMAX)
-  int tile_halves;          // image halves per 16-row tile
   int64_t MT, NT, MTpad, groups, tiles_per_chunk, Mpad;
 };
 
@@ -966,8 +641,6 @@ PlanX3 make_plan_x3(int64_t M, int64_t N, int r) {
   PlanX3 p;
   p.KB0 = x3_kb0(r);
   p.KB = p.KB0 + x3_kb12(r);
-  p.k80 = x3_k80(r);
-  p.tile_halves = x3_tile_halves(r);
   p.CT = p.KB <= 3 ? 8 : 4;
   p.MT = ceil_div(M > 0 ? M : 1, 16);
   p.NT = ceil_div(N > 0 ? N : 1, 16);
@@ -988,7 +661,7 @@ PlanX3 make_plan_x3(int64_t M, int64_t N, int r) {
 
 size_t plan_x3_ws(const PlanX3& p) {
   size_t off = 0;
-  size_only<_Float16>(off, (size_t)p.MTpad * p.tile_halves);  // candidate image
+  size_only<_Float16>(off, (size_t)p.MTpad * p.KB * 64 * 8);  // candidate image
   size_only<int32_t>(off, (size_t)p.Mpad);                     // candidate flags
   size_only<float>(off, (size_t)p.Mpad);                       // hinted offsets
   size_only<double>(off, (size_t)p.nchunk * p.Mpad);           // partial offsets
@@ -1014,20 +687,6 @@ void launch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
 
 int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
                 double* po, double* pl, bool pass1, hipStream_t s) {
-  if (p.k80) {
-    const int64_t blocks = p.groups * p.nchunk;
-    const _Float16* Ah = reinterpret_cast<const _Float16*>(A);
-    const _Float16* Bh = reinterpret_cast<const _Float16*>(B);
-    if (pass1)
-      hipLaunchKernelGGL((mvn_x3k80_kernel<8, true>), dim3((unsigned)blocks), dim3(256), 0, s,
-                         Ah, Bh, p.MT, p.NT, p.nchunk, p.tiles_per_chunk, p.groups, koff, po,
-                         pl, p.Mpad);
-    else
-      hipLaunchKernelGGL((mvn_x3k80_kernel<8, false>), dim3((unsigned)blocks), dim3(256), 0, s,
-                         Ah, Bh, p.MT, p.NT, p.nchunk, p.tiles_per_chunk, p.groups, koff, po,
-                         pl, p.Mpad);
-    return ABC_OK;
-  }
   switch (p.KB) {
     case 2: launch_x3<2, 8>(p, A, B, koff, po, pl, pass1, s); break;
     case 3: launch_x3<3, 8>(p, A, B, koff, po, pl, pass1, s); break;
@@ -1045,8 +704,9 @@ int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
 // ---- internal entry points used by abc_mvn.hip ------------------------------
 // image = header | fragments [NT][KB][64][8] f16 | Y [N x r] f64 | lw [N] f64
 size_t x3_frag_bytes(int64_t N, int r) {
+  const int KB = x3_kb0(r) + x3_kb12(r);
   const int64_t NT = ceil_div(N > 0 ? N : 1, 16) + X3_PAD;
-  return align_up((size_t)NT * x3_tile_halves(r) * sizeof(_Float16), 256);
+  return align_up((size_t)NT * KB * 64 * 8 * sizeof(_Float16), 256);
 }
 double* x3_Y(const void* packed, int64_t N, int r) {
   return (double*)((char*)packed + HDR + x3_frag_bytes(N, r));
@@ -1062,8 +722,8 @@ size_t x3_packed_bytes(int64_t N, int r) {
 int x3_max_rank() { return MAX_R; }
 
 extern "C" int abc_mvn_x3_layout(int r, int* kslots) {
-  if (kslots) *kslots = x3_k80(r) ? 80 : 32 * (x3_kb0(r) + x3_kb12(r));
-  return x3_k80(r) ? 1 : 0;
+  if (kslots) *kslots = 32 * (x3_kb0(r) + x3_kb12(r));
+  return 0;
 }
 
 int x3_pack_population(const double* X, const double* w, int64_t N, int d,
@@ -1107,7 +767,7 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
     return set_error(ABC_ERR_WORKSPACE, "mvn x3: workspace %zu < %zu", ws_bytes,
                      plan_x3_ws(p));
   Carver cv(ws, ws_bytes);
-  _Float16* Bimg = cv.take<_Float16>((size_t)p.MTpad * p.tile_halves);
+  _Float16* Bimg = cv.take<_Float16>((size_t)p.MTpad * p.KB * 64 * 8);
   int32_t* cflags = cv.take<int32_t>((size_t)p.Mpad);
   float* cand_o = cv.take<float>((size_t)p.Mpad);
   double* po = cv.take<double>((size_t)p.nchunk * p.Mpad);
@@ -1121,10 +781,10 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
   launch_pack<1>(r, dim3((unsigned)ceil_div(p.MTpad * 16, 128)), s, x,
                  (const double*)nullptr, M, d, mu, U, log_norm - log_const, p.KB0,
                  p.KB, hdr, Bimg, p.MTpad, cflags, x3_Y(packed, N, r),
-                 x3_lw(packed, N, r), N, hint, hint ? cand_o : (float*)nullptr, x3_koff(r));
+                 x3_lw(packed, N, r), N, hint, hint ? cand_o : (float*)nullptr, r + 6);
   ABC_LAUNCHED();
   profile_start(s, prof_channel);
-  int rc = dispatch_x3(p, Aimg, (const half8*)Bimg, x3_koff(r), po, pl, hint == nullptr, s);
+  int rc = dispatch_x3(p, Aimg, (const half8*)Bimg, r + 6, po, pl, hint == nullptr, s);
   profile_stop(s, prof_channel);
   if (rc) return rc;
   ABC_LAUNCHED();

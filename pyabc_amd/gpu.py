@@ -184,8 +184,8 @@ def mvn_logpdf(x, packed, N, mu, U, prec, log_const, out=None, X=None, w=None,
 
 
 def mvn_x3_layout(r):
-    """(kernel, K slots per pair) the x3 density runs at whitened rank r:
-    kernel 1 = mvn_x3k80_kernel (K = 80), 0 = mvn_x3_kernel (K = 32 x blocks)."""
+    """(kernel, K slots per pair) the x3 density runs at whitened rank r
+    (kernel 0 = mvn_x3_kernel, K = 32 x MFMA blocks)."""
     import ctypes
     k = ctypes.c_int(0)
     kernel = int(nat.load().abc_mvn_x3_layout(int(r), ctypes.byref(k)))

@@ -135,11 +135,10 @@ def test_mvn_x3_rescue_and_edges(dev):
 
 
 @pytest.mark.parametrize("d", [1, 7, 11, 12, 16, 25])
-def test_mvn_x3_layouts_vs_oracle(dev, d):
-    """Both x3 operand layouts against the fp64 oracle: the K80 layout (two
-    16x16x32 + one 16x16x16 f16 MFMAs, whitened rank <= 11) and the 32-slot
-    block layout above it (d = 12, 16, 25 = the largest x3 rank); unhinted
-    (max pre-pass) and hinted by the proposals' ancestors; 1e-6 / 2e-6."""
+def test_mvn_x3_ranks_vs_oracle(dev, d):
+    """The x3 density against the fp64 oracle over whitened ranks 1..25 (the
+    largest x3 rank; KB = 2..6 MFMA blocks per tile pair), unhinted (max
+    pre-pass) and hinted by the proposals' ancestors; 1e-6 / 2e-6."""
     import pandas as pd
     from pyabc_amd.transition import MultivariateNormalTransition
     rng = np.random.default_rng(100 + d)

@@ -1,22 +1,21 @@
 #!/bin/bash
-# Round-4 job c: parity of the changed kernels (K80 x3 density, weighted-
-# quantile select + sorted fallback, padded k-NN rows, accept tail, large-N
-# statistics), then same-box A/Bs: x3 K80 vs HEAD's KB layout (c3 bench,
-# alternating), c5 fit (unpadded baseline / padded / DEFER_V2); the k-NN PMC
-# on the padded kernel, the x3 traffic passes, the user-model probe.
+# Round-4 job c: parity of the changed kernels (weighted-quantile select +
+# sorted fallback, padded k-NN rows, accept tail, wide LocalTransition,
+# large-N statistics), then same-box A/Bs of the c5 fit (unpadded baseline /
+# padded / DEFER_V2 / dense-kernel shapes); the k-NN PMC on the padded
+# kernel, the c3 trace and x3 traffic passes, the user-model probe, the
+# candidate round with weight-sorted records.
 set -o pipefail
 export TMPDIR=/tmp PYTHONPATH=$PWD
 O=gpurun_out/r04c
 W=/tmp/r04cw
 mkdir -p $O $W
-# PART=tests: parity + x3 A/B; PART=rest: everything after (two gpurun calls)
+# PART=tests: the GPU parity suites; PART=rest: everything after (two gpurun calls)
 if [ "${PART:-tests}" = tests ]; then
 timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
   tests/test_gpu_kernels.py tests/test_gpu_rows.py tests/test_gpu_fused.py tests/test_gpu_fallbacks.py \
   tests/test_gpu_e2e.py::test_large_n_parity_vs_reference > $O/tests.log 2>&1 || { echo "tests failed"; tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
-STEPS=8 bash tools/ab_x3.sh > $O/ab_x3.log 2>&1 || { echo "x3 ab failed"; tail -20 $O/ab_x3.log; tail -20 gpurun_out/ab_x3.log; exit 1; }
-cat $O/ab_x3.log
 exit 0
 fi
 ABCGPU_LIB=ab/libdeferv2.so timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
@@ -38,7 +37,7 @@ for set in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $set --output-format csv -d $W/x3pmc$i -o run -- python3 bench.py $ARGS > $O/x3pmc$i.log 2>&1 || { echo "x3 pmc $i failed"; tail -3 $O/x3pmc$i.log; exit 1; }
 done
-python3 tools/traffic_from_pmc.py $W "mvn_x3k80_kernelILi8ELb0E" 1000000 10 $O/x3_traffic_c3.json > $O/traffic.log 2>&1 || true
+python3 tools/traffic_from_pmc.py $W "mvn_x3_kernelILi3ELi8ELb0E" 1000000 10 $O/x3_traffic_c3.json > $O/traffic.log 2>&1 || true
 cat $O/traffic.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $W/cm -o run -- python3 -u tools/probes/custom_model_c2.py 20 > $O/custom20.log 2>&1 || { echo "custom probe failed"; tail -5 $O/custom20.log; exit 1; }
 find $W/cm -name "*kernel_stats.csv" -exec cp {} $O/custom_model_kernel_stats.csv \;

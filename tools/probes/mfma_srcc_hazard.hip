@@ -16,6 +16,22 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+template <int G, typename T>
+__device__ __forceinline__ void gap2(f32x4& r, T& x) {
+  if constexpr (G == 0) asm volatile("" : "+v"(r), "+v"(x));
+  if constexpr (G == 1) asm volatile("s_nop 0" : "+v"(r), "+v"(x));
+  if constexpr (G == 2) asm volatile("s_nop 1" : "+v"(r), "+v"(x));
+  if constexpr (G == 3) asm volatile("s_nop 2" : "+v"(r), "+v"(x));
+  if constexpr (G == 4) asm volatile("s_nop 3" : "+v"(r), "+v"(x));
+  if constexpr (G == 6) asm volatile("s_nop 5" : "+v"(r), "+v"(x));
+  if constexpr (G == 8) asm volatile("s_nop 7" : "+v"(r), "+v"(x));
+  if constexpr (G == 10) asm volatile("s_nop 7\n\ts_nop 1" : "+v"(r), "+v"(x));
+  if constexpr (G == 12) asm volatile("s_nop 7\n\ts_nop 3" : "+v"(r), "+v"(x));
+  if constexpr (G == 16) asm volatile("s_nop 7\n\ts_nop 7" : "+v"(r), "+v"(x));
+  if constexpr (G == 20) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(r), "+v"(x));
+  if constexpr (G == 24) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(r), "+v"(x));
+}
+
 template <int G>
 __device__ __forceinline__ void gap(f32x4& r) {
   if constexpr (G == 0) asm volatile("" : "+v"(r));
@@ -38,7 +54,8 @@ __device__ __forceinline__ f32x4 mm(half8 a, half8 b, half4 a4, half4 b4, f32x4 
   else return __builtin_amdgcn_mfma_f32_16x16x16f16(a4, b4, c, 0, 0, 0);
 }
 
-// MODE 0: chain P -> G -> Q (SrcC); MODE 1: P -> G -> v_add
+// MODE 0: chain P -> G -> Q (SrcC); MODE 1: P -> G -> v_add;
+// MODE 2: P -> G -> independent Q (own accumulator from 0), both read
 template <int MODE, int P, int Q, int G>
 __global__ void probe(const half8* A, const half8* B, const half4* A4, const half4* B4,
                       float* out) {
@@ -53,14 +70,20 @@ __global__ void probe(const half8* A, const half8* B, const half4* A4, const hal
   asm volatile("" : "+v"(ra), "+v"(rb), "+v"(ra2), "+v"(rb2), "+v"(ra4), "+v"(rb4),
                "+v"(ra42), "+v"(rb42));   // the reference's copies (no CSE)
   f32x4 r = mm<P>(a, b, a4, b4, f32x4{0.f, 0.f, 0.f, 0.f});
-  gap<G>(r);
+  if constexpr (MODE == 2) {
+    if constexpr (Q == 32) gap2<G>(r, a2); else gap2<G>(r, a42);
+    f32x4 r2 = mm<Q>(a2, b2, a42, b42, f32x4{0.f, 0.f, 0.f, 0.f});
+    r += r2;
+  } else {
+    gap<G>(r);
+  }
   if (MODE == 0) r = mm<Q>(a2, b2, a42, b42, r);
   f32x4 v;
   for (int i = 0; i < 4; ++i) v[i] = r[i] + 1.0f;
   for (int i = 0; i < 4; ++i) out[lane * 4 + i] = v[i];
   // reference: separate products, summed on the VALU after a full drain
   f32x4 p = mm<P>(ra, rb, ra4, rb4, f32x4{0.f, 0.f, 0.f, 0.f});
-  f32x4 q = MODE == 0 ? mm<Q>(ra2, rb2, ra42, rb42, f32x4{0.f, 0.f, 0.f, 0.f})
+  f32x4 q = MODE != 1 ? mm<Q>(ra2, rb2, ra42, rb42, f32x4{0.f, 0.f, 0.f, 0.f})
                       : f32x4{0.f, 0.f, 0.f, 0.f};
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(p), "+v"(q));
   for (int i = 0; i < 4; ++i) out[256 + lane * 4 + i] = (p[i] + q[i]) + 1.0f;
@@ -75,6 +98,8 @@ void run(half8* A, half8* B, half4* A4, half4* B4, float* d_out) {
   for (int i = 0; i < 256; ++i) bad += h[i] != h[256 + i];
   if (MODE == 0)
     printf("chain x%d -> x%d  gap %3d: %3d / 256 wrong\n", P, Q, G, bad);
+  else if (MODE == 2)
+    printf("indep x%d -> x%d  gap %3d: %3d / 256 wrong\n", P, Q, G, bad);
   else
     printf("valu  x%d -> add  gap %3d: %3d / 256 wrong\n", P, G, bad);
 }
@@ -108,6 +133,8 @@ int main() {
   sweep<0, 32, 16>(A, B, A4, B4, out);
   sweep<0, 16, 32>(A, B, A4, B4, out);
   sweep<0, 16, 16>(A, B, A4, B4, out);
+  sweep<2, 32, 16>(A, B, A4, B4, out);
+  sweep<2, 16, 32>(A, B, A4, B4, out);
   sweep<1, 32, 0>(A, B, A4, B4, out);
   sweep<1, 16, 0>(A, B, A4, B4, out);
   return hipDeviceSynchronize() == hipSuccess ? 0 : 1;

@@ -1,4 +1,4 @@
-"""Which candidates does the x3 density get wrong?  x3 vs the f64-MFMA mode
+"""Which candidate tiles does the x3 density get wrong?  x3 vs the f64-MFMA mode
 (2e-6) on random populations; prints the wrong candidate tiles per shape.
 ABCGPU_LIB selects the library.  tools/probes, not part of the library."""
 import sys
@@ -23,6 +23,18 @@ for d, N, M in [(1, 1000, 256), (1, 1000, 1000), (2, 500, 256), (5, 4096, 512),
         t = MultivariateNormalTransition(precision=prec)
         t.fit(X, w.copy())
         res[prec] = np.asarray(t.pdf(x))
+        if prec == "x3":
+            # hinted pass (the sampler's path): nearest population row
+            import torch
+            dx = x.to_numpy()[:, None, :] - X.to_numpy()[None, :, :]
+            near = np.argmin((dx ** 2).sum(-1), axis=1)
+            xd = torch.as_tensor(x.to_numpy(), device="cuda")
+            hd = torch.as_tensor(near, dtype=torch.int64, device="cuda")
+            res["x3h"] = np.exp(t.logpdf_device(xd, hint=hd).cpu().numpy())
+    relh = np.abs(res["x3h"] / res["f64"] - 1)
+    wh = np.nonzero(relh > 1e-5)[0]
+    bad_total += len(wh)
+    print(f"  hinted: {len(wh)} wrong, tiles {sorted(set((wh // 16).tolist()))[:20]}")
     rel = np.abs(res["x3"] / res["f64"] - 1)
     wrong = np.nonzero(rel > 1e-5)[0]
     bad_total += len(wrong)
