@@ -689,7 +689,7 @@ __global__ __launch_bounds__(256) void local_finish_kernel(
     for (int a = 0; a < D; ++a)
       for (int b = 0; b < D; ++b) lu[a][b] = cov[a][b];
     det = lu_factor<D>(lu, perm);
-    if (det > 0.0 || it >= 1000000) break;
+    if (!(det <= 0.0) || it >= 1000000) break;  // NaN exits, as "while det <= 0" does
     for (int a = 0; a < D; ++a) cov[a][a] += eps;
   }
   double inv[D][D], L[D][D];

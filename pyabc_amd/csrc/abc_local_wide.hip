@@ -308,7 +308,7 @@ __global__ __launch_bounds__(WT) void local_wide_fit_kernel(WideFitArgs A) {
             for (int j = c + 1; j < d; ++j) a_lu[(r) * ld + (j)] -= fct * a_lu[(c) * ld + (j)];
           }
         }
-        if (det > 0.0 || it >= 1000000) break;
+        if (!(det <= 0.0) || it >= 1000000) break;  // NaN exits, as "while det <= 0" does
         for (int a = 0; a < d; ++a) cov[(a) * ld + (a)] += A.eps;
       }
       double* inv = A.invs + n * d * d;
