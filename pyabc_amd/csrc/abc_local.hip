@@ -1049,7 +1049,7 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const double* __restrict
       for (int y = 0; y < RS; ++y) c += part[((int64_t)y * NCP + f * ML_NL + l) * N + n];
       v += ldexp(c, e - 11 * (l + 1));
     }
-    if (extra) v += extra[(int64_t)f * N + n];   // deferred collect (ABC_DEFER_V2)
+    if (extra) v += extra[(int64_t)f * N + n];   // deferred collect: queued members
     S[f] = v;
     // last-limb rounding per member + the limb sum's own rounding
     E[f] = (double)nq * ldexp(1.0, e - 11 * ML_NL - 1) + 4.0 * MM_EPS * fabs(v);
@@ -1242,7 +1242,7 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
         ABC_LAUNCHED();
         hipLaunchKernelGGL((mm_finish_kernel<D>), dim3((unsigned)ceil_div(N, 256)), dim3(256), 0, s,
                            X, N, nq, (const double*)part16, RS16, (const double*)bnd, cenm, flag,
-                           (const double*)(ABC_DEFER_V2 ? part : nullptr));
+                           (const double*)part);
         ABC_LAUNCHED();
         int h_f[2] = {0, 0};
         ABC_HIP(hipMemcpyAsync(h_f, flag, 2 * sizeof(int), hipMemcpyDeviceToHost, s));

@@ -70,12 +70,6 @@ __global__ __launch_bounds__(256) void knn_rows_kernel(const double* __restrict_
 // queue per block (DQ_L per particle), flushed to the global queue at the
 // end with one atomic per particle; a full LDS queue spills by global atomics.
 constexpr int DQ_L = 16;
-#ifndef ABC_DEFER_V2
-// build-time A/B (unmeasured): one LDS queue atomic per lane instead of per
-// open pair, and the resolve's queued members summed as NM fp64 features in
-// index order (added by mm_finish_kernel) instead of 110 limb columns
-#define ABC_DEFER_V2 0
-#endif
 template <int D, bool DEFER>
 __global__ __launch_bounds__(DM_T) void knn_dense_kernel(
     const double* __restrict__ X, const double* __restrict__ cen,
@@ -210,7 +204,6 @@ __global__ __launch_bounds__(DM_T) void knn_dense_kernel(
         for (int g = 0; g < DM_G; ++g) nin[g] += __builtin_popcount((inm >> (8 * g)) & 0xFFu);
       }
       if (DEFER && __builtin_amdgcn_ballot_w64(openm != 0u) != 0ull) {
-#if ABC_DEFER_V2
         // queue the open pairs (their a stays 0): one LDS atomic per lane
         // reserves its slots
 #pragma unroll
@@ -236,26 +229,6 @@ __global__ __launch_bounds__(DM_T) void knn_dense_kernel(
             }
           }
         }
-#else
-        // queue the open pairs (their a stays 0)
-#pragma unroll
-        for (int g = 0; g < DM_G; ++g) {
-          const int64_t pn = p0 + 16 * g + (lane & 15);
-          const int pl = (wv * DM_G + g) * 16 + (lane & 15);
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const int64_t j = 32 * (sb + k) + 8 * kq + u;
-            if (!((openm >> (8 * g + u)) & 1u) || j >= N || pn >= N) continue;
-            const int slot = atomicAdd(&s_qn[pl], 1);
-            if (slot < DQ_L) {
-              s_q[pl * DQ_L + slot] = (int)j;
-            } else {
-              const int gs = atomicAdd(&qcnt[pn], 1);
-              if (gs < KN_QCAP) qidx[pn * KN_QCAP + gs] = (int)j;
-            }
-          }
-        }
-#endif
       } else if (!DEFER && __builtin_amdgcn_ballot_w64(openm != 0u) != 0ull) {
         // rare: settle the open pairs in fp64 (rank-0 row excluded)
 #pragma unroll
@@ -316,12 +289,14 @@ __global__ __launch_bounds__(DM_T) void knn_dense_kernel(
 // count, those in [T_lo, T_hi) are ranked in (key, index) order, and rank
 // nq - 1 - #below is the selected neighbour (as in knn_select_kernel's
 // steps 3-4).  The members among the queue (below T_lo, or ranked at most
-// the selected one; the rank-0 row excluded) add their limbs L_l(F_j,f) into
-// part's chunk 0: integers, so the sums are exactly the ones the MFMA would
-// have formed with those rows' membership set, in any order (deterministic
-// although the queue's order comes from atomics).  A particle flagged by the
-// select, with an overflowing queue or with the rank outside the kept set
-// counts into nfail (the host then reruns the fit with the in-kernel collect).
+// the selected one; the rank-0 row excluded) are put in index order -- the
+// queue's order comes from atomics, index order makes the sum deterministic
+// -- and lanes 0..NM-1 each sum one fp64 moment feature over them into
+// `extra` (mm_finish_kernel adds it to the limb sums of the certain members).
+// A particle flagged by the select, with an overflowing queue or with the
+// rank outside the kept set counts into nfail (the host then reruns the fit
+// with the in-kernel collect).  Queueing in knn_dense_kernel reserves a
+// lane's slots with one LDS atomic (popcount of its open pairs).
 template <int D>
 __global__ __launch_bounds__(256) void knn_resolve_kernel(
     const double* __restrict__ X, const double* __restrict__ w, int64_t N, int64_t nq,
@@ -335,9 +310,7 @@ __global__ __launch_bounds__(256) void knn_resolve_kernel(
   constexpr int CPL = (NC + 63) / 64;
   __shared__ double s_key[4][KN_QCAP];
   __shared__ int s_idx[4][KN_QCAP];
-#if ABC_DEFER_V2
   __shared__ int s_ord[4][KN_QCAP];
-#endif
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t n = (int64_t)blockIdx.x * 4 + wv;
   const bool live = n < N;
@@ -398,7 +371,6 @@ __global__ __launch_bounds__(256) void knn_resolve_kernel(
       sel_rank0[n] = r0l;
     }
   }
-#if ABC_DEFER_V2
   if (live && !ok && lane == 0) atomicAdd(nfail, 1);
   // members in index order (a deterministic summation order: the queue's
   // order comes from atomics), their NM features summed in fp64 into extra
@@ -434,43 +406,4 @@ __global__ __launch_bounds__(256) void knn_resolve_kernel(
     }
   if (ok && lane < NM) extra[(int64_t)lane * N + n] = sum;
   (void)bnd; (void)part;
-#else
-  if (live && !ok) {
-    if (lane == 0) atomicAdd(nfail, 1);
-    return;
-  }
-  if (!live) return;
-  // members' limbs: lane owns columns lane + 64 h
-  int ef[CPL];
-  double acc[CPL];
-#pragma unroll
-  for (int h = 0; h < CPL; ++h) {
-    const int c = lane + 64 * h;
-    ef[h] = c < NC ? mm_fexp<D>(c / ML_NL, bnd) : 0;
-    acc[h] = 0.0;
-  }
-#pragma unroll
-  for (int i = 0; i < E; ++i) {
-    unsigned long long m = __builtin_amdgcn_ballot_w64(mem[i]);
-    while (m) {
-      const int src = __builtin_ctzll(m);
-      m &= m - 1;
-      const int j = __shfl(jj[i], src, 64);
-      double y[D];
-#pragma unroll
-      for (int a = 0; a < D; ++a) y[a] = X[(int64_t)j * D + a] - X[a];
-      const double lw = w[j];
-#pragma unroll
-      for (int h = 0; h < CPL; ++h) {
-        const int c = lane + 64 * h;
-        if (c < NC) acc[h] += mm_limb(mm_feature<D>(c / ML_NL, lw, y), ef[h], c % ML_NL);
-      }
-    }
-  }
-#pragma unroll
-  for (int h = 0; h < CPL; ++h) {
-    const int c = lane + 64 * h;
-    if (c < NC) part[(int64_t)c * N + n] += acc[h];
-  }
-#endif
 }
