@@ -295,8 +295,9 @@ int abc_candidates_regen(const abc_candidate_spec* spec, int64_t idx0,
                          double* dist, void* stream);
 
 /* Proposals only, candidates idx0 .. idx0 + B - 1: theta [B x d], prior
- * log-density [B] (-inf when the proposal gave up), ancestor [B] (may be
- * null), attempts [B] (may be null).  The fused round's proposal
+ * log-density [B] (-inf when the proposal gave up; may be null -- the
+ * sampler computes it for the kept rows only, abc_prior_logpdf gives the
+ * same bits), ancestor [B] (may be null), attempts [B] (may be null).  The fused round's proposal
  * (propose_one over the ancestor table, the prior support box computed once):
  * bit-identical to abc_propose / abc_local_propose and to the rows
  * abc_candidates_regen returns.  The spec's simulator / distance fields must

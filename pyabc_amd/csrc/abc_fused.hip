@@ -353,8 +353,7 @@ __global__ __launch_bounds__(256) void fused_regen_kernel(
 }
 
 // ---- proposals only (the staged path of models without a fused simulator) --
-// Rows [0, B) of candidates idx0 + b: theta (through an LDS tile, so a
-// block's rows leave as consecutive doubles), prior log-density, ancestor,
+// Rows [0, B) of candidates idx0 + b: theta, prior log-density, ancestor,
 // attempts.  The same propose_one as the round and the regeneration (the
 // ancestor table, the support box computed once), so the staged path's
 // proposals are the fused path's bits; each block proposes FP_CPT groups of
@@ -365,35 +364,23 @@ __global__ __launch_bounds__(256) void fused_propose_kernel(
     RoundArgs A, int64_t idx0, int64_t B, double* __restrict__ theta,
     double* __restrict__ lp, int64_t* __restrict__ anc, int32_t* __restrict__ att_out) {
   constexpr int DM = D > 0 ? D : 64;
-  constexpr int TW = D > 0 ? D : 16;          // LDS tile width (D = 0: 16-column chunks)
   __shared__ BlockConsts C;
-  __shared__ double tile[FR_T][TW + 1];
   stage_block_consts<D, MODE, true>(C, A.P, nullptr, A.box);
   const int d = D > 0 ? D : A.P.d;
+  // rows stored straight from registers: a wave's d stores cover its 64 rows'
+  // 64 d contiguous doubles, which L2 merges into whole lines (an LDS
+  // transposition with two barriers per 256 rows ran at 1.2e10 rows/s)
   for (int c = 0; c < FP_CPT; ++c) {
-    const int64_t i0 = ((int64_t)blockIdx.x * FP_CPT + c) * FR_T;
-    if (i0 >= B) break;                        // uniform over the block
-    const int64_t i = i0 + threadIdx.x;
-    const bool valid = i < B;
-    const int nvalid = B - i0 < FR_T ? (int)(B - i0) : FR_T;
+    const int64_t i = ((int64_t)blockIdx.x * FP_CPT + c) * FR_T + threadIdx.x;
+    if (i >= B) break;
     double th[DM];
     int64_t j = -1;
-    int att = A.P.max_attempts + 1;
-    if (valid) att = propose_one<D, MODE, true>(A.P, C, (uint64_t)(idx0 + i), th, j);
-    for (int k0 = 0; k0 < d; k0 += TW) {
-      const int w = d - k0 < TW ? d - k0 : TW;
+    const int att = propose_one<D, MODE, true>(A.P, C, (uint64_t)(idx0 + i), th, j);
+    double* row = theta + i * d;
 #pragma unroll
-      for (int k = 0; k < TW; ++k)
-        if (k < w && valid) tile[threadIdx.x][k] = th[k0 + k];
-      __syncthreads();
-      for (int e = threadIdx.x; e < FR_T * w; e += FR_T) {
-        const int r = e / w, q = e - r * w;
-        if (r < nvalid) theta[(i0 + r) * d + k0 + q] = tile[r][q];
-      }
-      __syncthreads();
-    }
-    if (!valid) continue;
-    lp[i] = att <= A.P.max_attempts ? prior_logpdf(A.P.kind, A.P.params, d, th) : -INFINITY;
+    for (int k = 0; k < DM; ++k)
+      if (k < d) row[k] = th[k];
+    if (lp) lp[i] = att <= A.P.max_attempts ? prior_logpdf(A.P.kind, A.P.params, d, th) : -INFINITY;
     if (anc) anc[i] = j;
     if (att_out) att_out[i] = att;
   }
@@ -413,6 +400,11 @@ __global__ __launch_bounds__(256) void fused_propose_kernel(
 // on the prior support (attempts > max_attempts) is never accepted, as
 // abc_mask_gave_up's NaN.
 constexpr int PA_ROWS = 8;    // rows in flight per wave (wide path)
+// rows per LDS chunk of the row path: 256, fewer when 256 padded rows of S
+// doubles would pass 64 KB (S = 32: 248); even, so chunks stay 16-B aligned
+__host__ __device__ constexpr int pa_chunk_rows(int S) {
+  return (65536 / ((S + 1) * 8)) >= FR_T ? FR_T : ((65536 / ((S + 1) * 8)) & ~1);
+}
 template <bool WIDE>
 __global__ __launch_bounds__(FR_T) void pnorm_accept_kernel(
     const double* __restrict__ x, int64_t B, int S, const double* __restrict__ x0,
@@ -429,19 +421,67 @@ __global__ __launch_bounds__(FR_T) void pnorm_accept_kernel(
   };
   auto ok = [&](int64_t b) { return att == nullptr || att[b] <= max_attempts; };
   if (!WIDE) {
-#pragma unroll 1
-    for (int it = 0; it < FR_CPT; ++it) {
-      const int loc = it * FR_T + tid;
-      const int64_t b = tile0 + loc;
-      if (b >= B) break;
-      const double* xr = x + b * S;
-      double s = 0.0;
-      if (inf) {
-        for (int k = 0; k < S; ++k) s = fmax(s, fabs(wf[k] * (xr[k] - x0[k])));
-      } else {
-        for (int k = 0; k < S; ++k) s += pterm(fabs(wf[k] * (xr[k] - x0[k])), p);
+    // chunks of RC rows (pa_chunk_rows: 256, or what 64 KB of LDS holds):
+    // the chunk's RC * S contiguous doubles come in with 16-B coalesced loads
+    // (the next chunk's held in registers while this one is summed), land in
+    // LDS rows of stride S + 1 (2-way banked reads), and each thread sums its
+    // row in k order as abc_pnorm does
+    extern __shared__ double pa_rows[];
+    const int S1 = S + 1;
+    const int RC = pa_chunk_rows(S);
+    const int n16 = RC * S / 2;                   // 16-B pieces per chunk (RC even)
+    const int per = (n16 + FR_T - 1) / FR_T;      // <= 16 for S <= 32
+    double2 hold[16];
+    auto fetch = [&](int it) {
+      const int64_t e0 = (tile0 + (int64_t)it * RC) * S;   // first double of the chunk
+      const int64_t eend = B * S;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (q >= per) break;
+        const int piece = q * FR_T + tid;
+        const int64_t e = e0 + 2 * (int64_t)piece;
+        if (piece < n16 && e + 1 < eend) {
+          hold[q] = *reinterpret_cast<const double2*>(x + e);
+        } else if (piece < n16 && e < eend) {
+          hold[q] = double2{x[e], 0.0};
+        }
       }
-      if (finish(s) <= eps && ok(b)) atomicOr(&tbits[loc >> 5], 1u << (loc & 31));
+    };
+    auto stash = [&]() {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (q >= per) break;
+        const int piece = q * FR_T + tid;
+        if (piece < n16) {
+          const int e = 2 * piece;
+          const int r0 = e / S, k0 = e - r0 * S;
+          pa_rows[r0 * S1 + k0] = hold[q].x;
+          const int r1 = (e + 1) / S, k1 = e + 1 - r1 * S;
+          pa_rows[r1 * S1 + k1] = hold[q].y;
+        }
+      }
+    };
+    const int64_t rows = B - tile0 < FR_TILE ? B - tile0 : FR_TILE;
+    const int nchunk = (int)((rows + RC - 1) / RC);
+    fetch(0);
+#pragma unroll 1
+    for (int it = 0; it < nchunk; ++it) {
+      __syncthreads();                 // the previous chunk's rows are read
+      stash();
+      __syncthreads();
+      if (it + 1 < nchunk) fetch(it + 1);
+      const int loc = it * RC + tid;
+      const int64_t b = tile0 + loc;
+      if (tid < RC && loc < FR_TILE && b < B) {
+        const double* xr = pa_rows + tid * S1;
+        double s = 0.0;
+        if (inf) {
+          for (int k = 0; k < S; ++k) s = fmax(s, fabs(wf[k] * (xr[k] - x0[k])));
+        } else {
+          for (int k = 0; k < S; ++k) s += pterm(fabs(wf[k] * (xr[k] - x0[k])), p);
+        }
+        if (finish(s) <= eps && ok(b)) atomicOr(&tbits[loc >> 5], 1u << (loc & 31));
+      }
     }
   } else {
     // wave w takes rows w * PA_ROWS + 4 PA_ROWS i of the tile
@@ -765,8 +805,9 @@ extern "C" int abc_pnorm_accept(const double* x, int64_t B, int S, const double*
   if (!c.ok) return set_error(ABC_ERR_WORKSPACE, "pnorm_accept: workspace");
   // the same row / wave split as abc_pnorm (the same bits per row)
   if (S <= 32)
-    hipLaunchKernelGGL(pnorm_accept_kernel<false>, dim3((unsigned)nt), dim3(FR_T), 0, s, x, B,
-                       S, x0, wf, p, eps, attempts, max_attempts, bits, tcnt);
+    hipLaunchKernelGGL(pnorm_accept_kernel<false>, dim3((unsigned)nt), dim3(FR_T),
+                       (size_t)pa_chunk_rows(S) * (S + 1) * sizeof(double), s, x, B, S, x0, wf, p, eps,
+                       attempts, max_attempts, bits, tcnt);
   else
     hipLaunchKernelGGL(pnorm_accept_kernel<true>, dim3((unsigned)nt), dim3(FR_T), 0, s, x, B,
                        S, x0, wf, p, eps, attempts, max_attempts, bits, tcnt);
@@ -784,7 +825,7 @@ extern "C" int abc_candidates_propose(const abc_candidate_spec* spec, int64_t id
   if (rc != ABC_OK) return rc;
   ABC_CHECK_ARG(B >= 0 && B < (1ll << 40), "candidates_propose: bad B");
   if (B == 0) return ABC_OK;
-  ABC_CHECK_ARG(theta && prior_logpdf, "candidates_propose: null pointer");
+  ABC_CHECK_ARG(theta, "candidates_propose: null pointer");
   if (ws_bytes < abc_candidates_propose_workspace())
     return set_error(ABC_ERR_WORKSPACE, "candidates_propose: workspace too small");
   hipStream_t s = as_stream(stream);

@@ -375,17 +375,17 @@ class CandidateRound:
                  p(ws), ws.numel(), stream_ptr())
         return idx, cnt
 
-    def propose(self, idx0, B):
+    def propose(self, idx0, B, with_lp=True):
         """Proposals of candidates idx0 .. idx0 + B - 1 only
-        (abc_candidates_propose): theta [B, d], prior log-density [B],
-        ancestor [B] (int64), attempts [B] (int32) -- the rows gpu.propose
-        returns, through the round's proposal (ancestor table, support box
-        computed once)."""
+        (abc_candidates_propose): theta [B, d], prior log-density [B] (None
+        unless with_lp), ancestor [B] (int64), attempts [B] (int32) -- the
+        rows gpu.propose returns, through the round's proposal (ancestor
+        table, support box computed once)."""
         import ctypes as C
         dev = self.device
         B = int(B)
         theta = torch.empty((B, self.d), dtype=F64, device=dev)
-        lp = torch.empty(B, dtype=F64, device=dev)
+        lp = torch.empty(B, dtype=F64, device=dev) if with_lp else None
         anc = torch.empty(B, dtype=I64, device=dev)
         att = torch.empty(B, dtype=torch.int32, device=dev)
         if B:

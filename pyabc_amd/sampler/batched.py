@@ -329,16 +329,25 @@ class BatchedGPUSampler(Sampler):
             rec_rows = int(rec_all[rank])
             if k_mine:
                 sel = idx[:k_mine]
+                lp_cols = [lp] if lp is not None else []
                 if dist is None:
                     # the tail kept no distances: the kept rows' ones, the
                     # same per-row arithmetic (abc_pnorm)
-                    cols = [theta, lp, x] + ([anc] if anc is not None else [])
+                    cols = [theta] + lp_cols + [x] + ([anc] if anc is not None else [])
                     got = gpu.gather_rows_batch(cols, sel)
+                    if lp is None:
+                        got.insert(1, None)
                     got.insert(2, gpu.pnorm(got[2], spec.x0vec, *pnorm_tail))
                 else:
-                    cols = [theta, lp, dist, x] + ([anc] if anc is not None else []) \
-                        + ([accw] if stochastic else [])
+                    cols = [theta] + lp_cols + [dist, x] + \
+                        ([anc] if anc is not None else []) + ([accw] if stochastic else [])
                     got = gpu.gather_rows_batch(cols, sel)   # one launch
+                    if lp is None:
+                        got.insert(1, None)
+                if got[1] is None:
+                    # kept rows only (never a gave-up proposal): the bits the
+                    # proposal kernel would have written (same device function)
+                    got[1] = gpu.prior_logpdf(got[0], spec.prior_kind, spec.prior_params)
                 acc_theta.append(got[0])
                 acc_lp.append(got[1])
                 acc_d.append(got[2])
@@ -758,7 +767,8 @@ class BatchedGPUSampler(Sampler):
         if not (spec.transition is None and getattr(spec, "host_prior", None)):
             fr = self._proposal_round(spec, seed, gen, gpu.require_device())
         if fr is not None:
-            th, lp, anc, att = fr.propose(lo, B)
+            # the prior log-density only for the rows kept (_keep_lp)
+            th, lp, anc, att = fr.propose(lo, B, with_lp=False)
             return th, lp, (anc if spec.transition is not None else None), att
         if spec.transition is None:
             th, lp, _, att = gpu.propose(None, None, None, spec.prior_kind,
