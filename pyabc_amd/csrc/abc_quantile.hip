@@ -41,7 +41,8 @@ namespace {
 constexpr int WQ_T = 1024;
 constexpr int WQ_BITS = 12, WQ_NB = 1 << WQ_BITS;
 constexpr int WQ_CAP = 2048;
-constexpr int WQ_MAXB = 64;
+constexpr int WQ_MAXB = 256;
+static_assert(WQ_MAXB <= WQ_T, "wq_final_kernel sums one gather block per thread");
 
 typedef unsigned long long u64;
 
@@ -113,8 +114,16 @@ __device__ __forceinline__ int span_shift(u64 lo, u64 hi) {
 __global__ __launch_bounds__(WQ_T) void wq_range_kernel(const double* __restrict__ x,
                                                         const double* __restrict__ w,
                                                         int64_t N, int64_t chunk,
-                                                        WqPart* __restrict__ part) {
+                                                        WqPart* __restrict__ part,
+                                                        unsigned int* __restrict__ ghc,
+                                                        u64* __restrict__ ghw) {
   __shared__ u64 sh[WQ_T / 64];
+  // zero both levels' global histograms (the hist kernels add into them)
+  for (int64_t e = (int64_t)blockIdx.x * WQ_T + threadIdx.x; e < 2 * WQ_NB;
+       e += (int64_t)gridDim.x * WQ_T) {
+    ghc[e] = 0u;
+    ghw[e] = 0ull;
+  }
   const int64_t b0 = (int64_t)blockIdx.x * chunk;
   const int64_t b1 = b0 + chunk < N ? b0 + chunk : N;
   u64 mn = ~0ull, mx = 0ull, wm = 0ull;
@@ -130,7 +139,13 @@ __global__ __launch_bounds__(WQ_T) void wq_range_kernel(const double* __restrict
   mn = block_reduce(mn, sh, umin);
   mx = block_reduce(mx, sh, umax);
   wm = block_reduce(wm, sh, umax);
-  if (threadIdx.x == 0) part[blockIdx.x] = WqPart{mn, mx, wm};
+  // one global range: integer min / max atomics (order-free), initialised
+  // by the launcher's memsets
+  if (threadIdx.x == 0) {
+    atomicMin(reinterpret_cast<unsigned long long*>(&part->kmin), (unsigned long long)mn);
+    atomicMax(reinterpret_cast<unsigned long long*>(&part->kmax), (unsigned long long)mx);
+    atomicMax(reinterpret_cast<unsigned long long*>(&part->wmax), (unsigned long long)wm);
+  }
 }
 
 // ---- 2. histogram of one level ----------------------------------------------
@@ -158,9 +173,13 @@ __global__ __launch_bounds__(WQ_T) void wq_hist_kernel(
     atomicAdd(&ws[bin], wfix(w[i], R.S));
   }
   __syncthreads();
+  // into the level's global histogram: integer atomics, so the totals do
+  // not depend on the blocks' order
   for (int b = threadIdx.x; b < WQ_NB; b += WQ_T) {
-    ghc[(int64_t)blockIdx.x * WQ_NB + b] = cnt[b];
-    ghw[(int64_t)blockIdx.x * WQ_NB + b] = ws[b];
+    if (cnt[b]) {
+      atomicAdd(&ghc[b], cnt[b]);
+      atomicAdd(reinterpret_cast<unsigned long long*>(&ghw[b]), (unsigned long long)ws[b]);
+    }
   }
 }
 
@@ -237,6 +256,7 @@ __global__ __launch_bounds__(WQ_T) void wq_pick_kernel(
     int64_t N, double alpha, const WqPart* __restrict__ part, int nblk,
     const unsigned int* __restrict__ ghc, const u64* __restrict__ ghw, int nhb,
     const WqDesc* __restrict__ prev, WqDesc* __restrict__ out, unsigned int* __restrict__ list_n) {
+  (void)nhb;   // one global histogram per level (integer atomics in wq_hist_kernel)
   if (prev && prev->ok) {
     if (threadIdx.x == 0) *out = *prev;
     return;
@@ -248,12 +268,8 @@ __global__ __launch_bounds__(WQ_T) void wq_pick_kernel(
   const Range R = wq_global_range(part, nblk, N);
   u64 tw = 0ull;
   for (int b = threadIdx.x; b < WQ_NB; b += WQ_T) {
-    unsigned int c = 0u;
-    u64 sm = 0ull;
-    for (int k = 0; k < nhb; ++k) {
-      c += ghc[(int64_t)k * WQ_NB + b];
-      sm += ghw[(int64_t)k * WQ_NB + b];
-    }
+    const unsigned int c = ghc[b];
+    const u64 sm = ghw[b];
     cnt[b] = c;
     wsum[b] = sm;
     tw += sm;
@@ -362,8 +378,27 @@ __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
     if (t == 0) *q = NAN;
     return;
   }
-  double below = 0.0, total = 0.0;
-  for (int b = 0; b < nsum; ++b) { below += psum[2 * b]; total += psum[2 * b + 1]; }
+  // the gather blocks' fp64 sums: a fixed tree (lanes, then waves in order)
+  __shared__ double s_bt[2][WQ_T / 64];
+  __shared__ double s_below, s_total;
+  {
+    double bl = t < nsum ? psum[2 * t] : 0.0, al = t < nsum ? psum[2 * t + 1] : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      bl += __shfl_xor(bl, o, 64);
+      al += __shfl_xor(al, o, 64);
+    }
+    if ((t & 63) == 0) { s_bt[0][t >> 6] = bl; s_bt[1][t >> 6] = al; }
+    __syncthreads();
+    if (t == 0) {
+      double b2 = 0.0, a2 = 0.0;
+      for (int i = 0; i < WQ_T / 64; ++i) { b2 += s_bt[0][i]; a2 += s_bt[1][i]; }
+      s_below = b2;
+      s_total = a2;
+    }
+    __syncthreads();
+  }
+  const double below = s_below, total = s_total;
   const int m = (int)D.count;
   int M = 1;
   while (M < m) M <<= 1;
@@ -424,7 +459,7 @@ __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
 }
 
 int wq_blocks(int64_t N) {
-  const int64_t b = ceil_div(N, 16384);
+  const int64_t b = ceil_div(N, 4096);
   return (int)(b < 1 ? 1 : (b > WQ_MAXB ? WQ_MAXB : b));
 }
 
@@ -436,9 +471,9 @@ using namespace abc;
 extern "C" size_t abc_weighted_quantile_workspace(int64_t N) {
   const int nb = wq_blocks(N > 0 ? N : 1);
   size_t off = 0;
-  size_only<WqPart>(off, (size_t)nb);
-  size_only<unsigned int>(off, (size_t)nb * WQ_NB);
-  size_only<u64>(off, (size_t)nb * WQ_NB);
+  size_only<WqPart>(off, 1);
+  size_only<unsigned int>(off, (size_t)2 * WQ_NB);
+  size_only<u64>(off, (size_t)2 * WQ_NB);
   size_only<WqDesc>(off, 2);
   size_only<u64>(off, WQ_CAP);
   size_only<int>(off, WQ_CAP);
@@ -459,9 +494,9 @@ extern "C" int abc_weighted_quantile(const double* points, const double* w, int6
   const int nb = wq_blocks(N);
   const int64_t chunk = ceil_div(N, nb);
   Carver cv(ws, ws_bytes);
-  WqPart* part = cv.take<WqPart>((size_t)nb);
-  unsigned int* ghc = cv.take<unsigned int>((size_t)nb * WQ_NB);
-  u64* ghw = cv.take<u64>((size_t)nb * WQ_NB);
+  WqPart* part = cv.take<WqPart>(1);
+  unsigned int* ghc = cv.take<unsigned int>((size_t)2 * WQ_NB);   // level 1 | level 2
+  u64* ghw = cv.take<u64>((size_t)2 * WQ_NB);
   WqDesc* desc = cv.take<WqDesc>(2);
   u64* lkey = cv.take<u64>(WQ_CAP);
   int* lidx = cv.take<int>(WQ_CAP);
@@ -469,19 +504,22 @@ extern "C" int abc_weighted_quantile(const double* points, const double* w, int6
   unsigned int* list_n = cv.take<unsigned int>(4);   // [0]: count; [2..3]: total (fixed)
   double* psum = cv.take<double>((size_t)2 * nb);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "quantile: carve");
-  hipLaunchKernelGGL(wq_range_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, part);
+  ABC_HIP(hipMemsetAsync(&part->kmin, 0xFF, sizeof(u64), s));
+  ABC_HIP(hipMemsetAsync(&part->kmax, 0, 2 * sizeof(u64), s));
+  hipLaunchKernelGGL(wq_range_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, part,
+                     ghc, ghw);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_hist_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, part, nb,
+  hipLaunchKernelGGL(wq_hist_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, part, 1,
                      (const WqDesc*)nullptr, ghc, ghw);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_pick_kernel, dim3(1), dim3(WQ_T), 0, s, N, alpha, part, nb, ghc, ghw, nb,
+  hipLaunchKernelGGL(wq_pick_kernel, dim3(1), dim3(WQ_T), 0, s, N, alpha, part, 1, ghc, ghw, 1,
                      (const WqDesc*)nullptr, desc, list_n);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_hist_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, part, nb,
-                     (const WqDesc*)desc, ghc, ghw);
+  hipLaunchKernelGGL(wq_hist_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, part, 1,
+                     (const WqDesc*)desc, ghc + WQ_NB, ghw + WQ_NB);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_pick_kernel, dim3(1), dim3(WQ_T), 0, s, N, alpha, part, nb, ghc, ghw, nb,
-                     (const WqDesc*)desc, desc + 1, list_n);
+  hipLaunchKernelGGL(wq_pick_kernel, dim3(1), dim3(WQ_T), 0, s, N, alpha, part, 1,
+                     ghc + WQ_NB, ghw + WQ_NB, 1, (const WqDesc*)desc, desc + 1, list_n);
   ABC_LAUNCHED();
   hipLaunchKernelGGL(wq_gather_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk,
                      (const WqDesc*)(desc + 1), lkey, lidx, lw, list_n, psum);
