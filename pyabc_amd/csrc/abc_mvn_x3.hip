@@ -632,6 +632,10 @@ __global__ void x3_scatter_rescued(const int64_t* __restrict__ rescue, int64_t n
   if (q < n) out[rescue[q]] = outs[q];
 }
 
+// candidate tiles per wave for KB MFMA blocks, as dispatch_x3 instantiates
+// them (KB = 3: 10, A/B 8 -> 10 -1.2% at c3; 4 / 5 / 6 / 12 slower)
+__host__ __device__ constexpr int x3_ct(int KB) { return KB == 3 ? 10 : (KB == 2 ? 8 : 4); }
+
 struct PlanX3 {
   int KB0, KB, CT, nchunk;
   int64_t MT, NT, MTpad, groups, tiles_per_chunk, Mpad;
@@ -641,7 +645,7 @@ PlanX3 make_plan_x3(int64_t M, int64_t N, int r) {
   PlanX3 p;
   p.KB0 = x3_kb0(r);
   p.KB = p.KB0 + x3_kb12(r);
-  p.CT = p.KB <= 3 ? 8 : 4;
+  p.CT = x3_ct(p.KB);
   p.MT = ceil_div(M > 0 ? M : 1, 16);
   p.NT = ceil_div(N > 0 ? N : 1, 16);
   const int64_t waves = ceil_div(p.MT, p.CT);
@@ -674,6 +678,7 @@ size_t plan_x3_ws(const PlanX3& p) {
 template <int KB, int CT>
 void launch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
                double* po, double* pl, bool pass1, hipStream_t s) {
+  static_assert(CT == x3_ct(KB), "the plan's tiles per wave must match the instantiation");
   const int64_t blocks = p.groups * p.nchunk;
   if (pass1)
     hipLaunchKernelGGL((mvn_x3_kernel<KB, CT, true>), dim3((unsigned)blocks),
@@ -689,7 +694,7 @@ int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
                 double* po, double* pl, bool pass1, hipStream_t s) {
   switch (p.KB) {
     case 2: launch_x3<2, 8>(p, A, B, koff, po, pl, pass1, s); break;
-    case 3: launch_x3<3, 8>(p, A, B, koff, po, pl, pass1, s); break;
+    case 3: launch_x3<3, 10>(p, A, B, koff, po, pl, pass1, s); break;
     case 4: launch_x3<4, 4>(p, A, B, koff, po, pl, pass1, s); break;
     case 5: launch_x3<5, 4>(p, A, B, koff, po, pl, pass1, s); break;
     case 6: launch_x3<6, 4>(p, A, B, koff, po, pl, pass1, s); break;

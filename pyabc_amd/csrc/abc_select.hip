@@ -72,16 +72,19 @@ struct SelShared {
   int64_t below1;
 };
 
-// ascending bitonic sort of sh.smp (SMP = 2 x blockDim keys)
+// ascending bitonic sort of sh.smp (SMP keys, SMP / 2 compare-exchange
+// pairs per stage spread over the block)
 __device__ void sort_sample(SelShared& sh) {
-  const int t = threadIdx.x;
+  static_assert(SMP % (2 * SEL_T) == 0, "whole pair sets per thread");
   for (int size = 2; size <= SMP; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const int i = 2 * t - (t & (stride - 1));
-      const int j = i + stride;
-      const bool asc = (i & size) == 0;
-      const uint64_t a = sh.smp[i], b = sh.smp[j];
-      if ((a > b) == asc) { sh.smp[i] = b; sh.smp[j] = a; }
+      for (int pidx = threadIdx.x; pidx < SMP / 2; pidx += SEL_T) {
+        const int i = 2 * pidx - (pidx & (stride - 1));
+        const int j = i + stride;
+        const bool asc = (i & size) == 0;
+        const uint64_t a = sh.smp[i], b = sh.smp[j];
+        if ((a > b) == asc) { sh.smp[i] = b; sh.smp[j] = a; }
+      }
       __syncthreads();
     }
   }
