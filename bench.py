@@ -328,7 +328,7 @@ def measured_traffic(args, n_pop, kernel):
         except (OSError, ValueError):
             continue
         if (t.get("population") == n_pop and t.get("d") == args.dim
-                and kernel + "I" in t.get("kernel_name", "")):
+                and kernel in t.get("kernel_name", "")):
             return t["traffic_bytes"], os.path.relpath(f, ROOT)
     return None, None
 
@@ -402,7 +402,7 @@ def main():
     peak = F64_MFMA_PEAK_TFLOPS if args.precision == "f64" else F32_MFMA_PEAK_TFLOPS
     # executed K per pair and the kernel, as the library reports them
     from pyabc_amd import gpu
-    _, x3_k = gpu.mvn_x3_layout(args.dim) if args.precision == "x3" else (0, 0)
+    _, x3_k, x3_ct = gpu.mvn_x3_layout(args.dim) if args.precision == "x3" else (0, 0, 0)
     kpad = {"x3": x3_k,
             "f64": 4 * math.ceil((args.dim + 1) / 4),
             "f32": 4 * math.ceil((args.dim + 1) / 4)}[args.precision]
@@ -413,7 +413,9 @@ def main():
                     "operands, exact-grid f32 accumulation + exp2 + sum)"),
              "f64": "mvn_lse_kernel<double> (f64 MFMA cross term + exp2 + LSE)",
              "f32": "mvn_lse_kernel<float> (f32 MFMA cross term + exp2 + LSE)"}
-    traffic, traffic_src = measured_traffic(args, n_pop, "mvn_x3_kernel")
+    # the main (hinted) instantiation, mvn_x3_kernel<KB, CT, false>
+    traffic, traffic_src = measured_traffic(
+        args, n_pop, f"mvn_x3_kernelILi{x3_k // 32}ELi{x3_ct}ELb0E")
     # per-stage split of the timed region (HIP events on the launch streams)
     c_ms, c_n = timer.channels["candidates"]
     r_ms, r_n = timer.channels["regen"]

@@ -137,10 +137,12 @@ int abc_mvn_pack_population(const double* X, const double* w, int64_t N, int d,
                             double* range, void* stream);
 size_t abc_mvn_logpdf_workspace(int64_t M, int64_t N, int r, int prec);
 /* K slots the X3 kernel executes per (candidate, population row) pair at
- * whitened rank r (the f16 MFMA work per pair is 2 K FLOP), and the kernel it
- * runs (0 = mvn_x3_kernel, K = 32 x MFMA blocks).
- * A layout query for reporting; no device work. */
-int abc_mvn_x3_layout(int r, int* kslots);
+ * whitened rank r (the f16 MFMA work per pair is 2 K FLOP; K = 32 x MFMA
+ * blocks) and its candidate tiles per wave (nullable outputs); returns the
+ * kernel (0 = mvn_x3_kernel<K / 32, tiles>).  A layout query for reporting
+ * (bench.py names the instantiation its traffic file must match); no device
+ * work. */
+int abc_mvn_x3_layout(int r, int* kslots, int* tiles_per_wave);
 int abc_mvn_logpdf(const double* x, int64_t M, int d, const void* packed,
                    const double* X, const double* w, int64_t N,
                    const double* mu, const double* U, int r, int prec,

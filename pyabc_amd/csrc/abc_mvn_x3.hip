@@ -726,8 +726,10 @@ size_t x3_packed_bytes(int64_t N, int r) {
 
 int x3_max_rank() { return MAX_R; }
 
-extern "C" int abc_mvn_x3_layout(int r, int* kslots) {
-  if (kslots) *kslots = 32 * (x3_kb0(r) + x3_kb12(r));
+extern "C" int abc_mvn_x3_layout(int r, int* kslots, int* tiles_per_wave) {
+  const int KB = x3_kb0(r) + x3_kb12(r);
+  if (kslots) *kslots = 32 * KB;
+  if (tiles_per_wave) *tiles_per_wave = x3_ct(KB);
   return 0;
 }
 

@@ -184,12 +184,12 @@ def mvn_logpdf(x, packed, N, mu, U, prec, log_const, out=None, X=None, w=None,
 
 
 def mvn_x3_layout(r):
-    """(kernel, K slots per pair) the x3 density runs at whitened rank r
-    (kernel 0 = mvn_x3_kernel, K = 32 x MFMA blocks)."""
+    """(kernel, K slots per pair, candidate tiles per wave) the x3 density
+    runs at whitened rank r (kernel 0 = mvn_x3_kernel<K / 32, tiles>)."""
     import ctypes
-    k = ctypes.c_int(0)
-    kernel = int(nat.load().abc_mvn_x3_layout(int(r), ctypes.byref(k)))
-    return kernel, int(k.value)
+    k, ct = ctypes.c_int(0), ctypes.c_int(0)
+    kernel = int(nat.load().abc_mvn_x3_layout(int(r), ctypes.byref(k), ctypes.byref(ct)))
+    return kernel, int(k.value), int(ct.value)
 
 
 def mvn_logpdf_direct(x, X, w, U, V, support_tol, log_const, out=None):
