@@ -1049,10 +1049,15 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const double* __restrict
       for (int y = 0; y < RS; ++y) c += part[((int64_t)y * NCP + f * ML_NL + l) * N + n];
       v += ldexp(c, e - 11 * (l + 1));
     }
-    if (extra) v += extra[(int64_t)f * N + n];   // deferred collect: queued members
+    double eq = 0.0;
+    if (extra) {   // deferred collect: the queued members' fp64 sum and its bound
+      v += extra[(int64_t)f * N + n];
+      eq = MM_EPS * extra[(int64_t)(NM + f) * N + n];
+    }
     S[f] = v;
-    // last-limb rounding per member + the limb sum's own rounding
-    E[f] = (double)nq * ldexp(1.0, e - 11 * ML_NL - 1) + 4.0 * MM_EPS * fabs(v);
+    // last-limb rounding per member + the limb sum's own rounding (+ the
+    // queued members' sum)
+    E[f] = (double)nq * ldexp(1.0, e - 11 * ML_NL - 1) + 4.0 * MM_EPS * fabs(v) + eq;
   }
   double yn[D];
   for (int a = 0; a < D; ++a) yn[a] = X[n * D + a] - X[a];
@@ -1191,7 +1196,9 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   }
   const bool all_listed = list_ok && h_cnt[1] == N;
   const int RS = N > 1 ? moments_chunks(N) : 1;
-  double* part = cv.take<double>(all_listed ? 1 : (size_t)RS * NM * (size_t)N);
+  // (>= 2 NM N: the dense path's deferred collect keeps its member sums and
+  // their rounding bounds there)
+  double* part = cv.take<double>(all_listed ? 1 : (size_t)(RS < 2 ? 2 : RS) * NM * (size_t)N);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
   const double* mom = part;
   int mom_rs = RS;
@@ -1583,7 +1590,10 @@ extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
   size_only<double>(off, 1);                                     // max |X|
   // partial moments of the row chunks (local_moments_kernel)
   const size_t nm = 2 + (size_t)d + (size_t)d * (d + 1) / 2;
-  size_only<double>(off, (size_t)moments_chunks(N > 1 ? N : 1) * nm * (size_t)(N > 0 ? N : 1));
+  {
+    const int rs = moments_chunks(N > 1 ? N : 1);
+    size_only<double>(off, (size_t)(rs < 2 ? 2 : rs) * nm * (size_t)(N > 0 ? N : 1));
+  }
   {  // fp32-MFMA k-NN select (abc_local_knn.h)
     const int64_t n1 = N > 0 ? N : 1;
     const int64_t nt = (n1 + 15) / 16;

@@ -395,15 +395,22 @@ __global__ __launch_bounds__(256) void knn_resolve_kernel(
     if (mem[i]) s_ord[wv][pos[i]] = jj[i];
   __syncthreads();
   constexpr int NM = local_nm<D>();
-  double sum = 0.0;
+  double sum = 0.0, sabs = 0.0;
   if (ok && lane < NM)
     for (int q = 0; q < nmem; ++q) {
       const int j = s_ord[wv][q];
       double y[D];
 #pragma unroll
       for (int a = 0; a < D; ++a) y[a] = X[(int64_t)j * D + a] - X[a];
-      sum += mm_feature<D>(lane, w[j], y);
+      const double f = mm_feature<D>(lane, w[j], y);
+      sum += f;
+      sabs += fabs(f);
     }
-  if (ok && lane < NM) extra[(int64_t)lane * N + n] = sum;
+  // the sum and its rounding bound: a sequential fp64 sum of nmem terms is
+  // off by at most (nmem - 1) u sum |f| (mm_finish_kernel adds eps x this)
+  if (ok && lane < NM) {
+    extra[(int64_t)lane * N + n] = sum;
+    extra[(int64_t)(NM + lane) * N + n] = (double)nmem * sabs;
+  }
   (void)bnd; (void)part;
 }
