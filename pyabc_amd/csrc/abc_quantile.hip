@@ -42,7 +42,8 @@ constexpr int WQ_T = 1024;
 constexpr int WQ_BITS = 12, WQ_NB = 1 << WQ_BITS;
 constexpr int WQ_CAP = 2048;
 constexpr int WQ_MAXB = 256;
-static_assert(WQ_MAXB <= WQ_T, "wq_final_kernel sums one gather block per thread");
+constexpr int WQ_FT = 1024;  // threads of the final (single-block) kernel (256: 54 vs 35 us)
+static_assert(WQ_MAXB <= WQ_FT, "wq_final_kernel sums one gather block per thread");
 
 typedef unsigned long long u64;
 
@@ -363,7 +364,7 @@ __device__ __forceinline__ bool kless(u64 ka, int ia, u64 kb, int ib) {
   return ka < kb || (ka == kb && ia < ib);
 }
 
-__global__ __launch_bounds__(WQ_T) void wq_final_kernel(
+__global__ __launch_bounds__(WQ_FT) void wq_final_kernel(
     int64_t N, double alpha, const WqDesc* __restrict__ desc,
     const u64* __restrict__ gkey, const int* __restrict__ gidx, const double* __restrict__ gw,
     const double* __restrict__ psum, int nsum, double* __restrict__ q) {
@@ -371,7 +372,7 @@ __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
   __shared__ int sidx[WQ_CAP];
   __shared__ double sw[WQ_CAP];
   __shared__ Knot kn[WQ_CAP];
-  __shared__ double dsh[WQ_T / 64];
+  __shared__ double dsh[WQ_FT / 64];
   const int t = threadIdx.x;
   const WqDesc D = *desc;
   if (!D.ok) {   // the knots sit in more than WQ_CAP points (ties): not decided
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
     return;
   }
   // the gather blocks' fp64 sums: a fixed tree (lanes, then waves in order)
-  __shared__ double s_bt[2][WQ_T / 64];
+  __shared__ double s_bt[2][WQ_FT / 64];
   __shared__ double s_below, s_total;
   {
     double bl = t < nsum ? psum[2 * t] : 0.0, al = t < nsum ? psum[2 * t + 1] : 0.0;
@@ -392,7 +393,7 @@ __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
     __syncthreads();
     if (t == 0) {
       double b2 = 0.0, a2 = 0.0;
-      for (int i = 0; i < WQ_T / 64; ++i) { b2 += s_bt[0][i]; a2 += s_bt[1][i]; }
+      for (int i = 0; i < WQ_FT / 64; ++i) { b2 += s_bt[0][i]; a2 += s_bt[1][i]; }
       s_below = b2;
       s_total = a2;
     }
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
   const int m = (int)D.count;
   int M = 1;
   while (M < m) M <<= 1;
-  for (int i = t; i < M; i += WQ_T) {
+  for (int i = t; i < M; i += WQ_FT) {
     const bool in = i < m;
     skey[i] = in ? gkey[i] : ~0ull;
     sidx[i] = in ? gidx[i] : 0x7FFFFFFF;
@@ -412,7 +413,7 @@ __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
   // bitonic sort by (key, index): the stable order of the reference's sort
   for (int size = 2; size <= M; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = t; i < M; i += WQ_T) {
+      for (int i = t; i < M; i += WQ_FT) {
         const int jx = i ^ stride;
         if (jx > i) {
           const bool asc = (i & size) == 0;
@@ -429,7 +430,7 @@ __global__ __launch_bounds__(WQ_T) void wq_final_kernel(
   // cumulative weights: the fp64 sum below + an inclusive prefix in a fixed
   // order (each thread a run of consecutive elements, then the thread sums)
   {
-    const int per = (m + WQ_T - 1) / WQ_T;
+    const int per = (m + WQ_FT - 1) / WQ_FT;
     const int i0 = t * per;
     double sum = 0.0;
     for (int k = 0; k < per && i0 + k < m; ++k) sum += sw[i0 + k];
@@ -524,7 +525,7 @@ extern "C" int abc_weighted_quantile(const double* points, const double* w, int6
   hipLaunchKernelGGL(wq_gather_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk,
                      (const WqDesc*)(desc + 1), lkey, lidx, lw, list_n, psum);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_final_kernel, dim3(1), dim3(WQ_T), 0, s, N, alpha,
+  hipLaunchKernelGGL(wq_final_kernel, dim3(1), dim3(WQ_FT), 0, s, N, alpha,
                      (const WqDesc*)(desc + 1), lkey, lidx, lw, psum, nb, q);
   ABC_LAUNCHED();
   return ABC_OK;
