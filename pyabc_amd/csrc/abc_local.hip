@@ -1598,7 +1598,7 @@ extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
     const int64_t n1 = N > 0 ? N : 1;
     const int64_t nt = (n1 + 15) / 16;
     size_only<double>(off, (size_t)d);
-    size_only<float>(off, (size_t)(nt + 32) * ((d + 5) / 4) * 64);
+    size_only<float>(off, (size_t)(nt + 8 * KN_PF) * ((d + 5) / 4) * 64);   // + prefetch padding
     size_only<unsigned long long>(off, 1);
     size_only<int>(off, (size_t)n1);
     size_only<int>(off, (size_t)n1);

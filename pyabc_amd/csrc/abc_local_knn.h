@@ -51,7 +51,7 @@ constexpr int KN_SK = 512;   // sample rows
 constexpr int KN_NB = 520;   // window bins
 constexpr int KN_CAP = 192;  // list entries per particle (LDS: 4 blocks per CU)
 constexpr int KN_MARGIN = 32;
-constexpr int KN_PF = 4;     // row-tile groups in flight per sweep (kn_sweep)
+constexpr int KN_PF = 2;     // row-tile groups in flight per sweep (kn_sweep; A/B: 2 best, 1 / 3 / 4 / 6 slower)
 constexpr int KN_MIN_N = 4 * KN_SK;
 constexpr int KN_QCAP = 256; // open pairs per particle queued by the deferred collect
 typedef float knf4 __attribute__((ext_vector_type(4)));
