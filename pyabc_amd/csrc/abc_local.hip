@@ -1525,7 +1525,7 @@ size_t pdf_workspace(int64_t M, int64_t N, int* nchunks_out) {
   const int64_t ntiles = ceil_div(N, 16);
   const int64_t cblocks = ceil_div(M > 0 ? M : 1, 4 * LocalFeat<D>::NT * 16);
   // enough workgroups for 256 CUs x several waves, chunks of >= 64 tiles
-  int64_t nch = ceil_div(2048, cblocks);
+  int64_t nch = ceil_div(4096, cblocks);   // ~4096 blocks (A/B at c5: 2048 -> 4096 10.0 -> 9.2 ms; 1024, 8192, 16384 slower)
   nch = nch < 1 ? 1 : nch;
   const int64_t maxch = ceil_div(ntiles, 64);
   nch = nch > maxch ? maxch : nch;
