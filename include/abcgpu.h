@@ -37,6 +37,12 @@ extern "C" {
 #define ABC_ERR_UNSUPPORTED (-5)
 #define ABC_ERR_COMM (-6)      /* RCCL missing or a collective failed */
 
+/* Largest parameter dimension d the proposal, prior-density and
+ * LocalTransition entry points accept (one cap for all of them; the
+ * runtime-d LocalTransition fit stages a member row of d + 1 doubles in LDS,
+ * abc_local_wide.hip).  The fused candidate round takes d <= 64. */
+#define ABC_MAX_D 2048
+
 /* Precision of the transition-density kernel. */
 #define ABC_PREC_F64 0 /* f64 MFMA cross term: parity mode (default)   */
 #define ABC_PREC_F32 1 /* f32 MFMA cross term: fast mode (~3e-5 rel.)  */

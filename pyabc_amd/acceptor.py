@@ -1,3 +1,5 @@
+# Adapted from pyABC (https://github.com/ICB-DCM/pyABC), BSD-3-Clause,
+# Copyright 2017 the pyABC developers -- see NOTICE at the repository root.
 """Acceptors (pyabc/acceptor/acceptor.py:32-476, pdf_norm.py:1-110).
 
 UniformAcceptor ``d <= eps(t)``: the batched sampler applies the same test on

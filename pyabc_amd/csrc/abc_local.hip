@@ -1152,7 +1152,7 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
   int* knn_cnt = nullptr;
   float* knn_img = nullptr;
   if (knn) {
-    const int64_t nt = ceil_div(N, 16) + 8 * KN_PF;   // + prefetch padding
+    const int64_t nt = ceil_div(N, 16) + KN_PAD;   // + prefetch padding
     cen = cv.take<double>(D);
     float* img = cv.take<float>((size_t)nt * kn_kb<D>() * 64);
     r2 = cv.take<unsigned long long>(1);
@@ -1598,7 +1598,7 @@ extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
     const int64_t n1 = N > 0 ? N : 1;
     const int64_t nt = (n1 + 15) / 16;
     size_only<double>(off, (size_t)d);
-    size_only<float>(off, (size_t)(nt + 8 * KN_PF) * ((d + 5) / 4) * 64);   // + prefetch padding
+    size_only<float>(off, (size_t)(nt + KN_PAD) * ((d + 5) / 4) * 64);   // + prefetch padding
     size_only<unsigned long long>(off, 1);
     size_only<int>(off, (size_t)n1);
     size_only<int>(off, (size_t)n1);
@@ -1627,7 +1627,7 @@ extern "C" int abc_local_fit(const double* X, const double* w, int64_t N,
                              double* covs, double* inv_covs, double* dets,
                              double* chol, double* log_norm, void* ws,
                              size_t ws_bytes, void* stream) {
-  ABC_CHECK_ARG(N >= 1 && d >= 1 && k >= 1, "local_fit: bad N/d/k");
+  ABC_CHECK_ARG(N >= 1 && d >= 1 && d <= ABC_MAX_D && k >= 1, "local_fit: bad N/d/k");
   ABC_CHECK_ARG(N < (1ll << 31), "local_fit: N >= 2^31");
   ABC_CHECK_ARG(ws && ws_bytes >= abc_local_fit_workspace(N, d), "local_fit: workspace");
   ABC_CHECK_ARG(X && w && covs && inv_covs && dets && chol && log_norm, "local_fit: null pointer");
@@ -1660,7 +1660,7 @@ extern "C" int abc_local_logpdf(const double* x, int64_t M, const double* X,
                                 const double* inv_covs,
                                 const double* log_norm, double* out,
                                 void* ws, size_t ws_bytes, void* stream) {
-  ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1, "local_logpdf: bad M/N/d");
+  ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= ABC_MAX_D, "local_logpdf: bad M/N/d");
   if (M == 0) return ABC_OK;
   hipStream_t s = as_stream(stream);
   if (d > 16) {

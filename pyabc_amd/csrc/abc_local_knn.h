@@ -52,6 +52,10 @@ constexpr int KN_NB = 520;   // window bins
 constexpr int KN_CAP = 192;  // list entries per particle (LDS: 4 blocks per CU)
 constexpr int KN_MARGIN = 32;
 constexpr int KN_PF = 2;     // row-tile groups in flight per sweep (kn_sweep; A/B: 2 best, 1 / 3 / 4 / 6 slower)
+// padding tiles past the image's ceil(N / 16) tiles: kn_sweep's last group
+// (t0 <= nt - 1) prefetches tiles up to t0 + 2 G + 4 (KN_PF - 1), G = 4 KN_PF,
+// i.e. nt - 1 + 12 KN_PF - 4 < nt + 12 KN_PF
+constexpr int KN_PAD = 12 * KN_PF;
 constexpr int KN_MIN_N = 4 * KN_SK;
 constexpr int KN_QCAP = 256; // open pairs per particle queued by the deferred collect
 typedef float knf4 __attribute__((ext_vector_type(4)));
@@ -155,7 +159,7 @@ __global__ __launch_bounds__(256) void knn_prep_kernel(const double* __restrict_
                                                        unsigned long long* __restrict__ r2bits) {
   constexpr int KB = kn_kb<D>();
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t nt = (N + 15) / 16 + 8 * KN_PF;   // + the sweeps' prefetch padding
+  const int64_t nt = (N + 15) / 16 + KN_PAD;   // + the sweeps' prefetch padding
   double r2 = 0.0;
   if (j < nt * 16) {
     float f[4 * KB];
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(256) void knn_prep_kernel(const double* __restrict_
 // under its predecessors' work (one tile at a time the sweeps were
 // latency-bound at 3 waves per SIMD).  body(t, c) gets tile t's keys c
 // (lane: rows 16 t + 4 (lane >> 4) + r, particle lane & 15).
-// The image carries 4 KN_PF padding tiles past nt, so the prefetch of the
+// The image carries KN_PAD = 12 KN_PF padding tiles past nt, so the prefetch of the
 // last group needs no clamp; tile indices are wave-uniform 32-bit values
 // (scalar address arithmetic, the lane offset the only vector part).
 template <int KB, class Body>
@@ -227,7 +231,7 @@ __device__ __forceinline__ void kn_sweep(const float* __restrict__ img, int nt, 
 #pragma unroll
     for (int i = 0; i < KN_PF; ++i) c[i] = cn[i];
     mfma();                 // group t0 + G (its loads were issued a group ago)
-    load(t0 + 2 * G);       // the image has 2 G padding tiles past nt
+    load(t0 + 2 * G);       // <= nt - 1 + 2 G + 4 (KN_PF - 1) < nt + KN_PAD
 #pragma unroll
     for (int i = 0; i < KN_PF; ++i)
       if (t0 + 4 * i < nt) body(t0 + 4 * i, c[i]);

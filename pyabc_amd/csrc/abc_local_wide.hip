@@ -85,6 +85,7 @@ __host__ __device__ inline int64_t wide_big_doubles(int d) {
 }
 
 constexpr int WCH_FLAT = WCH * (WD_MAX + 1);   // LDS doubles of the member-row chunk
+static_assert(ABC_MAX_D + 1 <= WCH_FLAT, "a member row (d + 1 doubles) must fit the LDS chunk");
 
 template <bool BIG>
 __global__ __launch_bounds__(WT) void local_wide_fit_kernel(WideFitArgs A) {

@@ -336,7 +336,7 @@ extern "C" int abc_propose(const double* X, const double* cdf,
                            int max_attempts, double* theta,
                            double* prior_logpdf, int64_t* ancestor,
                            int32_t* attempts, void* stream) {
-  ABC_CHECK_ARG(d >= 1 && d <= 4096 && B >= 0 && max_attempts >= 1, "propose: bad d/B");
+  ABC_CHECK_ARG(d >= 1 && d <= ABC_MAX_D && B >= 0 && max_attempts >= 1, "propose: bad d/B");
   ABC_CHECK_ARG(max_attempts < (1 << 15), "propose: max_attempts too large");
   if (B == 0) return ABC_OK;
   ABC_CHECK_ARG(theta && prior_logpdf && prior_kind && prior_params, "propose: null pointer");
@@ -357,7 +357,7 @@ extern "C" int abc_local_propose(const double* X, const double* cdf,
                                  int max_attempts, double* theta,
                                  double* prior_logpdf, int64_t* ancestor,
                                  int32_t* attempts, void* stream) {
-  ABC_CHECK_ARG(d >= 1 && d <= 4096 && B >= 0 && max_attempts >= 1, "local_propose: bad d/B");
+  ABC_CHECK_ARG(d >= 1 && d <= ABC_MAX_D && B >= 0 && max_attempts >= 1, "local_propose: bad d/B");
   ABC_CHECK_ARG(max_attempts < (1 << 15), "local_propose: max_attempts too large");
   if (B == 0) return ABC_OK;
   ABC_CHECK_ARG(X && cdf && chol && N >= 1 && theta && prior_logpdf && prior_kind &&
@@ -373,7 +373,7 @@ extern "C" int abc_prior_logpdf(const double* theta, int64_t B, int d,
                                 const int32_t* prior_kind,
                                 const double* prior_params, double* out,
                                 void* stream) {
-  ABC_CHECK_ARG(d >= 1 && d <= 64 && B >= 0, "prior_logpdf: bad d/B");
+  ABC_CHECK_ARG(d >= 1 && d <= ABC_MAX_D && B >= 0, "prior_logpdf: bad d/B");
   if (B == 0) return ABC_OK;
   ABC_CHECK_ARG(theta && prior_kind && prior_params && out, "prior_logpdf: null pointer");
   hipLaunchKernelGGL(prior_logpdf_kernel, dim3((unsigned)ceil_div(B, 256)), dim3(256), 0,

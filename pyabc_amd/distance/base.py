@@ -1,3 +1,5 @@
+# Adapted from pyABC (https://github.com/ICB-DCM/pyABC), BSD-3-Clause,
+# Copyright 2017 the pyABC developers -- see NOTICE at the repository root.
 """Distance ABC (pyabc/distance/base.py:10-275), same interface."""
 import json
 from abc import ABC, abstractmethod

@@ -1,3 +1,5 @@
+# Adapted from pyABC (https://github.com/ICB-DCM/pyABC), BSD-3-Clause,
+# Copyright 2017 the pyABC developers -- see NOTICE at the repository root.
 """Population size strategies (pyabc/populationstrategy.py:22-261).
 
 AdaptivePopulationSize runs its bootstrapped CV

@@ -1,3 +1,5 @@
+# Adapted from pyABC (https://github.com/ICB-DCM/pyABC), BSD-3-Clause,
+# Copyright 2017 the pyABC developers -- see NOTICE at the repository root.
 """Sample / Sampler semantics (pyabc/sampler/base.py:8-233)."""
 from abc import ABC, ABCMeta, abstractmethod
 from typing import List

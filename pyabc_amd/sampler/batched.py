@@ -345,9 +345,15 @@ class BatchedGPUSampler(Sampler):
                     if lp is None:
                         got.insert(1, None)
                 if got[1] is None:
-                    # kept rows only (never a gave-up proposal): the bits the
-                    # proposal kernel would have written (same device function)
+                    # kept rows only: the bits the proposal kernel would have
+                    # written (same device function)
                     got[1] = gpu.prior_logpdf(got[0], spec.prior_kind, spec.prior_params)
+                    if (all_accepted or spec.distance is None) and att is not None:
+                        # this branch keeps rows 0..k-1 unfiltered, including
+                        # proposals that exhausted max_attempts: their last
+                        # draw's density is not the proposal's, and the
+                        # proposal kernel would have written -inf (weight 0)
+                        gpu.mask_gave_up(got[1], att[:k_mine], self.max_attempts, -np.inf)
                 acc_theta.append(got[0])
                 acc_lp.append(got[1])
                 acc_d.append(got[2])
@@ -767,7 +773,8 @@ class BatchedGPUSampler(Sampler):
         if not (spec.transition is None and getattr(spec, "host_prior", None)):
             fr = self._proposal_round(spec, seed, gen, gpu.require_device())
         if fr is not None:
-            # the prior log-density only for the rows kept (_keep_lp)
+            # the prior log-density only for the rows kept (computed after
+            # the kept-row gather in sample_until_n_accepted)
             th, lp, anc, att = fr.propose(lo, B, with_lp=False)
             return th, lp, (anc if spec.transition is not None else None), att
         if spec.transition is None:

@@ -1,3 +1,5 @@
+# Adapted from pyABC (https://github.com/ICB-DCM/pyABC), BSD-3-Clause,
+# Copyright 2017 the pyABC developers -- see NOTICE at the repository root.
 """SingleCoreSampler (pyabc/sampler/singlecore.py:6-38): the per-candidate
 loop over ``simulate_one``; each candidate's plugins still run through the
 GPU kernels (batch of one)."""

@@ -1,3 +1,5 @@
+# Adapted from pyABC (https://github.com/ICB-DCM/pyABC), BSD-3-Clause,
+# Copyright 2017 the pyABC developers -- see NOTICE at the repository root.
 """Population size for a target KDE coefficient of variation.
 
 Reference: pyabc/transition/predict_population_size.py:1-60.  Evaluates

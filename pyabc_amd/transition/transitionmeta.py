@@ -1,3 +1,5 @@
+# Adapted from pyABC (https://github.com/ICB-DCM/pyABC), BSD-3-Clause,
+# Copyright 2017 the pyABC developers -- see NOTICE at the repository root.
 """Zero-parameter handling and in-place weight normalisation around fit /
 pdf / rvs, as pyabc/transition/transitionmeta.py:8-62 does."""
 import functools

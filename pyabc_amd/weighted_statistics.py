@@ -1,3 +1,5 @@
+# Adapted from pyABC (https://github.com/ICB-DCM/pyABC), BSD-3-Clause,
+# Copyright 2017 the pyABC developers -- see NOTICE at the repository root.
 """Weighted statistics (pyabc/weighted_statistics.py:13-83), host versions
 for the per-particle API; the generation engine uses the device kernels
 (abc_weighted_quantile, pyabc_amd.gpu)."""

@@ -97,6 +97,45 @@ def gen_local():
         print("local", tag, t.k, pdf[:3])
 
 
+def gen_local_degenerate():
+    """LocalTransition on populations whose neighbour weights are degenerate
+    (local_transition.py:125-139 -> np.cov(aweights) with 1 - sum a^2 == 0,
+    or all neighbour weights 0): one particle carries all the weight of its
+    neighbourhood (the others at 1e-20 of it), and a far cluster has zero
+    weights.  The reference's covariances are non-finite exactly there; its
+    ``while det <= 0`` loop exits on the NaN determinant.  d = 3 (register
+    kernels), 20 (runtime-d, LDS) and 80 (runtime-d, workspace matrices)."""
+    import warnings
+    out = {}
+    for d, N, k in [(3, 160, 10), (20, 200, 30), (80, 420, 100)]:
+        rng = np.random.default_rng(1000 + d)
+        X = rng.standard_normal((N, d))
+        w = np.exp(0.3 * rng.standard_normal(N))
+        # a cluster far from the rest around particle 0, which dominates its
+        # neighbours' neighbourhoods (no other particle's k nearest reach it,
+        # so no covariance sits on the det <= 0 knife edge)
+        m = k + 6
+        X[0] = 20.0
+        X[1:m] = X[0] + 0.1 * rng.standard_normal((m - 1, d))
+        w[0] = 1.0
+        w[1:m] = 1e-20
+        # a far cluster of zero-weight particles (> k + 1 of them)
+        z0, z1 = N - (k + 8), N
+        X[z0:z1] = 40.0 + rng.standard_normal((z1 - z0, d))
+        w[z0:z1] = 0.0
+        w = w / w.sum()
+        t = LocalTransition(k=k, k_fraction=None)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            with np.errstate(all="ignore"):
+                t.fit(pd.DataFrame(X, columns=names(d)), w.copy())
+        fin = np.isfinite(t.covs).all(axis=(1, 2))
+        out[f"X{d}"], out[f"w{d}"], out[f"k{d}"] = X, w, t.k
+        out[f"covs{d}"], out[f"dets{d}"] = t.covs, t.determinants
+        print("local degenerate d", d, "non-finite covariances:", np.nonzero(~fin)[0])
+    np.savez_compressed(os.path.join(HERE, "local_degenerate.npz"), **out)
+
+
 def gen_distance():
     rng = np.random.default_rng(7)
     out = {}
@@ -643,6 +682,9 @@ if __name__ == "__main__":
         sys.exit(0)
     if "--e2e-large" in sys.argv:
         gen_e2e_large()
+        sys.exit(0)
+    if "--local-degenerate" in sys.argv:
+        gen_local_degenerate()
         sys.exit(0)
     if "--e2e-samples" in sys.argv:
         gen_e2e_samples()

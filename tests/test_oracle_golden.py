@@ -77,6 +77,24 @@ def test_local_fit_and_pdf(tag):
     np.testing.assert_allclose(pdf, g["pdf"], rtol=1e-9)
 
 
+@pytest.mark.parametrize("d", [3, 20, 80])
+def test_local_fit_degenerate_weights(d):
+    """Neighbourhoods whose weights make np.cov's 1 - sum a^2 exactly 0 (one
+    neighbour carries all the weight) or whose weights are all 0: the
+    reference's covariances (tests/golden/local_degenerate.npz, made by
+    importing pyABC) are non-finite exactly there and its det loop exits on
+    the NaN determinant; the oracle gives the same non-finite set and the
+    finite covariances to 1e-9 relative."""
+    g = load("local_degenerate.npz")
+    with np.errstate(all="ignore"):
+        fit = oracle.local_fit(g[f"X{d}"], g[f"w{d}"], k=int(g[f"k{d}"]), k_fraction=None)
+    ref = g[f"covs{d}"]
+    fin = np.isfinite(ref).all(axis=(1, 2))
+    assert 0 < fin.sum() < len(fin)
+    np.testing.assert_array_equal(np.isfinite(fit["covs"]).all(axis=(1, 2)), fin)
+    np.testing.assert_allclose(fit["covs"][fin], ref[fin], rtol=1e-9, atol=1e-13)
+
+
 def test_pnorm_golden():
     g = load("pnorm.npz")
     cases = sorted({k.split("__")[0] for k in g.files})
