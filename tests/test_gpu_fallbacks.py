@@ -330,7 +330,8 @@ def test_local_transition_d80_generations():
     those (r_ij = share of pair j in its density), its normalised log weight
     by that minus the weighted mean: |dlog w_i| <= b_i + sum_k w_k b_k with
     b_i = sum_j r_ij c_n u kappa_j (lambda_max_j |d_ij|^2 / 2 + d / 2).
-    The bound is asserted per row, and its largest value is printed."""
+    The bound is asserted per row; the largest error, its row's bound and
+    the largest ratio are printed (round 5: 1.6e-5 against 3.4e-4 at t = 2)."""
     import pyabc_amd as pa
     d = 80
     names = [f"p{q:02d}" for q in range(d)]
@@ -355,8 +356,9 @@ def test_local_transition_d80_generations():
         bound = _local_weight_bound(x, Xp, fit, np.exp(ref))
         got = np.log(w)
         err = np.abs(got - ref)
-        print(f"t={t}: max |dlog w| {err.max():.3e}, max bound {bound.max():.3e}, "
-              f"max ratio {np.max(err / bound):.3f}")
+        i = int(np.argmax(err))
+        print(f"t={t}: max |dlog w| {err[i]:.3e} (row {i}, its bound {bound[i]:.3e}), "
+              f"median bound {np.median(bound):.3e}, max ratio {np.max(err / bound):.3e}")
         assert (err <= bound).all(), np.max(err / bound)
 
 
