@@ -415,7 +415,7 @@ def main():
              "f32": "mvn_lse_kernel<float> (f32 MFMA cross term + exp2 + LSE)"}
     # the main (hinted) instantiation, mvn_x3_kernel<KB, CT, false>
     traffic, traffic_src = measured_traffic(
-        args, n_pop, f"mvn_x3_kernelILi{x3_k // 32}ELi{x3_ct}ELb0E")
+        args, n_pop, f"mvn_x3_kernelILi{x3_k // 16}ELi{x3_ct}ELb0E")
     # per-stage split of the timed region (HIP events on the launch streams)
     c_ms, c_n = timer.channels["candidates"]
     r_ms, r_n = timer.channels["regen"]
@@ -513,7 +513,7 @@ def main():
                                   "x3 runs f16 MFMA on 3-limb operands, so frac can "
                                   "exceed 1 (fp32-grade results above the fp32 MFMA "
                                   "roofline); its own bound is the MFMA + exp2 + add "
-                                  "issue rate per 16x16 tile, and executed_frac is "
+                                  "issue rate per 32x32 tile pair, and executed_frac is "
                                   "the f16 MFMA pipe's share"),
                          "pairs_per_s": k_pairs / (k_ms * 1e-3) if k_n else None,
                          "executed_mfma_tflops": executed,

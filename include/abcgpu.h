@@ -115,7 +115,9 @@ int abc_normalize_weights(double* w, int64_t N, double* stats, void* ws,
  * eigen-whitening of Sigma (scipy _PSD semantics): U [d x r], mean mu [d].
  * pack: builds the MFMA A-operand image of the population once per fit:
  *   y_j = (X_j - mu) U,  c_j = log(w_j) + log_w_shift - |y_j|^2 / 2
- * (log_w_shift = -log max w keeps every exponent <= 0).  `range` (device,
+ * (log_w_shift = -log max w keeps every exponent <= 0; log_w_shift_dev,
+ * device, nullable, X3 only: read the shift from there instead, e.g.
+ * abc_mvn_fit's stats[3], so the fit needs no host read).  `range` (device,
  * 2 doubles, nullable; X3 only) receives max_j |y_j| in the log2-scaled
  * units of the X3 kernel (sqrt(log2 e) y) and the limb grid exponent E the
  * image was built with; the X3 image is accurate to ~1e-7 for E <= 8 (use
@@ -139,13 +141,31 @@ int abc_normalize_weights(double* w, int64_t N, double* stats, void* ws,
 size_t abc_mvn_packed_bytes(int64_t N, int r, int prec);
 int abc_mvn_pack_population(const double* X, const double* w, int64_t N, int d,
                             const double* mu, const double* U, int r,
-                            double log_w_shift, int prec, void* packed,
-                            double* range, void* stream);
+                            double log_w_shift, const double* log_w_shift_dev,
+                            int prec, void* packed, double* range, void* stream);
+/* The host half of MultivariateNormalTransition.fit on the device
+ * (multivariatenormal.py:72-83 and scipy's _PSD behind its frozen
+ * multivariate_normal): from abc_weighted_moments' output `moments`
+ * [sum w, sum w^2, mean (d), biased cov (d x d), max w] of normalised
+ * weights, cov = np.cov(X, aweights=w) * bw^2 * scaling with bw the
+ * bandwidth rule of the effective sample size 1 / sum w^2 (bw_rule 0 =
+ * silverman_rule_of_thumb :27-37, 1 = scott_rule_of_thumb :14-24); its
+ * eigen-decomposition (parallel Jacobi, fp64) with eigenvalues `evals` (d,
+ * decreasing) and vectors `evec` (d x d, columns); the whitening U (d x d:
+ * columns of the eigenvalues above 1e6 eps max|s| scaled by 1/sqrt(s), the
+ * others zero); the lower sampling factor L (L L^T = cov, semidefinite
+ * Cholesky); stats (8) = [rank, log pdet, support tol, -log max w, bw,
+ * min s, max s, ok (0: cov not positive semidefinite)].  All device, one
+ * single-workgroup launch, no host read; d <= 64. */
+int abc_mvn_fit(const double* moments, int d, double scaling, int bw_rule,
+                double* cov, double* evec, double* evals, double* U, double* L,
+                double* stats, void* stream);
 size_t abc_mvn_logpdf_workspace(int64_t M, int64_t N, int r, int prec);
 /* K slots the X3 kernel executes per (candidate, population row) pair at
- * whitened rank r (the f16 MFMA work per pair is 2 K FLOP; K = 32 x MFMA
- * blocks) and its candidate tiles per wave (nullable outputs); returns the
- * kernel (0 = mvn_x3_kernel<K / 32, tiles>).  A layout query for reporting
+ * whitened rank r (the f16 MFMA work per pair is 2 K FLOP; K = 16 x the
+ * v_mfma_f32_32x32x16_f16 instructions per 32x32 tile pair) and its 32-column
+ * candidate tiles per wave (nullable outputs); returns the kernel (1 =
+ * mvn_x3_kernel<K / 16, tiles> on 32x32x16).  A layout query for reporting
  * (bench.py names the instantiation its traffic file must match); no device
  * work. */
 int abc_mvn_x3_layout(int r, int* kslots, int* tiles_per_wave);

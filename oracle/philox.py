@@ -77,10 +77,10 @@ def normal_pairs(x0, x1):
     f32 = np.float32
     a = np.asarray(x0, dtype=np.uint32).astype(np.uint64)
     b = np.asarray(x1, dtype=np.uint32).astype(np.uint64)
-    m1 = ((a >> np.uint64(9)) << np.uint64(1)) | np.uint64(1)
-    yi = np.uint64(1 << 24) - m1
+    m1 = a | np.uint64(1)                 # u1 = m1 2^-32 (32 bits)
+    yi = np.uint64(1 << 32) - m1
     # series branch: u1 > 1 - 2^-8
-    y = yi.astype(np.float32) * f32(2.0 ** -24)
+    y = yi.astype(np.float32) * f32(2.0 ** -32)
     z = y * f32(0.2) + f32(0.25)
     z = z * y + f32(1 / 3)
     z = z * y + f32(0.5)
@@ -90,16 +90,16 @@ def normal_pairs(x0, x1):
     e = (np.frexp(m1.astype(np.float64))[1] - 1).astype(np.uint64)
     t = (m1 << (np.uint64(31) - e)) & np.uint64(0xFFFFFFFF)
     i = ((t >> np.uint64(24)) & np.uint64(127)).astype(np.int64)
-    delta = ((t >> np.uint64(8)) & np.uint64(0xFFFF)).astype(np.float32) * f32(2.0 ** -23)
+    delta = (t & np.uint64(0xFFFFFF)).astype(np.float32) * f32(2.0 ** -31)
     r = delta * T["inv"][i]
     p = r * f32(-0.25) + f32(1 / 3)
     p = p * r - f32(0.5)
     p = p * r + f32(1.0)
     p = p * r
-    k = (np.uint64(24) - e).astype(np.float32)
+    k = (np.uint64(32) - e).astype(np.float32)
     LN2_HI, LN2_LO = f32(float.fromhex("0x1.62e4p-1")), f32(float.fromhex("0x1.7f7d1cp-20"))
     v_table = (k * LN2_HI - T["hi"][i]) + ((k * LN2_LO - T["lo"][i]) - p)
-    v = np.where(yi < np.uint64(1 << 16), v_series, v_table).astype(np.float32)
+    v = np.where(yi < np.uint64(1 << 24), v_series, v_table).astype(np.float32)
     R = np.sqrt((f32(2.0) * v).astype(np.float64)).astype(np.float32)
     m2 = ((b >> np.uint64(9)) << np.uint64(1)) | np.uint64(1)
     ia = (m2 >> np.uint64(16)).astype(np.int64)

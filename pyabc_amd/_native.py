@@ -34,8 +34,9 @@ SIGNATURES = {
     "abc_normalize_weights": (I32, [P, I64, P, P, SZ, P]),
     "abc_mvn_packed_bytes": (SZ, [I64, I32, I32]),
     "abc_mvn_x3_layout": (I32, [I32, P, P]),
-    "abc_mvn_pack_population": (I32, [P, P, I64, I32, P, P, I32, D, I32, P, P,
+    "abc_mvn_pack_population": (I32, [P, P, I64, I32, P, P, I32, D, P, I32, P, P,
                                       P]),
+    "abc_mvn_fit": (I32, [P, I32, D, I32, P, P, P, P, P, P, P]),
     "abc_mvn_logpdf_workspace": (SZ, [I64, I64, I32, I32]),
     "abc_mvn_logpdf": (I32, [P, I64, I32, P, P, P, I64, P, P, I32, I32, D, D,
                              P, P, P, SZ, P]),

@@ -104,17 +104,18 @@ __device__ __forceinline__ void stage_bm_tab(float* lds) {
 }
 
 // Box-Muller: n0 = R cos(2 pi u2), n1 = R sin(2 pi u2), R = sqrt(-2 ln u1),
-// u = uniform01 (24 significant bits: u = m 2^-24, m odd).  The transform is
-// evaluated in fp32 -- the precision its 24-bit inputs carry -- with only
-// correctly rounded operations in a fixed order (no contraction; sqrt_rn;
-// 4 KB of tables), so that
+// u1 = m1 2^-32 with m1 the whole 32-bit word made odd (so u1 >= 2^-32 and
+// R <= sqrt(64 ln 2) = 6.66: the normals are cut at |n| < 6.66, mass
+// 2.7e-11 per normal), u2 = m2 2^-24 (m2 odd, 24 bits: the angle).  The
+// transform is evaluated in fp32 with only correctly rounded operations in a
+// fixed order (no contraction; sqrt_rn; 4 KB of tables), so that
 // oracle/philox.py normal_pairs replays it bit for bit in numpy float32:
-//   ln: m = 2^e f, f = c_i + delta with c_i = 1 + i/128 for the top 7
-//     fraction bits i (delta exact); ln f = ln c_i + log1p(delta / c_i),
-//     the table value an fp32 pair and log1p a degree-4 series on
-//     [0, 2^-7); -ln u1 = (24 - e) ln2 - ln f, whose leading difference is
-//     exact where it cancels; for u1 > 1 - 2^-8 the series of -ln(1 - y),
-//     y = 1 - u1 exact (a rare branch);
+//   ln: m1 = 2^e f, f = c_i + delta with c_i = 1 + i/128 for the top 7
+//     fraction bits i (delta, the next 24 bits, exact in fp32); ln f = ln c_i
+//     + log1p(delta / c_i), the table value an fp32 pair and log1p a degree-4
+//     series on [0, 2^-7); -ln u1 = (32 - e) ln2 - ln f, whose leading
+//     difference is exact where it cancels; for u1 > 1 - 2^-8 the series of
+//     -ln(1 - y), y = 1 - u1 exact (a rare branch);
 //   sin/cos: angle = pi i / 128 + pi j 2^-23 (i, j = high 8 / low 16 bits of
 //     m2): table sin/cos of the first, degree-3/4 series of the second,
 //     combined by the angle-addition formulas.
@@ -128,29 +129,29 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, double& n0,
   constexpr float C3 = 0x1.555556p-2f, C5 = 0x1.99999ap-3f;  // 1/3, 1/5
   constexpr float C6 = 0x1.555556p-3f, C24 = 0x1.555556p-5f;  // 1/6, 1/24
   constexpr float PI_2M23 = 0x1.921fb6p-22f;  // pi 2^-23
-  // ---- v = -ln u1, u1 = m1 2^-24
-  const uint32_t m1 = ((a >> 9) << 1) | 1u;
-  const uint32_t yi = (1u << 24) - m1;
+  // ---- v = -ln u1, u1 = m1 2^-32
+  const uint32_t m1 = a | 1u;
+  const uint32_t yi = 0u - m1;                       // 2^32 - m1
   float v;
-  if (yi < (1u << 16)) {
-    const float y = (float)yi * 0x1p-24f;
+  if (yi < (1u << 24)) {
+    const float y = (float)yi * 0x1p-32f;
     float z = y * C5 + 0.25f;
     z = z * y + C3;
     z = z * y + 0.5f;
     z = z * y + 1.0f;
     v = z * y;
   } else {
-    const int e = 31 - __clz((int)m1);               // floor(log2 m1), 0..22
+    const int e = 31 - __clz((int)m1);               // floor(log2 m1), 0..31
     const uint32_t t = m1 << (31 - e);               // leading one at bit 31
     const int i = (int)((t >> 24) & 127u);
-    const float delta = (float)((t >> 8) & 0xFFFFu) * 0x1p-23f;
+    const float delta = (float)(t & 0xFFFFFFu) * 0x1p-31f;
     const float* lg = tab + BM_TAB_LOG + 4 * i;      // (INV_C, LN_HI, LN_LO, 0)
     const float r = delta * lg[0];
     float p = r * -0.25f + C3;
     p = p * r - 0.5f;
     p = p * r + 1.0f;
     p = p * r;                                       // log1p(r)
-    const float k = (float)(24 - e);
+    const float k = (float)(32 - e);
     v = (k * LN2_HI - lg[1]) + ((k * LN2_LO - lg[2]) - p);
   }
   const float R = sqrt_rn(2.0f * v);

@@ -384,8 +384,8 @@ size_t x3_packed_bytes(int64_t N, int r);
 int x3_max_rank();
 int x3_pack_population(const double* X, const double* w, int64_t N, int d,
                        const double* mu, const double* U, int r,
-                       double log_w_shift, void* packed, double* range,
-                       hipStream_t s);
+                       double log_w_shift, const double* shift_dev, void* packed,
+                       double* range, hipStream_t s);
 size_t x3_logpdf_workspace(int64_t M, int64_t N, int r);
 int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
               const double* X, const double* w, int64_t N, const double* mu,
@@ -406,7 +406,8 @@ extern "C" size_t abc_mvn_packed_bytes(int64_t N, int r, int prec) {
 extern "C" int abc_mvn_pack_population(const double* X, const double* w,
                                        int64_t N, int d, const double* mu,
                                        const double* U, int r,
-                                       double log_w_shift, int prec,
+                                       double log_w_shift,
+                                       const double* log_w_shift_dev, int prec,
                                        void* packed, double* range,
                                        void* stream) {
   ABC_CHECK_ARG(N >= 0 && d >= 1 && d <= 64, "pack: bad N=%lld d=%d", (long long)N, d);
@@ -414,9 +415,11 @@ extern "C" int abc_mvn_pack_population(const double* X, const double* w,
   ABC_CHECK_ARG(prec == ABC_PREC_F32 || prec == ABC_PREC_F64 || prec == ABC_PREC_X3,
                 "pack: bad prec");
   ABC_CHECK_ARG(packed && mu && U && (N == 0 || (X && w)), "pack: null pointer");
+  ABC_CHECK_ARG(log_w_shift_dev == nullptr || prec == ABC_PREC_X3,
+                "pack: a device shift is read by the X3 image only");
   if (prec == ABC_PREC_X3)
-    return x3_pack_population(X, w, N, d, mu, U, r, log_w_shift, packed, range,
-                              as_stream(stream));
+    return x3_pack_population(X, w, N, d, mu, U, r, log_w_shift, log_w_shift_dev, packed,
+                              range, as_stream(stream));
   if (range) ABC_HIP(hipMemsetAsync(range, 0, 2 * sizeof(double), as_stream(stream)));
   const int KB = (int)ceil_div(r + 1, 4);
   const int64_t NT = ceil_div(N > 0 ? N : 1, 16);

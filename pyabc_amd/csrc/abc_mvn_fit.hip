@@ -1,0 +1,216 @@
+// MultivariateNormalTransition.fit's host half on the device: from the
+// weighted moments (abc_weighted_moments), the KDE covariance, its PSD
+// eigen-whitening and the sampling factor, with no host read in the fit.
+//
+// Reference: pyabc/transition/multivariatenormal.py:72-83
+//   cov = smart_cov(X, w) * bandwidth_selector(ess, d)^2 * scaling
+//     (np.cov(X, aweights=w, rowvar=False); ess = 1 / sum w^2,
+//      silverman :27-37 or scott :14-24)
+//   normal = st.multivariate_normal(cov=cov, allow_singular=True)
+//     -> scipy.stats._multivariate._PSD: s, u = eigh(cov); cut-off
+//        1e6 eps max|s| ("not positive semidefinite" below -cut-off);
+//        U = u[:, s > cut] / sqrt(s); log pdet = sum log s[kept]
+//
+// One workgroup: the d x d matrix (d <= 64) in LDS, a parallel cyclic
+// Jacobi eigen-decomposition in fp64 (round-robin pair ordering: each step
+// rotates d/2 disjoint (p, q) pairs, rows then columns; sweeps until every
+// off-diagonal is below 2^-53 sqrt(|a_pp a_qq|)), eigenpairs sorted by
+// decreasing eigenvalue, the whitening U (kept columns scaled by 1/sqrt(s),
+// cut ones zero -- so the MFMA image can be packed at rank d before the
+// host knows the rank), and L L^T = cov by a semidefinite Cholesky (pivots
+// at or below the cut-off give zero columns).  stats = [rank, log pdet,
+// support tol, -log max w, bandwidth, min s, max s, ok].
+#include "abc_common.h"
+
+namespace abc {
+namespace {
+
+constexpr int FT = 256;
+constexpr int FD = 64;
+
+__global__ __launch_bounds__(FT) void mvn_fit_kernel(const double* __restrict__ mom, int d,
+                                                     double scaling, int rule,
+                                                     double* __restrict__ cov_out,
+                                                     double* __restrict__ evec,
+                                                     double* __restrict__ evals,
+                                                     double* __restrict__ U,
+                                                     double* __restrict__ L,
+                                                     double* __restrict__ stats) {
+  __shared__ double A[FD][FD + 1];
+  __shared__ double V[FD][FD + 1];
+  __shared__ double C[FD][FD + 1];   // the covariance, then its Cholesky work
+  __shared__ double rc[FD / 2], rs[FD / 2];
+  __shared__ int rp[FD / 2], rq[FD / 2];
+  __shared__ double lam[FD], srt[FD];
+  __shared__ double s_piv;
+  __shared__ int s_done;
+  const int t = threadIdx.x;
+  const double sw = mom[0], sw2 = mom[1];
+  const double wmax = mom[2 + d + d * d];
+  // bandwidth of the effective sample size 1 / sum w^2 (weights normalised)
+  const double ess = 1.0 / sw2;
+  const double bw = rule == 1 ? pow(ess, -1.0 / (d + 4))
+                              : pow(4.0 / ess / (d + 2), 1.0 / (d + 4));
+  const double bw2 = bw * bw;
+  const double den = sw - sw2 / sw;
+  for (int e = t; e < d * d; e += FT) {
+    const int i = e / d, j = e % d;
+    // the host's operation order: ((cov_b * sw) / (sw - sw2 / sw)) * bw^2 * scaling
+    double c = mom[2 + d + e] * sw;
+    c = c / den;
+    c = c * bw2;
+    c = c * scaling;
+    A[i][j] = c;
+    C[i][j] = c;
+    V[i][j] = i == j ? 1.0 : 0.0;
+    cov_out[e] = c;
+  }
+  __syncthreads();
+  // ---- parallel cyclic Jacobi
+  const int n2 = d + (d & 1);           // even number of players (d itself = a dummy)
+  const int np = n2 / 2;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    // convergence: every off-diagonal below 2^-53 sqrt(|a_pp a_qq|) (or 0)
+    int big = 0;
+    for (int e = t; e < d * d; e += FT) {
+      const int i = e / d, j = e % d;
+      if (i < j) {
+        const double a = fabs(A[i][j]);
+        if (a > 0.0 && a > 0x1p-53 * sqrt(fabs(A[i][i] * A[j][j])) && a > 1e-300) big = 1;
+      }
+    }
+    if (t == 0) s_done = 1;
+    __syncthreads();
+    if (big) s_done = 0;
+    __syncthreads();
+    if (s_done) break;
+    for (int step = 0; step < n2 - 1; ++step) {
+      if (t < np) {
+        int p, q;
+        if (t == 0) { p = 0; q = 1 + step % (n2 - 1); }
+        else {
+          p = 1 + (step + t) % (n2 - 1);
+          q = 1 + (step - t + n2 - 1) % (n2 - 1);
+        }
+        if (p > q) { const int x = p; p = q; q = x; }
+        double c = 1.0, s = 0.0;
+        if (q < d) {
+          const double apq = A[p][q];
+          if (apq != 0.0) {
+            const double tau = (A[q][q] - A[p][p]) / (2.0 * apq);
+            const double tt = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+            c = 1.0 / sqrt(1.0 + tt * tt);
+            s = tt * c;
+          }
+        }
+        rp[t] = p; rq[t] = q < d ? q : p; rc[t] = c; rs[t] = s;
+      }
+      __syncthreads();
+      // rows: A <- J^T A
+      for (int e = t; e < np * d; e += FT) {
+        const int k = e / d, j = e % d;
+        const int p = rp[k], q = rq[k];
+        if (p == q) continue;
+        const double c = rc[k], s = rs[k];
+        const double a = A[p][j], b = A[q][j];
+        A[p][j] = c * a - s * b;
+        A[q][j] = s * a + c * b;
+      }
+      __syncthreads();
+      // columns: A <- A J, V <- V J
+      for (int e = t; e < np * d; e += FT) {
+        const int k = e / d, i = e % d;
+        const int p = rp[k], q = rq[k];
+        if (p == q) continue;
+        const double c = rc[k], s = rs[k];
+        const double a = A[i][p], b = A[i][q];
+        A[i][p] = c * a - s * b;
+        A[i][q] = s * a + c * b;
+        const double va = V[i][p], vb = V[i][q];
+        V[i][p] = c * va - s * vb;
+        V[i][q] = s * va + c * vb;
+      }
+      __syncthreads();
+      if (t < np && rp[t] != rq[t]) { A[rp[t]][rq[t]] = 0.0; A[rq[t]][rp[t]] = 0.0; }
+      __syncthreads();
+    }
+  }
+  // ---- eigenpairs by decreasing eigenvalue (ties by index), PSD cut-off
+  if (t < d) lam[t] = A[t][t];
+  __syncthreads();
+  double mx = 0.0, mn = INFINITY;
+  bool nan = false;
+  for (int i = 0; i < d; ++i) {
+    mx = fmax(mx, fabs(lam[i]));
+    mn = fmin(mn, lam[i]);
+    nan = nan || !(lam[i] == lam[i]);
+  }
+  const double cut = 1e6 * 0x1p-52 * mx;
+  if (t < d) {
+    int r = 0;
+    for (int j = 0; j < d; ++j) r += (lam[j] > lam[t] || (lam[j] == lam[t] && j < t)) ? 1 : 0;
+    srt[r] = lam[t];
+    evals[r] = lam[t];
+    const bool keep = lam[t] > cut;
+    const double f = keep ? 1.0 / sqrt(lam[t]) : 0.0;
+    for (int i = 0; i < d; ++i) {
+      evec[i * d + r] = V[i][t];
+      U[i * d + r] = V[i][t] * f;
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    // log pdet over the kept eigenvalues, in decreasing order
+    int rank = 0;
+    double lp = 0.0;
+    for (int r = 0; r < d; ++r)
+      if (srt[r] > cut) { ++rank; lp += log(srt[r]); }
+    stats[0] = (double)rank;
+    stats[1] = lp;
+    stats[2] = 1e3 * cut;
+    stats[3] = -log(wmax);
+    stats[4] = bw;
+    stats[5] = mn;
+    stats[6] = mx;
+    stats[7] = (nan || mn < -cut) ? 0.0 : 1.0;
+  }
+  // ---- L L^T = cov, lower; pivots <= cut give zero columns
+  for (int j = 0; j < d; ++j) {
+    if (t == 0) {
+      const double s = C[j][j];
+      const double ljj = s > cut ? sqrt(s) : 0.0;
+      C[j][j] = ljj;
+      s_piv = ljj;
+    }
+    __syncthreads();
+    const double ljj = s_piv;
+    for (int i = j + 1 + t; i < d; i += FT) C[i][j] = ljj > 0.0 ? C[i][j] / ljj : 0.0;
+    __syncthreads();
+    for (int e = t; e < (d - j - 1) * (d - j - 1); e += FT) {
+      const int i = j + 1 + e / (d - j - 1), k = j + 1 + e % (d - j - 1);
+      if (k <= i) C[i][k] -= C[i][j] * C[k][j];
+    }
+    __syncthreads();
+  }
+  for (int e = t; e < d * d; e += FT) {
+    const int i = e / d, j = e % d;
+    L[e] = j <= i ? C[i][j] : 0.0;
+  }
+}
+
+}  // namespace
+}  // namespace abc
+
+using namespace abc;
+
+extern "C" int abc_mvn_fit(const double* moments, int d, double scaling, int bw_rule,
+                           double* cov, double* evec, double* evals, double* U, double* L,
+                           double* stats, void* stream) {
+  ABC_CHECK_ARG(d >= 1 && d <= FD, "mvn_fit: d=%d outside [1, %d]", d, FD);
+  ABC_CHECK_ARG(bw_rule == 0 || bw_rule == 1, "mvn_fit: bw_rule %d", bw_rule);
+  ABC_CHECK_ARG(moments && cov && evec && evals && U && L && stats, "mvn_fit: null pointer");
+  hipLaunchKernelGGL(mvn_fit_kernel, dim3(1), dim3(FT), 0, as_stream(stream), moments, d,
+                     scaling, bw_rule, cov, evec, evals, U, L, stats);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}

@@ -1,5 +1,5 @@
 // MultivariateNormalTransition.pdf, "x3" precision: the whitened cross-term
-// GEMM on f16 MFMA (v_mfma_f32_16x16x32_f16) with every operand split into
+// GEMM on f16 MFMA (v_mfma_f32_32x32x16_f16) with every operand split into
 // three 11-bit limbs, exact-grid accumulation in f32, fused with exp2 and the
 // weighted sum over the population.  Result accuracy is that of an f32
 // direct-difference evaluation (~1e-7 relative; tested at 2e-6 against the
@@ -27,26 +27,35 @@
 //   class 2: v1 w3 + v2 w2 + v3 w1      multiples of G^2 2^-22
 // c and m are split into five limbs on the grids 2^22 G^2, 2^11 G^2, G^2
 // (hi) and G^2 2^-11, G^2 2^-22 (lo).  The K dimension holds, in this order,
-//   MFMA block 0       : class 0 (r), C0 C1 C2, M0 M1 M2, O     -> r + 7
-//   MFMA blocks 1 ..   : class 1 (2r), class 2 (3r), C3 C4, M3 M4 -> 5r + 4
-// The f16 MFMA sums each group of 8 products wide and adds the groups to the
-// accumulator in K order with f32 rounding (same probe).  Every block-0 term
-// is a multiple of G^2 and every partial sum is bounded by |c| + |m| + |o| +
-// |z||y| < 2^(2E+2) = 2^24 G^2 (norm checks below), so block 0 is EXACT.  O is
+//   exact groups : class 0 (r), C0 C1 C2, M0 M1 M2, O  -> r + 7, padded to
+//                  whole 8-slot groups (g0 = ceil((r + 7) / 8))
+//   lo groups    : class 1 (2r), class 2 (3r), C3 C4, M3 M4 -> 5r + 4
+// and is run as KB = ceil((8 g0 + 5r + 4) / 16) v_mfma_f32_32x32x16_f16
+// (K = 80 at r = 10: 5 instructions per 32x32 tile pair against the 16x16
+// layout's 6 per 2x2 16x16 tiles).  The f16 MFMA sums each group of 8
+// products wide and adds the groups to the accumulator in K order with f32
+// rounding (probes: tools/probes/mfma_f16_groups.hip for 16x16x32,
+// mfma32_f16_sum.hip for 32x32x16 -- K 0-7 then K 8-15, an exact-grid block
+// sums exactly), so an exact group must not share an 8-slot group with lo
+// terms but may share an MFMA with them.  Every exact-group
+// term is a multiple of G^2 and every partial sum is bounded by |c| + |m| + |o| +
+// |z||y| < 2^(2E+2) = 2^24 G^2 (norm checks below), so the exact groups sum
+// EXACTLY.  O is
 // a per-candidate integer offset (B = -o, A = 1): a first pass over the
-// chunk runs block 0 alone (1 MFMA of KB per tile, exact s_hi) to find each
+// chunk runs the exact groups alone (exact s_hi) to find each
 // column's max, then o = ceil(max s_hi) is written into the B fragment and
 // the main pass leaves s - o <= 1 with the dominant pairs near 0, so the lo
-// blocks round at 2^-24 |s - o|.  Dropped
+// groups round at 2^-24 |s - o|.  Dropped
 // terms (class 3, limb residual) are < 2^(2E-35) per coordinate; numpy
 // emulation of this exact scheme: <= 1e-7 relative on the golden vectors.
 //
 // Layout (HBM): image = 256-byte header (max |y|^2/2, E, ok) + fragments
-// [NT][KB][64 lanes][8 halves] in the order of v_mfma_f32_16x16x32_f16 (lane
-// l holds row l & 15, k = 32 kb + 8 (l >> 4) + j); the population image is
-// built once per fit, the candidate image per call.  Each lane owns ONE
-// candidate column (l & 15) and four population rows of every 16x16 tile, so
-// the sum over the population stays in registers until a final 4-lane
+// [NT][KB][64 lanes][8 halves] of 32-row tiles in the order of
+// v_mfma_f32_32x32x16_f16 (lane l holds row l & 31, k = 16 kb + 8 (l >> 5) +
+// j); the population image is built once per fit, the candidate image per
+// call.  Each lane owns ONE candidate column (l & 31) and sixteen population
+// rows of every 32x32 tile (rows (i & 3) + 8 (i >> 2) + 4 (l >> 5)), so the
+// sum over the population stays in registers until a final 2-lane
 // combine.  Candidates outside the norm bound, and candidates whose density
 // underflows 2^-60 relative to max w (all pairs beyond ~11 kernel widths),
 // are recomputed in fp64 from the whitened population Y and log2 weights lw
@@ -57,23 +66,27 @@ namespace abc {
 namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr double LOG2E = 1.4426950408889634074;
 constexpr double SQRT_LOG2E = 1.2011224087864498;  // sqrt(log2 e)
 constexpr double LN2 = 0.69314718055994530942;
-constexpr int MAX_R = 25;       // K0 = r + 7 <= 32
+constexpr int MAX_R = 25;       // exact groups r + 7 <= 32
 constexpr int E_MIN = 3, E_MAX = 8;
 constexpr float O_MIN = -64.f;  // offsets below this: density < 2^-60 -> rescue
 constexpr size_t HDR = 256;     // image header bytes
 constexpr int X3_PAD = 8;       // pad tiles after the population fragments
+constexpr int TR = 32;          // rows (and candidate columns) per tile
 
 struct Header { double maxsq; int E; int ok; };
 
-__host__ __device__ constexpr int x3_k0(int r) { return r + 7; }
-__host__ __device__ constexpr int x3_k12(int r) { return 5 * r + 4; }
-__host__ __device__ constexpr int x3_kb0(int r) { return (x3_k0(r) + 31) / 32; }
-__host__ __device__ constexpr int x3_kb12(int r) { return (x3_k12(r) + 31) / 32; }
+// exact 8-slot groups, their padded slot count, MFMA instructions per tile
+// pair, and the instructions the max pass needs (those holding exact groups)
+__host__ __device__ constexpr int x3_g0(int r) { return (r + 7 + 7) / 8; }
+__host__ __device__ constexpr int x3_k0pad(int r) { return 8 * x3_g0(r); }
+__host__ __device__ constexpr int x3_kb(int r) { return (x3_k0pad(r) + 5 * r + 4 + 15) / 16; }
+__host__ __device__ constexpr int x3_kb0(int r) { return (x3_g0(r) + 1) / 2; }
+static_assert(x3_kb(10) == 5, "K = 80 at r = 10");
 
 struct Limbs3 { double a1, a2, a3; };  // integers
 struct Limbs5 { double c[5]; };        // integers
@@ -213,19 +226,20 @@ template <int SIDE, int R>
 __global__ __launch_bounds__(128) void pack_x3_kernel(
     const double* __restrict__ P, const double* __restrict__ w, int64_t n,
     int d, const double* __restrict__ mu, const double* __restrict__ U, int r_rt,
-    double log_w_shift, int KB0_rt, int KB_rt, const Header* __restrict__ hdr,
+    double log_w_shift, int K0pad_rt, int KB_rt, const Header* __restrict__ hdr,
     _Float16* __restrict__ img, int64_t ntiles, int32_t* __restrict__ flags,
     double* __restrict__ Y, double* __restrict__ lw, int64_t Np,
-    const int64_t* __restrict__ hint, float* __restrict__ cand_o, int koff) {
+    const int64_t* __restrict__ hint, float* __restrict__ cand_o, int koff,
+    const double* __restrict__ shift_dev) {
   // SIDE 0 writes the fp64 whitened population Y [n x r] and its log2
   // weights lw [n] (rescue + hints); SIDE 1 reads them for the hint rows
   constexpr int RR = R > 0 ? R : MAX_R;
   const int r = R > 0 ? R : r_rt;
-  const int KB0 = R > 0 ? x3_kb0(R) : KB0_rt;
-  const int KB = R > 0 ? x3_kb0(R) + x3_kb12(R) : KB_rt;
-  constexpr int NG = R > 0 ? (x3_kb0(R) + x3_kb12(R)) * 4 : 0;  // 8-slot groups
+  const int K0pad = R > 0 ? x3_k0pad(R) : K0pad_rt;
+  const int KB = R > 0 ? x3_kb(R) : KB_rt;
+  constexpr int NG = R > 0 ? x3_kb(R) * 2 : 0;  // 8-slot groups
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= ntiles * 16) return;
+  if (row >= ntiles * TR) return;
   const int E = hdr->E;
   const bool ok = hdr->ok != 0;
   const double L2 = ldexp(1.0, 2 * E);  // 2^(2E): bound of |y|^2 and |c|
@@ -241,7 +255,8 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
     if (SIDE == 0) {
       const double wj = w[row];
       bad = !(wj > 0.0) || !(2.0 * h <= L2);
-      const double lwj = wj > 0.0 ? (log(wj) + log_w_shift) * LOG2E : -INFINITY;
+      const double sh = shift_dev ? *shift_dev : log_w_shift;
+      const double lwj = wj > 0.0 ? (log(wj) + sh) * LOG2E : -INFINITY;
       scalar = bad ? -L2 : fmax(lwj - h, -L2);
 #pragma unroll
       for (int k = 0; k < RR; ++k)
@@ -276,10 +291,9 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
 #pragma unroll
   for (int k = 0; k < RR; ++k) L[k] = split_coord(v[k], E);
   const Limbs5 S = split_scalar(scalar, E);
-  const int64_t t = row >> 4;
-  const int rl = (int)(row & 15);
-  const int K0pad = 32 * KB0;
-  const int Ktot = 32 * KB;
+  const int64_t t = row / TR;
+  const int rl = (int)(row % TR);
+  const int Ktot = 16 * KB;
   // 8 consecutive K slots of this row form one lane's 16-byte fragment:
   // assemble them in registers and store them as one vector
 #pragma unroll
@@ -293,25 +307,30 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
       if (SIDE == 1 && hint && k == koff) val = -hint_o;  // B = -o (A = 1)
       frag[j] = (_Float16)val;
     }
-    const int kb = g >> 2, lane = rl + 16 * (g & 3);
+    const int kb = g >> 1, lane = rl + 32 * (g & 1);
     *reinterpret_cast<half8*>(img + (((t * KB + kb) * 64) + lane) * 8) = frag;
   }
 }
 
 // ---- the fused limb-split GEMM + exp2 + weighted sum -----------------------
-// One wave = CT candidate tiles x one population chunk; block = 4 waves; 1-D
-// grid, block b -> XCD b % 8 owns chunks {xcd, xcd + 8, ...} so that the
-// blocks sharing a population chunk share one XCD's L2 (speed only).
-// Pass 1: block 0 only -> per-column max of s_hi -> integer offset o.
-// Pass 2: all blocks -> per lane, sum over its population rows of 2^(s - o).
+// One wave = CT candidate tiles (32 columns each) x one population chunk;
+// block = 4 waves; 1-D grid, block b -> XCD b % 8 owns chunks {xcd, xcd + 8,
+// ...} so that the blocks sharing a population chunk share one XCD's L2
+// (speed only).
+// Pass 1: the exact groups only -> per-column max of s_hi -> integer offset o.
+// Pass 2: all groups -> per lane, sum over its population rows of 2^(s - o).
 __device__ __forceinline__ float max3(float a, float b, float c) {
   return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+
+__device__ __forceinline__ f32x16 mfma32(const half8& a, const half8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
 template <int KB, int CT, bool PASS1>
 __global__ __launch_bounds__(256) void mvn_x3_kernel(
     const half8* __restrict__ A, const half8* __restrict__ Bi, int64_t MT,
-    int64_t NT, int nchunk, int64_t tiles_per_chunk, int64_t ngroups, int koff,
+    int64_t NT, int nchunk, int64_t tiles_per_chunk, int64_t ngroups, int koff, int kb0,
     double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -322,9 +341,9 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
   const int64_t group = jb / cpx;
   if (group >= ngroups) return;
   const int64_t ct0 = (group * 4 + wave) * CT;
-  // which lane / element of the block-0 B fragment holds the offset slot
-  const bool off_lane = (lane >> 4) == ((koff & 31) >> 3);
-  const int off_j = koff & 7;
+  // which lanes / instruction / element of the B fragments hold the offset slot
+  const bool off_lane = (lane >> 5) == ((koff >> 3) & 1);
+  const int off_kb = koff >> 4, off_j = koff & 7;
 
   half8 b[CT][KB];
 #pragma unroll
@@ -341,37 +360,49 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
   // never used).  A chunk starting at or past NT (small N) loads nothing.
   static_assert(X3_PAD >= 7, "pad must cover the prefetch distance");
   auto tile = [&](int64_t t) { return t * KB; };
+  const f32x16 zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f,
+                         0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
-  // ---- pass 1: exact s_hi (offset slot still 0) -> column max -> o.
-  // Block-0 fragments through a ring of 4 registers (prefetch distance 4).
+  // ---- pass 1: exact s_hi (offset slot still 0) -> column max -> o.  The
+  // instructions holding exact groups (kb < kb0 <= 2) through a ring of 4
+  // tiles (prefetch distance 4).
   float o[CT];
   if (PASS1 && t_begin < t_end) {
     float mx[CT];
 #pragma unroll
     for (int c = 0; c < CT; ++c) mx[c] = -INFINITY;
-    half8 ring[4];
+    half8 ring[4][2];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) ring[u] = Al[tile(t_begin + u) * 64];
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+        if (kb < KB) ring[u][kb] = Al[(tile(t_begin + u) + kb) * 64];
     for (int64_t t = t_begin; t < t_end; t += 4) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (t + u < t_end) {
 #pragma unroll
           for (int c = 0; c < CT; ++c) {
-            const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                ring[u], b[c][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            mx[c] = max3(max3(mx[c], acc[0], acc[1]), acc[2], acc[3]);
+            f32x16 acc = mfma32(ring[u][0], b[c][0], zero16);
+            if (KB > 1 && kb0 > 1) acc = mfma32(ring[u][1], b[c][1 < KB ? 1 : 0], acc);
+            float m = mx[c];
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) m = max3(m, acc[i], acc[i + 1]);
+            mx[c] = m;
           }
         }
-        ring[u] = Al[tile(t + u + 4) * 64];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+          if (kb < KB) ring[u][kb] = Al[(tile(t + u + 4) + kb) * 64];
       }
     }
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
-      float cm = fmaxf(mx[c], __shfl_xor(mx[c], 16, 64));
-      cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+      const float cm = fmaxf(mx[c], __shfl_xor(mx[c], 32, 64));
       o[c] = fmaxf(ceilf(cm), O_MIN);
-      if (off_lane) b[c][0][off_j] = (_Float16)(-o[c]);
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+        if (kb == off_kb && off_lane) b[c][kb][off_j] = (_Float16)(-o[c]);
     }
   } else {
 #pragma unroll
@@ -395,25 +426,30 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
     }
   }
   auto chain = [&](const half8 (&a)[KB], int c) {
-    f32x4 r = {0.f, 0.f, 0.f, 0.f};
+    f32x16 r = mfma32(a[0], b[c][0], zero16);
 #pragma unroll
-    for (int kb = 0; kb < KB; ++kb)
-      r = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[kb], b[c][kb], r, 0, 0, 0);
+    for (int kb = 1; kb < KB; ++kb) r = mfma32(a[kb], b[c][kb], r);
     return r;
   };
-  auto expsum = [&](const f32x4& v) {
-    return (__builtin_amdgcn_exp2f(v[0]) + __builtin_amdgcn_exp2f(v[1])) +
-           (__builtin_amdgcn_exp2f(v[2]) + __builtin_amdgcn_exp2f(v[3]));
+  auto expsum = [&](const f32x16& v) {
+    float e[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_exp2f(v[i]);
+#pragma unroll
+    for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+      for (int i = 0; i < w; ++i) e[i] += e[i + w];
+    return e[0];
   };
   // one tile: units (t, 0..CT-1); the exp2/sum of unit c - 1 is issued under
   // the MFMA chain of unit c.  Every candidate slot c sums the same tiles in
   // the same order, so a candidate's bits do not depend on where it sits in
   // the launch (and so not on the sharding over ranks).
   auto do_tile = [&](const half8 (&a)[KB]) {
-    f32x4 prev = chain(a, 0);
+    f32x16 prev = chain(a, 0);
 #pragma unroll
     for (int c = 1; c < CT; ++c) {
-      const f32x4 cur = chain(a, c);
+      const f32x16 cur = chain(a, c);
       ls[c - 1] += expsum(prev);
       prev = cur;
     }
@@ -429,8 +465,8 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) a1[kb] = Al[(tile(t + 3) + kb) * 64];
     }
-    // f32 partial sums over at most 16 tiles (64 terms per lane), then fp64
-    if (++nflush == 8) {
+    // f32 partial sums over at most 4 tiles (64 terms per lane), then fp64
+    if (++nflush == 2) {
       nflush = 0;
 #pragma unroll
       for (int c = 0; c < CT; ++c) { l64[c] += (double)ls[c]; ls[c] = 0.f; }
@@ -438,16 +474,15 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
   }
 #pragma unroll
   for (int c = 0; c < CT; ++c) l64[c] += (double)ls[c];
-  // lanes l, l^16, l^32, l^48 hold the same candidate column (same o)
+  // lanes l and l ^ 32 hold the same candidate column (same o)
 #pragma unroll
   for (int c = 0; c < CT; ++c) {
     double v = l64[c];
-    v += __shfl_xor(v, 16, 64);
     v += __shfl_xor(v, 32, 64);
     const int64_t ct = ct0 + c;
-    if (lane < 16 && ct < MT) {
-      if (PASS1) part_o[(int64_t)chunk * Mpad + ct * 16 + lane] = (double)o[c];
-      part_l[(int64_t)chunk * Mpad + ct * 16 + lane] = v;
+    if (lane < 32 && ct < MT) {
+      if (PASS1) part_o[(int64_t)chunk * Mpad + ct * TR + lane] = (double)o[c];
+      part_l[(int64_t)chunk * Mpad + ct * TR + lane] = v;
     }
   }
 }
@@ -597,15 +632,15 @@ __global__ void x3_rescue_final(const int64_t* __restrict__ rescue,
 template <int SIDE>
 void launch_pack(int r, dim3 grid, hipStream_t s, const double* P, const double* w,
                  int64_t n, int d, const double* mu, const double* U,
-                 double log_w_shift, int KB0, int KB, const Header* hdr,
+                 double log_w_shift, int K0pad, int KB, const Header* hdr,
                  _Float16* img, int64_t ntiles, int32_t* flags, double* Y,
                  double* lw, int64_t Np, const int64_t* hint, float* cand_o,
-                 int koff) {
+                 int koff, const double* shift_dev = nullptr) {
 #define ABC_PACK_CASE(RC)                                                          \
   case RC:                                                                         \
     hipLaunchKernelGGL((pack_x3_kernel<SIDE, RC>), grid, dim3(128), 0, s, P, w, n, \
-                       d, mu, U, r, log_w_shift, KB0, KB, hdr, img, ntiles, flags, \
-                       Y, lw, Np, hint, cand_o, koff);                             \
+                       d, mu, U, r, log_w_shift, K0pad, KB, hdr, img, ntiles, flags, \
+                       Y, lw, Np, hint, cand_o, koff, shift_dev);                  \
     break;
   switch (r) {
     ABC_PACK_CASE(1) ABC_PACK_CASE(2) ABC_PACK_CASE(3) ABC_PACK_CASE(4)
@@ -632,26 +667,31 @@ __global__ void x3_scatter_rescued(const int64_t* __restrict__ rescue, int64_t n
   if (q < n) out[rescue[q]] = outs[q];
 }
 
-// candidate tiles per wave for KB MFMA blocks, as dispatch_x3 instantiates
-// them (KB = 3: 10, A/B 8 -> 10 -1.2% at c3; 4 / 5 / 6 / 12 slower)
-__host__ __device__ constexpr int x3_ct(int KB) { return KB == 3 ? 10 : (KB == 2 ? 8 : 4); }
+// candidate tiles (32 columns) per wave for KB MFMA instructions per tile
+// pair, as dispatch_x3 instantiates them
+// (register budget of the hinted pass at 2 waves per SIMD: 4 KB VGPRs per
+// candidate tile, 8 KB for the two population buffers, 32 accumulators)
+__host__ __device__ constexpr int x3_ct(int KB) {
+  return KB <= 3 ? 8 : (KB <= 5 ? 6 : (KB == 6 ? 4 : (KB == 7 ? 3 : 2)));
+}
 
 struct PlanX3 {
-  int KB0, KB, CT, nchunk;
+  int K0pad, KB, KB0, CT, nchunk;
   int64_t MT, NT, MTpad, groups, tiles_per_chunk, Mpad;
 };
 
 PlanX3 make_plan_x3(int64_t M, int64_t N, int r) {
   PlanX3 p;
+  p.K0pad = x3_k0pad(r);
+  p.KB = x3_kb(r);
   p.KB0 = x3_kb0(r);
-  p.KB = p.KB0 + x3_kb12(r);
   p.CT = x3_ct(p.KB);
-  p.MT = ceil_div(M > 0 ? M : 1, 16);
-  p.NT = ceil_div(N > 0 ? N : 1, 16);
+  p.MT = ceil_div(M > 0 ? M : 1, TR);
+  p.NT = ceil_div(N > 0 ? N : 1, TR);
   const int64_t waves = ceil_div(p.MT, p.CT);
   p.groups = ceil_div(waves, 4);
   p.MTpad = p.groups * 4 * p.CT;
-  p.Mpad = p.MTpad * 16;
+  p.Mpad = p.MTpad * TR;
   // Population chunks depend on N only (8..32, a multiple of 8 for the
   // XCD map): a candidate's summation order -- and so its bits -- does not
   // depend on M or on its position, which keeps results identical for any
@@ -683,34 +723,34 @@ void launch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
   if (pass1)
     hipLaunchKernelGGL((mvn_x3_kernel<KB, CT, true>), dim3((unsigned)blocks),
                        dim3(256), 0, s, A, B, p.MT, p.NT, p.nchunk,
-                       p.tiles_per_chunk, p.groups, koff, po, pl, p.Mpad);
+                       p.tiles_per_chunk, p.groups, koff, p.KB0, po, pl, p.Mpad);
   else
     hipLaunchKernelGGL((mvn_x3_kernel<KB, CT, false>), dim3((unsigned)blocks),
                        dim3(256), 0, s, A, B, p.MT, p.NT, p.nchunk,
-                       p.tiles_per_chunk, p.groups, koff, po, pl, p.Mpad);
+                       p.tiles_per_chunk, p.groups, koff, p.KB0, po, pl, p.Mpad);
 }
 
 int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
                 double* po, double* pl, bool pass1, hipStream_t s) {
   switch (p.KB) {
-    case 2: launch_x3<2, 8>(p, A, B, koff, po, pl, pass1, s); break;
-    case 3: launch_x3<3, 10>(p, A, B, koff, po, pl, pass1, s); break;
-    case 4: launch_x3<4, 4>(p, A, B, koff, po, pl, pass1, s); break;
-    case 5: launch_x3<5, 4>(p, A, B, koff, po, pl, pass1, s); break;
-    case 6: launch_x3<6, 4>(p, A, B, koff, po, pl, pass1, s); break;
+#define ABC_X3_CASE(K) case K: launch_x3<K, x3_ct(K)>(p, A, B, koff, po, pl, pass1, s); break;
+    ABC_X3_CASE(2) ABC_X3_CASE(3) ABC_X3_CASE(4) ABC_X3_CASE(5) ABC_X3_CASE(6)
+    ABC_X3_CASE(7) ABC_X3_CASE(8) ABC_X3_CASE(9) ABC_X3_CASE(10) ABC_X3_CASE(11)
+#undef ABC_X3_CASE
     default:
       return set_error(ABC_ERR_UNSUPPORTED, "mvn x3: KB=%d unsupported", p.KB);
   }
   return ABC_OK;
 }
+static_assert(x3_kb(MAX_R) <= 11 && x3_kb(1) >= 2, "dispatch_x3 covers every rank");
 
 }  // namespace
 
 // ---- internal entry points used by abc_mvn.hip ------------------------------
 // image = header | fragments [NT][KB][64][8] f16 | Y [N x r] f64 | lw [N] f64
 size_t x3_frag_bytes(int64_t N, int r) {
-  const int KB = x3_kb0(r) + x3_kb12(r);
-  const int64_t NT = ceil_div(N > 0 ? N : 1, 16) + X3_PAD;
+  const int KB = x3_kb(r);
+  const int64_t NT = ceil_div(N > 0 ? N : 1, TR) + X3_PAD;
   return align_up((size_t)NT * KB * 64 * 8 * sizeof(_Float16), 256);
 }
 double* x3_Y(const void* packed, int64_t N, int r) {
@@ -726,20 +766,22 @@ size_t x3_packed_bytes(int64_t N, int r) {
 
 int x3_max_rank() { return MAX_R; }
 
+// kernel 1 = mvn_x3_kernel<KB, CT, *> on v_mfma_f32_32x32x16_f16: K slots
+// per pair (16 KB) and 32-column candidate tiles per wave
 extern "C" int abc_mvn_x3_layout(int r, int* kslots, int* tiles_per_wave) {
-  const int KB = x3_kb0(r) + x3_kb12(r);
-  if (kslots) *kslots = 32 * KB;
+  const int KB = x3_kb(r);
+  if (kslots) *kslots = 16 * KB;
   if (tiles_per_wave) *tiles_per_wave = x3_ct(KB);
-  return 0;
+  return 1;
 }
 
 int x3_pack_population(const double* X, const double* w, int64_t N, int d,
                        const double* mu, const double* U, int r,
-                       double log_w_shift, void* packed, double* range,
-                       hipStream_t s) {
+                       double log_w_shift, const double* shift_dev, void* packed,
+                       double* range, hipStream_t s) {
   if (r > MAX_R)
     return set_error(ABC_ERR_UNSUPPORTED, "mvn x3: rank %d > %d", r, MAX_R);
-  const int64_t NT = ceil_div(N > 0 ? N : 1, 16);
+  const int64_t NT = ceil_div(N > 0 ? N : 1, TR);
   Header* hdr = (Header*)packed;
   ABC_HIP(hipMemsetAsync(hdr, 0, HDR, s));
   if (N > 0) {
@@ -749,11 +791,11 @@ int x3_pack_population(const double* X, const double* w, int64_t N, int d,
   }
   hipLaunchKernelGGL(x3_setup_kernel, dim3(1), dim3(1), 0, s, hdr, r, range);
   ABC_LAUNCHED();
-  launch_pack<0>(r, dim3((unsigned)ceil_div(NT * 16, 128)), s, X, w, N, d, mu, U,
-                 log_w_shift, x3_kb0(r), x3_kb0(r) + x3_kb12(r), (const Header*)hdr,
+  launch_pack<0>(r, dim3((unsigned)ceil_div(NT * TR, 128)), s, X, w, N, d, mu, U,
+                 log_w_shift, x3_k0pad(r), x3_kb(r), (const Header*)hdr,
                  (_Float16*)((char*)packed + HDR), NT, (int32_t*)nullptr,
                  x3_Y(packed, N, r), x3_lw(packed, N, r), N, (const int64_t*)nullptr,
-                 (float*)nullptr, 0);
+                 (float*)nullptr, 0, shift_dev);
   ABC_LAUNCHED();
   return ABC_OK;
 }
@@ -785,8 +827,8 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
   const Header* hdr = (const Header*)packed;
   const half8* Aimg = (const half8*)((const char*)packed + HDR);
   ABC_HIP(hipMemsetAsync(nres, 0, sizeof(unsigned int), s));
-  launch_pack<1>(r, dim3((unsigned)ceil_div(p.MTpad * 16, 128)), s, x,
-                 (const double*)nullptr, M, d, mu, U, log_norm - log_const, p.KB0,
+  launch_pack<1>(r, dim3((unsigned)ceil_div(p.MTpad * TR, 128)), s, x,
+                 (const double*)nullptr, M, d, mu, U, log_norm - log_const, p.K0pad,
                  p.KB, hdr, Bimg, p.MTpad, cflags, x3_Y(packed, N, r),
                  x3_lw(packed, N, r), N, hint, hint ? cand_o : (float*)nullptr, r + 6);
   ABC_LAUNCHED();

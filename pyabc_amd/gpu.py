@@ -149,17 +149,43 @@ def normalize_weights(w):
 
 # ---- MultivariateNormalTransition -----------------------------------------
 
-def mvn_pack(X, w, mu, U, shift, prec, with_range=False):
+def mvn_pack(X, w, mu, U, shift, prec, with_range=False, shift_dev=None):
     """Population operand image; with_range also returns the device range
-    [max |y_jk|, max |y_j|^2 / 2] (log2-scaled whitened units)."""
+    [max |y_jk|, max |y_j|^2 / 2] (log2-scaled whitened units).  shift_dev:
+    a device scalar read instead of the host shift (X3 only)."""
     N, d = X.shape
     r = U.shape[1]
     nb = nat.query("abc_mvn_packed_bytes", N, r, prec)
     packed = torch.empty(nb, dtype=torch.uint8, device=X.device)
     rng = torch.empty(2, dtype=F64, device=X.device) if with_range else None
     nat.call("abc_mvn_pack_population", p(X), p(w), N, d, p(mu), p(U), r,
-             float(shift), prec, p(packed), p(rng), stream_ptr())
+             float(shift), p(shift_dev), prec, p(packed), p(rng), stream_ptr())
     return (packed, rng) if with_range else packed
+
+
+def weighted_moments_dev(X, w):
+    """abc_weighted_moments' output left on the device: [sum w, sum w^2,
+    mean (d), biased cov (d x d), max w]."""
+    N, d = X.shape
+    out = torch.empty(3 + d + d * d, dtype=F64, device=X.device)
+    nb = nat.query("abc_weighted_moments_workspace", N, d)
+    ws = workspace(nb)
+    nat.call("abc_weighted_moments", p(X), p(w), N, d, p(out), p(ws), ws.numel(),
+             stream_ptr())
+    return out
+
+
+def mvn_fit(moments, d, scaling, bw_rule):
+    """abc_mvn_fit: (cov, evec, evals, U, L, stats) as device tensors, from
+    weighted_moments_dev's output; no host read."""
+    dev = moments.device
+    blob = torch.empty(4 * d * d + d + 8, dtype=F64, device=dev)
+    cov, evec, U, L = (blob[k * d * d:(k + 1) * d * d].view(d, d) for k in range(4))
+    evals = blob[4 * d * d:4 * d * d + d]
+    stats = blob[4 * d * d + d:]
+    nat.call("abc_mvn_fit", p(moments), d, float(scaling), int(bw_rule), p(cov), p(evec),
+             p(evals), p(U), p(L), p(stats), stream_ptr())
+    return cov, evec, evals, U, L, stats
 
 
 def mvn_logpdf(x, packed, N, mu, U, prec, log_const, out=None, X=None, w=None,

@@ -6,9 +6,15 @@ Reference: pyabc/transition/multivariatenormal.py:40-113.
   rvs  :85-97   ancestor ~ Cat(w), theta = X_j + N(0, Sigma)
   pdf  :99-113  sum_j w_j mvn.pdf(x - X_j)
 
-fit: weighted moments on the device (abc_weighted_moments), eigen-whitening
-of Sigma on the host in fp64 with scipy's _PSD cut-off, population packed
-once into the MFMA operand image (abc_mvn_pack_population).  pdf: the fused
+fit: weighted moments (abc_weighted_moments) and the covariance, its
+eigen-whitening with scipy's _PSD cut-off and the sampling factor
+(abc_mvn_fit: fp64 Jacobi in one workgroup) all on the device, population
+packed once into the MFMA operand image at rank d (abc_mvn_pack_population,
+cut eigen-directions contribute zero columns); the fit reads nothing back --
+its scalars (rank, log pdet, max w) arrive through a pinned async copy read
+at the first density call, which takes the direct kernel if the covariance
+turned out singular.  Custom bandwidth selectors, N = 1 and d > 64 run the
+eigen-whitening on the host as before.  pdf: the fused
 cross-term GEMM + log-sum-exp kernel (abc_mvn_logpdf); singular Sigma (or
 rank > 59) goes through the direct fp64 kernel that applies scipy's support
 mask.  rvs: the Philox proposal kernel with a flat prior.
@@ -35,6 +41,11 @@ def scott_rule_of_thumb(n_samples, dimension):
 def silverman_rule_of_thumb(n_samples, dimension):
     """pyabc/transition/multivariatenormal.py:27-37."""
     return (4 / n_samples / (dimension + 2)) ** (1 / (dimension + 4))
+
+
+# bandwidth rules abc_mvn_fit evaluates on the device (its bw_rule argument)
+def _bw_rule(selector):
+    return {silverman_rule_of_thumb: 0, scott_rule_of_thumb: 1}.get(selector)
 
 
 def psd_whitening(cov):
@@ -82,6 +93,20 @@ class MultivariateNormalTransition(Transition):
         self._X_arr = None
         self.cov = None
         self._normal = None
+        self._fit_future = None
+
+    # the KDE covariance: a host array, fetched from the device fit on use
+    @property
+    def cov(self):
+        if self.__dict__.get("_cov_host") is None and \
+                self.__dict__.get("_dev_cov") is not None:
+            self._cov_host = self._dev_cov.cpu().numpy()
+        return self.__dict__.get("_cov_host")
+
+    @cov.setter
+    def cov(self, value):
+        self._cov_host = value
+        self._dev_cov = None
 
     # -- fit ---------------------------------------------------------------
     def fit(self, X: pd.DataFrame, w: np.ndarray) -> None:
@@ -107,6 +132,78 @@ class MultivariateNormalTransition(Transition):
 
     def _fit_device_arrays(self, Xd, wd):
         N, d = Xd.shape
+        rule = _bw_rule(self.bandwidth_selector)
+        if N == 1 or rule is None or d > 64:
+            return self._fit_host(Xd, wd)
+        # device fit: moments -> cov, eigen-whitening, L (abc_mvn_fit); no
+        # host read here (the GPU may still be busy with the generation's
+        # densities: the host keeps queueing)
+        mom = gpu.weighted_moments_dev(Xd, wd)
+        cov, evec, evals, U, L, stats = gpu.mvn_fit(mom, d, self.scaling, rule)
+        self._cov_host = None
+        self._dev_cov, self._dev_evec, self._dev_evals = cov, evec, evals
+        self._dev_stats = stats
+        self._fit_future = gpu.HostFuture(stats)
+        self._normal = None
+        self._dev_X, self._dev_w = Xd, wd
+        self._dev_mu = mom[2:2 + d]
+        self._dev_L = L
+        self._dev_U = U                       # d x d, cut directions zero
+        self._dev_V = None
+        self._dev_cdf = gpu.inclusive_scan(wd)
+        self._dev_guide = gpu.cdf_guide(self._dev_cdf)
+        self._prec = {"f32": nat.ABC_PREC_F32, "f64": nat.ABC_PREC_F64,
+                      "x3": nat.ABC_PREC_X3}[self.precision]
+        # tentatively full rank; _resolve_fit checks it at the first density
+        self._rank = d
+        self._mfma = d <= self.MFMA_MAX_RANK
+        if self._prec == nat.ABC_PREC_X3 and d > self.X3_MAX_RANK:
+            self._prec = nat.ABC_PREC_F64
+        self._dev_packed = None
+        self._x3_range = None
+        if self._mfma and self._prec == nat.ABC_PREC_X3:
+            # exponents <= 0: the shift -log max w read on the device
+            packed, rng = gpu.mvn_pack(Xd, wd, self._dev_mu, U, 0.0, self._prec,
+                                       with_range=True, shift_dev=stats[3:4])
+            self._dev_packed = packed
+            self._x3_range = gpu.HostFuture(rng)
+        elif self._mfma:
+            self._pack_f64()
+        self._dev_flat_kind, self._dev_flat_params = gpu.flat_prior(d, Xd.device)
+        self._seed = int(np.random.randint(0, 2 ** 62))
+        self._counter = 0
+
+    def _resolve_fit(self):
+        """The device fit's scalars (first use after fit_device): rank, the
+        normalisation, the shift; a singular covariance switches to the direct
+        kernel with scipy's support mask (compact U [d x r] and the null
+        space V); a covariance that is not positive semidefinite raises as
+        scipy's _PSD does (multivariatenormal.py:83)."""
+        fut = self._fit_future
+        if fut is None:
+            return
+        self._fit_future = None
+        st = fut.get()
+        if st[7] == 0:
+            raise ValueError("The input matrix must be symmetric positive "
+                             "semidefinite.")
+        d = self._dev_X.shape[1]
+        rank = int(st[0])
+        self._rank = rank
+        self._log_norm = -0.5 * (rank * gpu.LOG_2PI + float(st[1]))
+        self._support_tol = float(st[2])
+        if self._prec == nat.ABC_PREC_X3 and self._mfma:
+            self._shift = float(st[3])
+        if rank < d or rank == 0:
+            self._mfma = False
+            self._dev_packed = None
+            self._x3_range = None
+            self._dev_U = self._dev_U[:, :rank].contiguous() if rank else None
+            self._dev_V = self._dev_evec[:, rank:].contiguous()
+
+    def _fit_host(self, Xd, wd):
+        """Host eigen-whitening (custom bandwidth selector, N = 1, d > 64)."""
+        N, d = Xd.shape
         sw, sw2, mean, cov_b, wmax = gpu.weighted_moments(Xd, wd, with_max=True)
         self._wmax = float(wmax)
         if N == 1:
@@ -119,6 +216,7 @@ class MultivariateNormalTransition(Transition):
         bw_factor = self.bandwidth_selector(eff_sample_size, d)
         self.cov = sample_cov * bw_factor ** 2 * self.scaling
         self._normal = None
+        self._fit_future = None
         self._set_kernel(Xd, wd, mean)
 
     def _set_kernel(self, Xd, wd, mean):
@@ -175,6 +273,7 @@ class MultivariateNormalTransition(Transition):
                                         self._dev_U, self._shift, self._prec)
 
     def _check_x3_range(self):
+        self._resolve_fit()
         rng = getattr(self, "_x3_range", None)
         if rng is None:
             return

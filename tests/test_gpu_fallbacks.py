@@ -321,17 +321,19 @@ def test_local_transition_d80_generations():
     wide propose kernel, the BIG fit and density): every generation's
     weights equal the oracle's prior / LocalTransition density of the
     previous population, row by row within a first-order rounding bound of
-    the inverses: the 80-D covariances of 100 neighbours have condition
-    numbers kappa_j ~ 1e8..1e10, so the device's LU inverse and LAPACK's
-    differ in each quadratic form q_ij = d^T inv_j d by up to
-    c_n u kappa_j lambda_max(inv_j) |d|^2 and in log det_j by up to
-    c_n u kappa_j d (u = 2^-53, c_n = d, the LU's dimension factor).  A
-    candidate's log density moves by the responsibility-weighted sum of
-    those (r_ij = share of pair j in its density), its normalised log weight
-    by that minus the weighted mean: |dlog w_i| <= b_i + sum_k w_k b_k with
-    b_i = sum_j r_ij c_n u kappa_j (lambda_max_j |d_ij|^2 / 2 + d / 2).
-    The bound is asserted per row; the largest error, its row's bound and
-    the largest ratio are printed (round 5: 1.6e-5 against 3.4e-4 at t = 2)."""
+    the inverses (the 80-D covariances of 100 neighbours have condition
+    numbers up to ~1e10 and beyond).  A backward-stable inverse is the exact
+    inverse of A_j + E_j with |E_j| <= c_n u |A_j| componentwise (u = 2^-53,
+    c_n = d for an LU with small growth), so to first order the quadratic
+    form q_ij = d^T inv_j d moves by |v^T E_j v| <= c_n u |v|^T |A_j| |v|
+    (v = inv_j d_ij) and log det_j by |tr(inv_j E_j)| <= c_n u
+    tr(|inv_j| |A_j|); both the device's LU and LAPACK's are within that
+    of the exact values, hence of each other within twice it.  A
+    candidate's log density moves by the responsibility-weighted sum of the
+    pair terms (r_ij = share of pair j in its density), its normalised log
+    weight by that minus the weighted mean: |dlog w_i| <= b_i + sum_k w_k b_k,
+    b_i = sum_j r_ij 2 c_n u (|v|^T |A_j| |v| + tr(|inv_j| |A_j|)) / 2.
+    Asserted per row; the worst row's error and bound are printed."""
     import pyabc_amd as pa
     d = 80
     names = [f"p{q:02d}" for q in range(d)]
@@ -365,18 +367,20 @@ def test_local_transition_d80_generations():
 def _local_weight_bound(x, Xp, fit, wn):
     """Per-row first-order bound on |dlog w_i| (test_local_transition_d80_generations)."""
     n, d = Xp.shape
-    u = 2.0 ** -53
+    cu = 2.0 * d * 2.0 ** -53
     covs, inv, w = fit["covs"], fit["inv_covs"], fit["w"]
-    kappa = np.linalg.cond(covs)
-    lmax = np.linalg.eigvalsh(inv)[:, -1]
+    absA = np.abs(covs)
+    tr = np.einsum("jab,jba->j", np.abs(inv), absA)
     b = np.empty(len(x))
     for i in range(len(x)):
         dl = Xp - x[i]
-        q = np.einsum("ij,ijk,ik->i", dl, inv, dl)
+        v = np.einsum("jab,jb->ja", inv, dl)
+        q = np.einsum("ja,ja->j", dl, v)
+        vav = np.einsum("ja,jab,jb->j", np.abs(v), absA, np.abs(v))
         lt = np.log(w) - 0.5 * q - np.log(fit["normalization"])
         r = np.exp(lt - lt.max())
         r /= r.sum()
-        b[i] = np.sum(r * d * u * kappa * (0.5 * lmax * (dl * dl).sum(1) + 0.5 * d))
+        b[i] = np.sum(r * cu * 0.5 * (vav + tr))
     return b + np.sum(wn * b)
 
 

@@ -399,7 +399,8 @@ def test_box_muller_accuracy(dev):
     simulator with a = 0, sigma = 1 returns the raw normals) the device
     normals equal the oracle's float32 replay (oracle/philox.py
     normal_pairs) BIT FOR BIT, and are within 4 fp32 ulp of R of an 80-bit
-    long-double evaluation of R cos / R sin, R = sqrt(-2 ln u1)."""
+    long-double evaluation of R cos / R sin, R = sqrt(-2 ln u1), u1 = (a | 1)
+    2^-32 (32-bit u1: normals reach 6.66)."""
     from pyabc_amd import gpu
     from oracle.philox import normal_pairs, philox4x32_10
     B, S = 1 << 20, 4
@@ -413,9 +414,9 @@ def test_box_muller_accuracy(dev):
         ref = np.stack(normal_pairs(r[:, 2 * h], r[:, 2 * h + 1]), 1)
         np.testing.assert_array_equal(x[:, 2 * h:2 * h + 2], ref)
         rr = r.astype(np.uint64)
-        m1 = ((rr[:, 2 * h] >> np.uint64(9)) * 2 + 1).astype(ld)
+        m1 = (rr[:, 2 * h] | np.uint64(1)).astype(ld)
         m2 = ((rr[:, 2 * h + 1] >> np.uint64(9)) * 2 + 1).astype(ld)
-        R = np.sqrt(-2 * np.log(m1 * ld(2.0) ** -24))
+        R = np.sqrt(-2 * np.log(m1 * ld(2.0) ** -32))
         ang = ld("3.14159265358979323846264338327950288") * m2 * ld(2.0) ** -23
         exact = np.stack([(R * np.cos(ang)).astype(np.float64),
                           (R * np.sin(ang)).astype(np.float64)], 1)
