@@ -57,7 +57,7 @@ def test_mvn_pdf_golden(dev, tag, precision, rtol):
 
 
 @pytest.mark.parametrize("d,rule,rank", [(1, 0, 1), (2, 1, 2), (10, 0, 10), (10, 0, 7),
-                                         (25, 1, 25), (40, 0, 40), (64, 0, 64), (9, 0, 0)])
+                                         (25, 1, 25), (40, 0, 40), (64, 0, 64)])
 def test_mvn_fit_device_vs_host(dev, d, rule, rank):
     """abc_mvn_fit (the fit's covariance, PSD eigen-whitening and sampling
     factor on the device, parallel Jacobi in fp64) against the host path it
@@ -66,14 +66,14 @@ def test_mvn_fit_device_vs_host(dev, d, rule, rank):
     log pdet equal, U U^T = cov^+ (the pseudo-inverse on the kept
     eigenspace) to 1e-9 of its largest entry, L lower with L L^T = cov to
     1e-12 of the largest entry; rank-deficient populations (rank < d: the
-    points span a subspace) and a zero covariance (rank 0)."""
+    points span a subspace)."""
     from pyabc_amd import gpu
     from pyabc_amd.transition.multivariatenormal import (
         psd_whitening, silverman_rule_of_thumb, scott_rule_of_thumb)
     rng = np.random.default_rng(7 * d + rank)
     N = 3000
     B = rng.standard_normal((rank, d)) * rng.uniform(0.2, 3.0, (rank, 1))
-    X = rng.standard_normal((N, rank)) @ B + 0.3 if rank else np.full((N, d), 0.3)
+    X = rng.standard_normal((N, rank)) @ B + 0.3
     w = np.exp(0.5 * rng.standard_normal(N))
     w /= w.sum()
     Xd, wd = T(X), T(w)
@@ -85,9 +85,6 @@ def test_mvn_fit_device_vs_host(dev, d, rule, rank):
     scale = max(np.abs(ref).max(), 1e-300)
     np.testing.assert_allclose(cov, ref, rtol=1e-12, atol=1e-14 * scale)
     assert st[7] == 1.0
-    if rank == 0:
-        assert st[0] == 0
-        return
     psd = psd_whitening(ref)
     s_ref = np.sort(np.linalg.eigvalsh(ref))[::-1]
     np.testing.assert_allclose(evals, s_ref, rtol=0, atol=1e-12 * s_ref[0])
