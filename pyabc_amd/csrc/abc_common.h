@@ -43,6 +43,9 @@ struct Carver {
     if (off > cap) ok = false;
     return reinterpret_cast<T*>(base + start);
   }
+  // what is left after the pieces taken so far (256-byte aligned)
+  void* rest() const { return base + align_up(off, 256); }
+  size_t rest_bytes() const { return align_up(off, 256) < cap ? cap - align_up(off, 256) : 0; }
 };
 template <class T> inline void size_only(size_t& off, size_t n) {
   off = align_up(off, 256) + n * sizeof(T);

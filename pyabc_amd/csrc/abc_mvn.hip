@@ -391,7 +391,8 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
               const double* X, const double* w, int64_t N, const double* mu,
               const double* U, int r, double log_const, double log_norm,
               double* out, const int64_t* hint, void* ws, size_t ws_bytes,
-              hipStream_t s, int prof_channel = ABC_PROF_DENSITY);
+              hipStream_t s, int prof_channel = ABC_PROF_DENSITY,
+              const unsigned int* count_dev = nullptr);
 }  // namespace abc
 
 using namespace abc;

@@ -25,9 +25,10 @@
 namespace abc {
 namespace {
 
-constexpr int FT = 256;
 constexpr int FD = 64;
 
+// FT threads: one wave for d <= 16 (its barriers are nearly free), four above
+template <int FT>
 __global__ __launch_bounds__(FT) void mvn_fit_kernel(const double* __restrict__ mom, int d,
                                                      double scaling, int rule,
                                                      double* __restrict__ cov_out,
@@ -209,8 +210,12 @@ extern "C" int abc_mvn_fit(const double* moments, int d, double scaling, int bw_
   ABC_CHECK_ARG(d >= 1 && d <= FD, "mvn_fit: d=%d outside [1, %d]", d, FD);
   ABC_CHECK_ARG(bw_rule == 0 || bw_rule == 1, "mvn_fit: bw_rule %d", bw_rule);
   ABC_CHECK_ARG(moments && cov && evec && evals && U && L && stats, "mvn_fit: null pointer");
-  hipLaunchKernelGGL(mvn_fit_kernel, dim3(1), dim3(FT), 0, as_stream(stream), moments, d,
-                     scaling, bw_rule, cov, evec, evals, U, L, stats);
+  if (d <= 16)
+    hipLaunchKernelGGL(mvn_fit_kernel<64>, dim3(1), dim3(64), 0, as_stream(stream), moments,
+                       d, scaling, bw_rule, cov, evec, evals, U, L, stats);
+  else
+    hipLaunchKernelGGL(mvn_fit_kernel<256>, dim3(1), dim3(256), 0, as_stream(stream), moments,
+                       d, scaling, bw_rule, cov, evec, evals, U, L, stats);
   ABC_LAUNCHED();
   return ABC_OK;
 }

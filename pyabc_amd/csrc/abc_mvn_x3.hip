@@ -230,9 +230,12 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
     _Float16* __restrict__ img, int64_t ntiles, int32_t* __restrict__ flags,
     double* __restrict__ Y, double* __restrict__ lw, int64_t Np,
     const int64_t* __restrict__ hint, float* __restrict__ cand_o, int koff,
-    const double* __restrict__ shift_dev) {
+    const double* __restrict__ shift_dev, const unsigned int* __restrict__ count_dev) {
   // SIDE 0 writes the fp64 whitened population Y [n x r] and its log2
-  // weights lw [n] (rescue + hints); SIDE 1 reads them for the hint rows
+  // weights lw [n] (rescue + hints); SIDE 1 reads them for the hint rows.
+  // count_dev (SIDE 1, nullable): only the first *count_dev of the n rows
+  // are candidates (a device-sized launch), the rest are padding
+  if (count_dev) { const int64_t c = (int64_t)*count_dev; n = c < n ? c : n; }
   constexpr int RR = R > 0 ? R : MAX_R;
   const int r = R > 0 ? R : r_rt;
   const int K0pad = R > 0 ? x3_k0pad(R) : K0pad_rt;
@@ -240,6 +243,8 @@ __global__ __launch_bounds__(128) void pack_x3_kernel(
   constexpr int NG = R > 0 ? x3_kb(R) * 2 : 0;  // 8-slot groups
   const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (row >= ntiles * TR) return;
+  // tiles wholly past the count are never read (the waves that own them leave)
+  if (count_dev && (row / TR) * TR >= n) return;
   const int E = hdr->E;
   const bool ok = hdr->ok != 0;
   const double L2 = ldexp(1.0, 2 * E);  // 2^(2E): bound of |y|^2 and |c|
@@ -331,7 +336,8 @@ template <int KB, int CT, bool PASS1>
 __global__ __launch_bounds__(256) void mvn_x3_kernel(
     const half8* __restrict__ A, const half8* __restrict__ Bi, int64_t MT,
     int64_t NT, int nchunk, int64_t tiles_per_chunk, int64_t ngroups, int koff, int kb0,
-    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad) {
+    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad,
+    const unsigned int* __restrict__ count_dev) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int64_t bid = blockIdx.x;
@@ -341,6 +347,9 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
   const int64_t group = jb / cpx;
   if (group >= ngroups) return;
   const int64_t ct0 = (group * 4 + wave) * CT;
+  // a device-sized launch: waves past the candidate count leave at once (no
+  // barrier in this kernel)
+  if (count_dev && ct0 * TR >= (int64_t)*count_dev) return;
   // which lanes / instruction / element of the B fragments hold the offset slot
   const bool off_lane = (lane >> 5) == ((koff >> 3) & 1);
   const int off_kb = koff >> 4, off_j = koff & 7;
@@ -494,9 +503,10 @@ __global__ void x3_combine_kernel(const double* __restrict__ part_o,
                                   const float* __restrict__ cand_o,
                                   double* __restrict__ out,
                                   int64_t* __restrict__ rescue,
-                                  unsigned int* __restrict__ nrescue) {
+                                  unsigned int* __restrict__ nrescue,
+                                  const unsigned int* __restrict__ count_dev) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= M) return;
+  if (i >= M || (count_dev && i >= (int64_t)*count_dev)) return;
   double om = -INFINITY;
   double s = 0.0;
   if (cand_o) {  // one offset per candidate (hinted launch): plain sum
@@ -635,12 +645,13 @@ void launch_pack(int r, dim3 grid, hipStream_t s, const double* P, const double*
                  double log_w_shift, int K0pad, int KB, const Header* hdr,
                  _Float16* img, int64_t ntiles, int32_t* flags, double* Y,
                  double* lw, int64_t Np, const int64_t* hint, float* cand_o,
-                 int koff, const double* shift_dev = nullptr) {
+                 int koff, const double* shift_dev = nullptr,
+                 const unsigned int* count_dev = nullptr) {
 #define ABC_PACK_CASE(RC)                                                          \
   case RC:                                                                         \
     hipLaunchKernelGGL((pack_x3_kernel<SIDE, RC>), grid, dim3(128), 0, s, P, w, n, \
                        d, mu, U, r, log_w_shift, K0pad, KB, hdr, img, ntiles, flags, \
-                       Y, lw, Np, hint, cand_o, koff, shift_dev);                  \
+                       Y, lw, Np, hint, cand_o, koff, shift_dev, count_dev);       \
     break;
   switch (r) {
     ABC_PACK_CASE(1) ABC_PACK_CASE(2) ABC_PACK_CASE(3) ABC_PACK_CASE(4)
@@ -653,18 +664,20 @@ void launch_pack(int r, dim3 grid, hipStream_t s, const double* P, const double*
 
 // rows of the rescued candidates (x [M x d] -> xs [n x d]) and their
 // densities back (outs [n] -> out at the rescued positions)
-__global__ void x3_gather_rescued(const int64_t* __restrict__ rescue, int64_t n,
+__global__ void x3_gather_rescued(const int64_t* __restrict__ rescue,
+                                  const unsigned int* __restrict__ nres,
                                   const double* __restrict__ x, int d,
                                   double* __restrict__ xs) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * d) return;
+  if (e >= (int64_t)*nres * d) return;
   xs[e] = x[rescue[e / d] * d + e % d];
 }
-__global__ void x3_scatter_rescued(const int64_t* __restrict__ rescue, int64_t n,
+__global__ void x3_scatter_rescued(const int64_t* __restrict__ rescue,
+                                   const unsigned int* __restrict__ nres,
                                    const double* __restrict__ outs,
                                    double* __restrict__ out) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q < n) out[rescue[q]] = outs[q];
+  if (q < (int64_t)*nres) out[rescue[q]] = outs[q];
 }
 
 // candidate tiles (32 columns) per wave for KB MFMA instructions per tile
@@ -717,23 +730,26 @@ size_t plan_x3_ws(const PlanX3& p) {
 
 template <int KB, int CT>
 void launch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
-               double* po, double* pl, bool pass1, hipStream_t s) {
+               double* po, double* pl, bool pass1, const unsigned int* count_dev,
+               hipStream_t s) {
   static_assert(CT == x3_ct(KB), "the plan's tiles per wave must match the instantiation");
   const int64_t blocks = p.groups * p.nchunk;
   if (pass1)
     hipLaunchKernelGGL((mvn_x3_kernel<KB, CT, true>), dim3((unsigned)blocks),
                        dim3(256), 0, s, A, B, p.MT, p.NT, p.nchunk,
-                       p.tiles_per_chunk, p.groups, koff, p.KB0, po, pl, p.Mpad);
+                       p.tiles_per_chunk, p.groups, koff, p.KB0, po, pl, p.Mpad, count_dev);
   else
     hipLaunchKernelGGL((mvn_x3_kernel<KB, CT, false>), dim3((unsigned)blocks),
                        dim3(256), 0, s, A, B, p.MT, p.NT, p.nchunk,
-                       p.tiles_per_chunk, p.groups, koff, p.KB0, po, pl, p.Mpad);
+                       p.tiles_per_chunk, p.groups, koff, p.KB0, po, pl, p.Mpad, count_dev);
 }
 
 int dispatch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
-                double* po, double* pl, bool pass1, hipStream_t s) {
+                double* po, double* pl, bool pass1, const unsigned int* count_dev,
+                hipStream_t s) {
   switch (p.KB) {
-#define ABC_X3_CASE(K) case K: launch_x3<K, x3_ct(K)>(p, A, B, koff, po, pl, pass1, s); break;
+#define ABC_X3_CASE(K) \
+  case K: launch_x3<K, x3_ct(K)>(p, A, B, koff, po, pl, pass1, count_dev, s); break;
     ABC_X3_CASE(2) ABC_X3_CASE(3) ABC_X3_CASE(4) ABC_X3_CASE(5) ABC_X3_CASE(6)
     ABC_X3_CASE(7) ABC_X3_CASE(8) ABC_X3_CASE(9) ABC_X3_CASE(10) ABC_X3_CASE(11)
 #undef ABC_X3_CASE
@@ -800,15 +816,25 @@ int x3_pack_population(const double* X, const double* w, int64_t N, int d,
   return ABC_OK;
 }
 
+// the main launch's plan, then (hinted calls) room for the nested exact
+// pass over up to all M candidates: their rows, results and its own plan
 size_t x3_logpdf_workspace(int64_t M, int64_t N, int r) {
-  return plan_x3_ws(make_plan_x3(M, N, r));
+  const size_t main = plan_x3_ws(make_plan_x3(M, N, r));
+  const int64_t m1 = M > 0 ? M : 1;
+  size_t nested = 0;
+  size_only<double>(nested, (size_t)m1 * 64);           // rows (d <= 64)
+  size_only<double>(nested, (size_t)m1);                // results
+  size_only<char>(nested, main);                        // the nested plan
+  return main + nested + 256;
 }
 
+// count_dev (nullable): a device-sized launch -- only the first *count_dev
+// of the M rows of x are candidates (the nested rescue pass below)
 int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
               const double* X, const double* w, int64_t N, const double* mu,
               const double* U, int r, double log_const, double log_norm,
               double* out, const int64_t* hint, void* ws, size_t ws_bytes,
-              hipStream_t s, int prof_channel) {
+              hipStream_t s, int prof_channel, const unsigned int* count_dev) {
   if (r > MAX_R)
     return set_error(ABC_ERR_UNSUPPORTED, "mvn x3: rank %d > %d", r, MAX_R);
   PlanX3 p = make_plan_x3(M, N, r);
@@ -830,48 +856,45 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
   launch_pack<1>(r, dim3((unsigned)ceil_div(p.MTpad * TR, 128)), s, x,
                  (const double*)nullptr, M, d, mu, U, log_norm - log_const, p.K0pad,
                  p.KB, hdr, Bimg, p.MTpad, cflags, x3_Y(packed, N, r),
-                 x3_lw(packed, N, r), N, hint, hint ? cand_o : (float*)nullptr, r + 6);
+                 x3_lw(packed, N, r), N, hint, hint ? cand_o : (float*)nullptr, r + 6,
+                 (const double*)nullptr, count_dev);
   ABC_LAUNCHED();
   profile_start(s, prof_channel);
-  int rc = dispatch_x3(p, Aimg, (const half8*)Bimg, r + 6, po, pl, hint == nullptr, s);
+  int rc = dispatch_x3(p, Aimg, (const half8*)Bimg, r + 6, po, pl, hint == nullptr,
+                       count_dev, s);
   profile_stop(s, prof_channel);
   if (rc) return rc;
   ABC_LAUNCHED();
   hipLaunchKernelGGL(x3_combine_kernel, dim3((unsigned)ceil_div(M, 256)), dim3(256),
                      0, s, po, pl, p.nchunk, M, p.Mpad, log_const, cflags,
                      hint ? (const float*)cand_o : (const float*)nullptr, out,
-                     rescue, nres);
+                     rescue, nres, count_dev);
   ABC_LAUNCHED();
   if (hint) {
     // Hinted candidates whose ancestor offset was far below their true
     // maximum (or outside the limb range / underflowing) are re-run through
-    // the unhinted pass -- exact max pre-pass, still MFMA -- on a gathered
-    // subset, in the partial arrays freed by the combine.  One host read of
-    // their count; a candidate's result stays independent of M and of its
-    // position (same chunking), so sharded runs keep identical bits.
-    unsigned int nh = 0;
-    ABC_HIP(hipMemcpyAsync(&nh, nres, sizeof(nh), hipMemcpyDeviceToHost, s));
-    ABC_HIP(hipStreamSynchronize(s));
-    if (nh == 0) return ABC_OK;
-    const size_t free_bytes = (size_t)p.nchunk * p.Mpad * sizeof(double) * 2;
-    Carver sub(po, free_bytes);
-    double* xs = sub.take<double>((size_t)nh * d);
-    double* outs = sub.take<double>((size_t)nh);
-    const size_t need = plan_x3_ws(make_plan_x3(nh, N, r));
-    void* ws2 = sub.take<char>(need + 256);
-    if (sub.ok) {
-      hipLaunchKernelGGL(x3_gather_rescued, dim3((unsigned)ceil_div((int64_t)nh * d, 256)),
-                         dim3(256), 0, s, rescue, (int64_t)nh, x, d, xs);
-      ABC_LAUNCHED();
-      const int rc2 = x3_logpdf(xs, nh, d, packed, X, w, N, mu, U, r, log_const, log_norm,
-                                outs, nullptr, ws2, need + 256, s, ABC_PROF_RESCUE);
-      if (rc2) return rc2;
-      hipLaunchKernelGGL(x3_scatter_rescued, dim3((unsigned)ceil_div(nh, 256)), dim3(256), 0,
-                         s, rescue, (int64_t)nh, outs, out);
-      ABC_LAUNCHED();
-      return ABC_OK;
-    }
-    // (more than ~1/4 of the launch rescued: the fp64 path below)
+    // the unhinted pass -- exact max pre-pass, still MFMA -- on the gathered
+    // rescue list.  The list's length stays on the device: the nested pass
+    // is launched for all M and its waves past the count leave at once, so
+    // the call never waits for the GPU.  A candidate's result is independent
+    // of M, of its slot in the list and of the list's length (chunking by N
+    // only), so sharded runs keep identical bits.
+    Carver sub(cv.rest(), cv.rest_bytes());
+    double* xs = sub.take<double>((size_t)M * d);
+    double* outs = sub.take<double>((size_t)M);
+    const size_t need = plan_x3_ws(make_plan_x3(M, N, r));
+    void* ws2 = sub.take<char>(need);
+    if (!sub.ok) return set_error(ABC_ERR_WORKSPACE, "mvn x3: nested rescue workspace");
+    hipLaunchKernelGGL(x3_gather_rescued, dim3((unsigned)ceil_div(M * d, 256)),
+                       dim3(256), 0, s, rescue, nres, x, d, xs);
+    ABC_LAUNCHED();
+    const int rc2 = x3_logpdf(xs, M, d, packed, X, w, N, mu, U, r, log_const, log_norm,
+                              outs, nullptr, ws2, need, s, ABC_PROF_RESCUE, nres);
+    if (rc2) return rc2;
+    hipLaunchKernelGGL(x3_scatter_rescued, dim3((unsigned)ceil_div(M, 256)), dim3(256), 0,
+                       s, rescue, nres, outs, out);
+    ABC_LAUNCHED();
+    return ABC_OK;
   }
   // fp64 rescue of the listed candidates (count on the device): launch
   // pairs over slot ranges of the partial arrays' capacity; pairs past the

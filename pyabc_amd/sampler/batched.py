@@ -614,12 +614,7 @@ class BatchedGPUSampler(Sampler):
                 # kept rows regenerated straight into one per-generation
                 # buffer (rows of later rounds follow): no concatenation
                 if kept is None or kept_off + k_mine > kept[0].shape[0]:
-                    cap = max(n - n_acc, k_mine)
-                    kept = (torch.empty((cap, fr.d), dtype=gpu.F64, device=dev),
-                            torch.empty(cap, dtype=gpu.F64, device=dev),
-                            torch.empty(cap, dtype=torch.int64, device=dev),
-                            torch.empty((cap, S), dtype=gpu.F64, device=dev),
-                            torch.empty(cap, dtype=gpu.F64, device=dev))
+                    kept = self._kept_buffers(max(n - n_acc, k_mine), fr.d, S, dev)
                     kept_off = 0
                 th, lp, anc, x, dist = fr.regen(
                     lo, idx[:k_mine], out=tuple(a[kept_off:kept_off + k_mine] for a in kept))
@@ -672,6 +667,31 @@ class BatchedGPUSampler(Sampler):
             recorded = out.sum_stats
         return ColumnarSample(out, recorded, spec.sum_stat_keys, record,
                               ok and n_acc == n)
+
+    # population columns of the fused rounds are carved from pooled device
+    # arenas: a generation's new population (kept by the History) would
+    # otherwise need fresh allocations -- a hipMalloc and its host stall --
+    # every generation
+    _POOL_BYTES = 1 << 28
+
+    def _kept_buffers(self, cap, d, S, dev):
+        """theta [cap, d], lp, anc (int64), x [cap, S], dist as views of one
+        pooled fp64 arena."""
+        torch = gpu.torch
+        pieces = (((cap, d), cap * d), ((cap,), cap), ((cap,), cap),
+                  ((cap, S), cap * S), ((cap,), cap))
+        need = sum(n_el + (-n_el) % 32 for _, n_el in pieces)   # 256-byte aligned
+        pool, off = getattr(self, "_pool", (None, 0))
+        if pool is None or pool.device != dev or off + need > pool.numel():
+            pool = torch.empty(max(need, self._POOL_BYTES // 8), dtype=gpu.F64, device=dev)
+            off = 0
+        views = []
+        for shape, n_el in pieces:
+            views.append(pool[off:off + n_el].view(shape))
+            off += n_el + (-n_el) % 32
+        views[2] = views[2].view(torch.int64)
+        self._pool = (pool, off)
+        return tuple(views)
 
     def _gather_recorded(self, pieces, rec_keeps, dev, ws):
         """Concatenate this rank's recorded rows and, over several ranks,

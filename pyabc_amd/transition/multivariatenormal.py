@@ -172,6 +172,10 @@ class MultivariateNormalTransition(Transition):
         self._dev_flat_kind, self._dev_flat_params = gpu.flat_prior(d, Xd.device)
         self._seed = int(np.random.randint(0, 2 ** 62))
         self._counter = 0
+        # the fused rounds' ancestor table, queued with the fit (it would
+        # otherwise be built at the next generation's first round, on the
+        # critical path between the epsilon read and the first launch)
+        self._ancestor_table()
 
     def _resolve_fit(self):
         """The device fit's scalars (first use after fit_device): rank, the
