@@ -384,6 +384,7 @@ def main():
     if "t1" not in clock:
         raise RuntimeError("run stopped before the timed generations finished")
     elapsed = clock["t1"] - clock["t0"]
+    elapsed_local = elapsed
     k_ms, k_n, k_flops, k_pairs = clock["kernel"]
     n_before = clock["n0"]
     gens = abc.generation_log[n_before:n_before + args.steps]
@@ -444,7 +445,18 @@ def main():
     avg_m = k_pairs / max(k_n, 1) / n_pop if k_n else 0
     algo_bytes = ((n_pop + avg_m) * kpad * 2 + avg_m * 8) if args.precision == "x3" else None
     out = None
+    stages_per_rank = None
     if ws > 1:
+        # each rank's own stage split (its density launches, candidate
+        # rounds, ...) so a scaling line can be read from its own output
+        mine = {k: (round(v, 3) if isinstance(v, float) else v)
+                for k, v in stages.items() if k != "note"}
+        mine["other_ms"] = round(1e3 * elapsed_local - k_ms - c_ms - r_ms - x_ms, 3)
+        mine.update(rank=rank, elapsed_ms=round(1e3 * elapsed_local, 3),
+                    density_launches=k_n, candidate_launches=c_n)
+        box = [None] * ws
+        torch.distributed.all_gather_object(box, mine)
+        stages_per_rank = box
         # every rank is done with the GPU; rank 0 alone times the host leg
         torch.distributed.destroy_process_group()
     if rank == 0:
@@ -502,6 +514,7 @@ def main():
             "acceptance_rate_last": n_pop / gens[-1]["n_sim"] if gens else None,
             "generation_ms": [round(1e3 * g["seconds"], 3) for g in gens],
             "stages": stages,
+            "stages_per_rank": stages_per_rank,
             "candidate_kernel": cand,
             "roofline": {"bound": "mfma", "kernel": kname[args.precision],
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s",

@@ -329,3 +329,83 @@ def test_cutoff_prefix():
     np.testing.assert_array_equal(cutoff([0, 0], 3), [0, 0])
     np.testing.assert_array_equal(cutoff([4, 4], 8), [4, 4])
     assert rank_range(100, 10, 3) == (130, 140)
+
+
+def _nccl_branch_worker(rank, ws, port, out_dir):
+    """The sampler's collectives with dist.get_backend() reporting "nccl",
+    so all_gather_flat takes its RCCL branch (no host staging: the tensors
+    go to all_gather_into_tensor as given); a gloo stand-in underneath
+    checks every call the way RCCL would take it -- contiguous buffers of
+    one dtype on one device, out = world_size x the input along dim 0 --
+    then performs it."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    calls = []
+    real_into, real_list = dist.all_gather_into_tensor, dist.all_gather
+    try:
+        from pyabc_amd.sampler import distributed as dd
+
+        def into(out, t, *a, **k):
+            assert out.is_contiguous() and t.is_contiguous()
+            assert out.dtype == t.dtype and out.device == t.device
+            assert out.shape[0] == ws * t.shape[0] and out.shape[1:] == t.shape[1:]
+            calls.append(("into", tuple(t.shape), str(t.dtype)))
+            return real_into(out, t, *a, **k)
+
+        def lst(outs, t, *a, **k):
+            assert len(outs) == ws and t.is_contiguous()
+            assert all(o.shape == t.shape and o.dtype == t.dtype for o in outs)
+            calls.append(("list", tuple(t.shape), str(t.dtype)))
+            return real_list(outs, t, *a, **k)
+        dist.all_gather_into_tensor, dist.all_gather = into, lst
+        dist.get_backend = lambda *a, **k: "nccl"
+        dev = torch.device("cpu")
+        # ragged keeps over 3 rounds: ranks with nothing in a round, one rank
+        # with nothing at all; rows carry their global order number
+        rng = np.random.default_rng(ws)
+        keeps = rng.integers(0, 4, (3, ws))
+        keeps[:, ws - 1] = 0
+        keeps[1, 0] = 0
+        order = np.arange(keeps.sum())
+        mine, o = [], 0
+        for r in range(keeps.shape[0]):
+            for q in range(ws):
+                if q == rank:
+                    mine.extend(order[o:o + keeps[r, q]])
+                o += keeps[r, q]
+        g = torch.tensor(mine, dtype=torch.float64).reshape(-1)
+        cols = [torch.stack([g, -g], 1), g + 0.5, torch.stack([g] * 4, 1)]
+        (th, w, x), ex = dd.allgather_rows_ordered(
+            cols, keeps, dev, extra=torch.tensor([float(100 + rank)], dtype=torch.float64))
+        counts = dd.allgather_counts(torch.tensor([5 * rank + 1]), dev)
+        np.savez(os.path.join(out_dir, f"n{rank}.npz"), th=th.numpy(), w=w.numpy(),
+                 x=x.numpy(), ex=ex, counts=counts, n=np.array(len(order)),
+                 calls=np.array([f"{a}:{b}:{c}" for a, b, c in calls]))
+    finally:
+        dist.all_gather_into_tensor, dist.all_gather = real_into, real_list
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws", [2, 8])
+def test_nccl_branch_collectives(ws):
+    """The RCCL code path of the packed row gather and the count gather
+    (sampler/distributed.py all_gather_flat with backend "nccl") at world
+    size 2 and 8, through a gloo stand-in that asserts RCCL's buffer
+    contract on every call: one all_gather_into_tensor of the packed
+    [rows x (2 + 1 + 4)] f64 buffer (+ the cutoff row), one list all_gather
+    of the int64 counts; every rank gets the rows in global order and the
+    extras in rank order."""
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_nccl_branch_worker, args=(ws, _free_port(), tmp),
+                           nprocs=ws, join=True, start_method="spawn")
+        for rank in range(ws):
+            r = np.load(os.path.join(tmp, f"n{rank}.npz"))
+            g = np.arange(int(r["n"]), dtype=np.float64)
+            np.testing.assert_array_equal(r["th"], np.stack([g, -g], 1))
+            np.testing.assert_array_equal(r["w"], g + 0.5)
+            np.testing.assert_array_equal(r["x"], np.stack([g] * 4, 1))
+            np.testing.assert_array_equal(r["ex"], 100.0 + np.arange(ws))
+            np.testing.assert_array_equal(r["counts"], 5 * np.arange(ws) + 1)
+            calls = list(r["calls"])
+            assert [c.split(":")[0] for c in calls] == ["into", "list"], calls
+            assert calls[0].endswith("torch.float64") and calls[1].endswith("torch.int64")
