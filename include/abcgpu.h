@@ -303,7 +303,10 @@ int abc_ancestor_table(const double* X, const double* cdf, int64_t N, int d,
                        void* table, size_t table_bytes, void* stream);
 /* One round of B candidates: writes the positions b (0 <= b < B, increasing)
  * of the first `cap` accepted candidates to idx and the number accepted in
- * the round (uncapped) to *count (device int64).  rec_x (nullable) receives
+ * the round (uncapped) to *count (device int64).  The threshold is eps, or,
+ * when eps_dev (device, nullable) is given, *eps_dev * eps_scale read on the
+ * device (QuantileEpsilon's quantile x its multiplier, so the round can be
+ * queued before the host has the value).  rec_x (nullable) receives
  * the sum stats of every candidate [B x S] (record_rejected).  filter != 0
  * allows the exact early-rejection mode (first 4 statistics, p in {1,2,inf},
  * no rec_x; for the shared-L transition with every coordinate beyond the
@@ -311,7 +314,8 @@ int abc_ancestor_table(const double* X, const double* cdf, int64_t N, int d,
  * the same accept set at lower cost when few candidates pass. */
 size_t abc_candidates_workspace(int64_t B);
 int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0,
-                         int64_t B, double eps, int filter, int64_t cap,
+                         int64_t B, double eps, const double* eps_dev,
+                         double eps_scale, int filter, int64_t cap,
                          int64_t* idx, int64_t* count, double* rec_x,
                          void* ws, size_t ws_bytes, void* stream);
 /* Rows of the kept candidates: for i < n, candidate idx0 + idx[i] ->

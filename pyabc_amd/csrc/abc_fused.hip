@@ -35,6 +35,8 @@ struct RoundArgs {
   ProposalArgs P;
   SimDistArgs M;
   const double* box;  // prior support [d x (lo, hi)] (support_box_kernel)
+  const double* eps_dev;   // nullable: threshold *eps_dev * eps_scale
+  double eps_scale;
 };
 
 // Full evaluation of candidate g: proposal + simulation + distance.  Returns
@@ -102,9 +104,12 @@ __device__ __forceinline__ double evaluate_staged(const RoundArgs& A, const Bloc
 
 template <int D, int MODE, bool FILTER, int PK>
 __device__ __forceinline__ void round_body(
-    RoundArgs A, int64_t idx0, int64_t B, double eps,
+    RoundArgs A, int64_t idx0, int64_t B, double eps_host,
     uint64_t* __restrict__ bits, int64_t* __restrict__ tile_cnt,
     double* __restrict__ rec_x) {
+  // the threshold read on the device (the host's float(q) * multiplier, one
+  // IEEE product either way)
+  const double eps = A.eps_dev ? (*A.eps_dev) * A.eps_scale : eps_host;
   constexpr bool filter = FILTER;
   constexpr int DM = D > 0 ? D : 64;
   __shared__ BlockConsts C;
@@ -617,6 +622,8 @@ inline AncTable anc_table_view(const void* t, int64_t N, int d) {
 RoundArgs round_args(const abc_candidate_spec* s, const double* box) {
   RoundArgs A;
   A.box = box;
+  A.eps_dev = nullptr;
+  A.eps_scale = 1.0;
   A.P = ProposalArgs{s->X, s->cdf, s->guide, s->N, s->L, s->prior_kind,
                      s->prior_params, s->d, s->max_attempts, s->seed, s->generation};
   if (s->X && s->anc_table) {
@@ -728,7 +735,8 @@ extern "C" int abc_ancestor_table(const double* X, const double* cdf, int64_t N,
 }
 
 extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0,
-                                    int64_t B, double eps, int filter, int64_t cap,
+                                    int64_t B, double eps, const double* eps_dev,
+                                    double eps_scale, int filter, int64_t cap,
                                     int64_t* idx, int64_t* count, double* rec_x,
                                     void* ws, size_t ws_bytes, void* stream) {
   const int rc = check_spec(spec);
@@ -758,7 +766,9 @@ extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0
   hipLaunchKernelGGL(support_box_kernel, dim3((unsigned)spec->d), dim3(64), 0, s,
                      spec->prior_kind, spec->prior_params, spec->d, box);
   ABC_LAUNCHED();
-  const RoundArgs A = round_args(spec, box);
+  RoundArgs A = round_args(spec, box);
+  A.eps_dev = eps_dev;
+  A.eps_scale = eps_scale;
   ABC_CHECK_ARG(nt < (1ll << 31), "candidates_round: too many tiles");
   profile_start(s, ABC_PROF_CANDIDATES);
   const bool p2 = p == 2.0;

@@ -110,17 +110,28 @@ class QuantileEpsilon(Epsilon):
         q = gpu.weighted_quantile(d, w, self.alpha)
         # read back lazily: __call__(t) is the first consumer
         self._look_up[t] = _PendingEps(gpu.HostFuture(q), self.quantile_multiplier,
-                                       (d, w, self.alpha))
+                                       (d, w, self.alpha), q)
+
+    def device_threshold(self, t):
+        """(device quantile, multiplier) of generation t while its value is
+        still on the way to the host -- the fused candidate round reads the
+        threshold q * multiplier on the device, so it can be queued behind
+        the quantile kernel -- else None."""
+        eps = self._look_up.get(t) if self._look_up else None
+        if isinstance(eps, _PendingEps) and eps.q_dev is not None:
+            return eps.q_dev, eps._mult, eps._fut
+        return None
 
 
 class _PendingEps:
     """Quantile of the device kernel, resolved to a float on first use (an
     undecided select reruns on the sort-based kernel, gpu.resolve_quantile)."""
 
-    def __init__(self, fut, multiplier, inputs=None):
+    def __init__(self, fut, multiplier, inputs=None, q_dev=None):
         self._fut = fut
         self._mult = multiplier
         self._inputs = inputs
+        self.q_dev = q_dev
 
     def value(self):
         v = self._fut.get()[0]

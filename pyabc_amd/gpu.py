@@ -384,9 +384,11 @@ class CandidateRound:
         self.device = prior_params.device
 
     def run(self, idx0, B, eps, cap, filter=True, rec_x=None, idx_out=None,
-            count_out=None):
+            count_out=None, eps_dev=None, eps_scale=1.0):
         """One round (abc_candidates_round): (idx [cap] int64 positions of the
-        first cap accepted, count [1] int64 accepted in the round)."""
+        first cap accepted, count [1] int64 accepted in the round).  eps_dev
+        (device scalar, optional): the threshold is eps_dev * eps_scale, read
+        on the device."""
         import ctypes as C
         idx = (torch.empty(max(int(cap), 1), dtype=I64, device=self.device)
                if idx_out is None else idx_out)
@@ -397,7 +399,8 @@ class CandidateRound:
         nb = nat.query("abc_candidates_workspace", int(B))
         ws = workspace(nb, "candidates")
         nat.call("abc_candidates_round", C.addressof(self.spec), int(idx0), int(B),
-                 float(eps), int(bool(filter)), int(cap), p(idx), p(cnt), p(rec_x),
+                 float(eps), p(eps_dev), float(eps_scale), int(bool(filter)), int(cap),
+                 p(idx), p(cnt), p(rec_x),
                  p(ws), ws.numel(), stream_ptr())
         return idx, cnt
 

@@ -585,7 +585,15 @@ class BatchedGPUSampler(Sampler):
             filt = (rate is not None and rate < self.filter_below and rx is None
                     and self._lazy_capable(spec, fr))
             filtered += int(filt)
-            idx, cnt = fr.run(lo, B, spec.eps, cap=need, filter=filt, rec_x=rx)
+            # the generation's first round takes the threshold on the device
+            # (queued behind the quantile kernel, no host wait); later rounds
+            # the host value, which has arrived by then
+            thr = spec.eps_device if rounds == 0 else None
+            if thr is not None:
+                idx, cnt = fr.run(lo, B, 0.0, cap=need, filter=filt, rec_x=rx,
+                                  eps_dev=thr[0], eps_scale=thr[1])
+            else:
+                idx, cnt = fr.run(lo, B, spec.eps, cap=need, filter=filt, rec_x=rx)
             if ws == 1:
                 # one read: the count and the index of the need-th accepted
                 kk = min(need, B)
@@ -594,6 +602,15 @@ class BatchedGPUSampler(Sampler):
             else:
                 cnt_local = cnt
             counts = dd.allgather_counts(cnt_local, dev)
+            if thr is not None:
+                spec.eps_device = None
+                if np.isnan(thr[2].get()[0]):
+                    # the select left the quantile undecided (knots in a tie
+                    # run): the round ran at a NaN threshold and accepted
+                    # nothing; run the same candidates again at the host
+                    # value (the sort-based rerun, gpu.resolve_quantile)
+                    spec.eps
+                    continue
             keep = dd.cutoff(counts, need)
             total_keep = int(keep.sum())
             k_mine = int(keep[rank])

@@ -58,7 +58,12 @@ class GenerationSpec:
         self.weight_scale = 1.0 / self.nr_samples_per_parameter
         self.transition = None if (t <= 0 or all_accepted) else abc.transitions[0]
         self.distance = None if all_accepted else abc.distance_function
-        self.eps = None if all_accepted else abc.eps(t)
+        # the threshold on the host is read on first use (the fused rounds
+        # take it on the device, eps_device, and need the host value only
+        # after their first round)
+        self._eps = None
+        dev_thr = getattr(abc.eps, "device_threshold", None)
+        self.eps_device = None if (all_accepted or dev_thr is None) else dev_thr(t)
         self.sum_stat_keys = list(abc.x_0.keys())
         # StochasticAcceptor: (pdf_norm, temperature, log scale, importance
         # weighting) of this generation for abc_stochastic_accept
@@ -67,6 +72,14 @@ class GenerationSpec:
             self.stochastic = abc.acceptor.device_config(t, self.eps)
         self._closure = None
         self._init_device(abc)
+
+    @property
+    def eps(self):
+        if self.all_accepted:
+            return None
+        if self._eps is None:
+            self._eps = self._abc.eps(self.t)
+        return self._eps
 
     def _init_device(self, abc):
         why = []
@@ -527,8 +540,9 @@ class ABCSMC:
         t_max = t0 + max_nr_populations - 1
         t = t0
         while t <= t_max:
-            current_eps = self.eps(t)
-            logger.info(f"t: {t}, eps: {current_eps}.")
+            # the threshold is read after the sample: the fused rounds take
+            # it on the device (GenerationSpec.eps_device), so the first round
+            # is queued behind the quantile kernel instead of waiting for it
             t_start = datetime.datetime.now()
             simulate_one = self._create_simulate_function(t)
             pop_size = self.population_size(t)
@@ -537,6 +551,8 @@ class ABCSMC:
             sample = self.sampler.sample_until_n_accepted(
                 pop_size, simulate_one, max_eval,
                 show_progress=self.show_progress)
+            current_eps = self.eps(t)
+            logger.info(f"t: {t}, eps: {current_eps}.")
             if not sample.ok:
                 logger.info("Stopping: sample not ok.")
                 break
