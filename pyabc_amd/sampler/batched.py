@@ -588,7 +588,7 @@ class BatchedGPUSampler(Sampler):
             # the generation's first round takes the threshold on the device
             # (queued behind the quantile kernel, no host wait); later rounds
             # the host value, which has arrived by then
-            thr = spec.eps_device if rounds == 0 else None
+            thr = getattr(spec, "eps_device", None) if rounds == 0 else None
             if thr is not None:
                 idx, cnt = fr.run(lo, B, 0.0, cap=need, filter=filt, rec_x=rx,
                                   eps_dev=thr[0], eps_scale=thr[1])
