@@ -156,7 +156,11 @@ int abc_mvn_pack_population(const double* X, const double* w, int64_t N, int d,
  * others zero); the lower sampling factor L (L L^T = cov, semidefinite
  * Cholesky); stats (8) = [rank, log pdet, support tol, -log max w, bw,
  * min s, max s, ok (0: cov not positive semidefinite)].  All device, one
- * single-workgroup launch, no host read; d <= 64. */
+ * single-workgroup launch, no host read; d <= 64.  A full-rank covariance
+ * whose smallest eigenvalue is certified above the cut-off (1 / |L^-1|_F^2 >
+ * 4e6 eps trace) is whitened by U = L^-T instead, with no eigen-
+ * decomposition: evals / evec are then NaN and stats[5], stats[6] the
+ * eigenvalue bounds used. */
 int abc_mvn_fit(const double* moments, int d, double scaling, int bw_rule,
                 double* cov, double* evec, double* evals, double* U, double* L,
                 double* stats, void* stream);

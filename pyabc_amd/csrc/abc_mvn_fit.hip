@@ -11,7 +11,9 @@
 //        1e6 eps max|s| ("not positive semidefinite" below -cut-off);
 //        U = u[:, s > cut] / sqrt(s); log pdet = sum log s[kept]
 //
-// One workgroup: the d x d matrix (d <= 64) in LDS, a parallel cyclic
+// One workgroup: the d x d matrix (d <= 64) in LDS.  A full-rank covariance
+// (certified by a lower bound on its smallest eigenvalue, see the fast path)
+// is whitened by its Cholesky factor (U = L^-T).  Otherwise a parallel cyclic
 // Jacobi eigen-decomposition in fp64 (round-robin pair ordering: each step
 // rotates d/2 disjoint (p, q) pairs, rows then columns; sweeps until every
 // off-diagonal is below 2^-53 sqrt(|a_pp a_qq|)), eigenpairs sorted by
@@ -67,6 +69,80 @@ __global__ __launch_bounds__(FT) void mvn_fit_kernel(const double* __restrict__ 
     cov_out[e] = c;
   }
   __syncthreads();
+  // ---- fast path (full rank, certified): Cholesky C = L L^T, W = L^-1 and
+  // U = W^T (U U^T = C^-1: any such factor whitens the same quadratic
+  // form).  Full rank is certified when lambda_min >= 1 / |W|_F^2 exceeds
+  // 4 x scipy's cut-off bound 1e6 eps trace(C) >= 1e6 eps lambda_max: then
+  // _PSD would keep every eigenvalue, log pdet = 2 sum log L_jj.  Otherwise
+  // (singular or nearly so) the Jacobi path below decides the rank.
+  {
+    double tr = 0.0;
+    for (int i = 0; i < d; ++i) tr += A[i][i];
+    const double cutf = 1e6 * 0x1p-52 * tr;
+    bool pos = true;
+    for (int j = 0; j < d; ++j) {
+      if (t == 0) {
+        const double sj = C[j][j];
+        s_piv = sj > cutf ? sqrt(sj) : 0.0;
+        C[j][j] = s_piv;
+      }
+      __syncthreads();
+      const double ljj = s_piv;
+      pos = pos && ljj > 0.0;
+      for (int i = j + 1 + t; i < d; i += FT) C[i][j] = ljj > 0.0 ? C[i][j] / ljj : 0.0;
+      __syncthreads();
+      for (int e = t; e < (d - j - 1) * (d - j - 1); e += FT) {
+        const int i = j + 1 + e / (d - j - 1), k = j + 1 + e % (d - j - 1);
+        if (k <= i) C[i][k] -= C[i][j] * C[k][j];
+      }
+      __syncthreads();
+    }
+    double fro = 0.0;
+    if (pos) {
+      // W = L^-1 (lower), one column per thread, into V
+      for (int j = t; j < d; j += FT)
+        for (int i = 0; i < d; ++i) {
+          double v = i == j ? 1.0 : 0.0;
+          if (i < j) { V[i][j] = 0.0; continue; }
+          for (int k = j; k < i; ++k) v -= C[i][k] * V[k][j];
+          V[i][j] = v / C[i][i];
+        }
+      __syncthreads();
+      for (int i = 0; i < d; ++i)
+        for (int j = 0; j <= i; ++j) fro += V[i][j] * V[i][j];
+    }
+    const bool certified = pos && 1.0 / fro > 4.0 * cutf;
+    if (certified) {
+      for (int e = t; e < d * d; e += FT) {
+        const int i = e / d, j = e % d;
+        U[e] = V[j][i];                       // U = W^T = L^-T
+        L[e] = j <= i ? C[i][j] : 0.0;
+        evec[e] = NAN;                        // not computed on this path
+      }
+      if (t < d) evals[t] = NAN;
+      if (t == 0) {
+        double lp = 0.0;
+        for (int j = 0; j < d; ++j) lp += log(C[j][j]);
+        stats[0] = (double)d;
+        stats[1] = 2.0 * lp;
+        stats[2] = 1e3 * cutf;
+        stats[3] = -log(wmax);
+        stats[4] = bw;
+        stats[5] = 1.0 / fro;                 // lambda_min lower bound
+        stats[6] = tr;                        // lambda_max upper bound
+        stats[7] = 1.0;
+      }
+      return;
+    }
+    // not certified: the covariance back into C for the semidefinite
+    // Cholesky after the eigen-decomposition, V back to the identity
+    for (int e = t; e < d * d; e += FT) {
+      const int i = e / d, j = e % d;
+      C[i][j] = A[i][j];
+      V[i][j] = i == j ? 1.0 : 0.0;
+    }
+    __syncthreads();
+  }
   // ---- parallel cyclic Jacobi
   const int n2 = d + (d & 1);           // even number of players (d itself = a dummy)
   const int np = n2 / 2;

@@ -332,24 +332,14 @@ __device__ __forceinline__ f32x16 mfma32(const half8& a, const half8& b, const f
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// one wave's work: candidate tiles ct0 .. ct0 + CT - 1 against population
+// chunk `chunk`
 template <int KB, int CT, bool PASS1>
-__global__ __launch_bounds__(256) void mvn_x3_kernel(
+__device__ __forceinline__ void x3_wave(
     const half8* __restrict__ A, const half8* __restrict__ Bi, int64_t MT,
-    int64_t NT, int nchunk, int64_t tiles_per_chunk, int64_t ngroups, int koff, int kb0,
-    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad,
-    const unsigned int* __restrict__ count_dev) {
+    int64_t NT, int chunk, int64_t tiles_per_chunk, int64_t ct0, int koff, int kb0,
+    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int64_t bid = blockIdx.x;
-  const int cpx = nchunk >> 3;
-  const int64_t xcd = bid & 7, jb = bid >> 3;
-  const int chunk = (int)(xcd + 8 * (jb % cpx));
-  const int64_t group = jb / cpx;
-  if (group >= ngroups) return;
-  const int64_t ct0 = (group * 4 + wave) * CT;
-  // a device-sized launch: waves past the candidate count leave at once (no
-  // barrier in this kernel)
-  if (count_dev && ct0 * TR >= (int64_t)*count_dev) return;
   // which lanes / instruction / element of the B fragments hold the offset slot
   const bool off_lane = (lane >> 5) == ((koff >> 3) & 1);
   const int off_kb = koff >> 4, off_j = koff & 7;
@@ -496,6 +486,31 @@ __global__ __launch_bounds__(256) void mvn_x3_kernel(
   }
 }
 
+// blocks: (groups of 4 waves x CT candidate tiles) x population chunks; a
+// device-sized launch (count_dev) covers a few groups and strides over the
+// rest, its waves past the candidate count leaving at once (no barrier in
+// this kernel); a full launch has every group in the grid (one pass)
+template <int KB, int CT, bool PASS1>
+__global__ __launch_bounds__(256) void mvn_x3_kernel(
+    const half8* __restrict__ A, const half8* __restrict__ Bi, int64_t MT,
+    int64_t NT, int nchunk, int64_t tiles_per_chunk, int64_t ngroups, int koff, int kb0,
+    double* __restrict__ part_o, double* __restrict__ part_l, int64_t Mpad,
+    const unsigned int* __restrict__ count_dev) {
+  const int wave = threadIdx.x >> 6;
+  const int64_t bid = blockIdx.x;
+  const int cpx = nchunk >> 3;
+  const int64_t xcd = bid & 7, jb = bid >> 3;
+  const int chunk = (int)(xcd + 8 * (jb % cpx));
+  const int64_t gstride = (int64_t)gridDim.x / nchunk;
+  const int64_t cnt = count_dev ? (int64_t)*count_dev : MT * TR;
+  for (int64_t group = jb / cpx; group < ngroups; group += gstride) {
+    const int64_t ct0 = (group * 4 + wave) * CT;
+    if (ct0 * TR >= cnt) break;
+    x3_wave<KB, CT, PASS1>(A, Bi, MT, NT, chunk, tiles_per_chunk, ct0, koff, kb0, part_o,
+                           part_l, Mpad);
+  }
+}
+
 __global__ void x3_combine_kernel(const double* __restrict__ part_o,
                                   const double* __restrict__ part_l, int nchunk,
                                   int64_t M, int64_t Mpad, double log_const,
@@ -527,6 +542,41 @@ __global__ void x3_combine_kernel(const double* __restrict__ part_o,
   // (lg - om); beyond lg - om > 20 (offset far below the true maximum, or
   // > 2^20 comparable terms) recompute in fp64 too
   if (cflags[i] || !(s > 0.0) || !(lg >= -60.0) || (cand_o && lg - om > 20.0)) {
+    const unsigned int q = atomicAdd(nrescue, 1u);
+    rescue[q] = i;
+    out[i] = -INFINITY;
+    return;
+  }
+  out[i] = log_const + LN2 * lg;
+}
+
+// Unhinted combine of a device-sized launch (the nested rescue pass: a few
+// rows, up to 256 chunks): one wave per row, lanes over the chunks, so the
+// row's partials are read in parallel rather than one latency-bound load
+// after the other.  Max by a butterfly (exact); the sum adds each lane's
+// chunks c, c+64, ... in order and then butterflies in a fixed pattern, so
+// a row's bits depend on N (the chunking) only, never on M or its slot.
+__global__ __launch_bounds__(256) void x3_combine_rows_kernel(
+    const double* __restrict__ part_o, const double* __restrict__ part_l, int nchunk,
+    int64_t M, int64_t Mpad, double log_const, const int32_t* __restrict__ cflags,
+    double* __restrict__ out, int64_t* __restrict__ rescue,
+    unsigned int* __restrict__ nrescue, const unsigned int* __restrict__ count_dev) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= M || i >= (int64_t)*count_dev) return;
+  double om = -INFINITY;
+  for (int c = lane; c < nchunk; c += 64)
+    if (part_l[(int64_t)c * Mpad + i] > 0.0) om = fmax(om, part_o[(int64_t)c * Mpad + i]);
+  for (int m = 32; m >= 1; m >>= 1) om = fmax(om, __shfl_xor(om, m, 64));
+  double s = 0.0;
+  for (int c = lane; c < nchunk; c += 64) {
+    const double l = part_l[(int64_t)c * Mpad + i];
+    if (l > 0.0) s += l * exp2(part_o[(int64_t)c * Mpad + i] - om);
+  }
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (lane) return;
+  const double lg = om + log2(s);
+  if (cflags[i] || !(s > 0.0) || !(lg >= -60.0)) {
     const unsigned int q = atomicAdd(nrescue, 1u);
     rescue[q] = i;
     out[i] = -INFINITY;
@@ -693,7 +743,11 @@ struct PlanX3 {
   int64_t MT, NT, MTpad, groups, tiles_per_chunk, Mpad;
 };
 
-PlanX3 make_plan_x3(int64_t M, int64_t N, int r) {
+// fine: the nested rescue pass (few candidates, launched for all M): more,
+// shorter population chunks (up to 256, >= 16 tiles each) so its handful of
+// candidate waves spread over the chip instead of one wave per 1/32 of the
+// population.  Chunking still depends on N only.
+PlanX3 make_plan_x3(int64_t M, int64_t N, int r, bool fine = false) {
   PlanX3 p;
   p.K0pad = x3_k0pad(r);
   p.KB = x3_kb(r);
@@ -709,8 +763,8 @@ PlanX3 make_plan_x3(int64_t M, int64_t N, int r) {
   // XCD map): a candidate's summation order -- and so its bits -- does not
   // depend on M or on its position, which keeps results identical for any
   // candidate sharding over ranks.  32 chunks fill the chip from M ~ 1e4.
-  int64_t nc = ceil_div(ceil_div(p.NT, 128), 8) * 8;
-  nc = nc < 8 ? 8 : (nc > 32 ? 32 : nc);
+  int64_t nc = fine ? ceil_div(ceil_div(p.NT, 16), 8) * 8 : ceil_div(ceil_div(p.NT, 128), 8) * 8;
+  nc = nc < 8 ? 8 : (nc > (fine ? 256 : 32) ? (fine ? 256 : 32) : nc);
   p.nchunk = (int)nc;
   p.tiles_per_chunk = ceil_div(p.NT, p.nchunk);
   return p;
@@ -733,7 +787,9 @@ void launch_x3(const PlanX3& p, const half8* A, const half8* B, int koff,
                double* po, double* pl, bool pass1, const unsigned int* count_dev,
                hipStream_t s) {
   static_assert(CT == x3_ct(KB), "the plan's tiles per wave must match the instantiation");
-  const int64_t blocks = p.groups * p.nchunk;
+  // a device-sized launch strides over its groups with at most 16 in the grid
+  const int64_t gg = count_dev && p.groups > 16 ? 16 : p.groups;
+  const int64_t blocks = gg * p.nchunk;
   if (pass1)
     hipLaunchKernelGGL((mvn_x3_kernel<KB, CT, true>), dim3((unsigned)blocks),
                        dim3(256), 0, s, A, B, p.MT, p.NT, p.nchunk,
@@ -824,7 +880,7 @@ size_t x3_logpdf_workspace(int64_t M, int64_t N, int r) {
   size_t nested = 0;
   size_only<double>(nested, (size_t)m1 * 64);           // rows (d <= 64)
   size_only<double>(nested, (size_t)m1);                // results
-  size_only<char>(nested, main);                        // the nested plan
+  size_only<char>(nested, plan_x3_ws(make_plan_x3(M, N, r, true)));  // the nested plan
   return main + nested + 256;
 }
 
@@ -837,7 +893,7 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
               hipStream_t s, int prof_channel, const unsigned int* count_dev) {
   if (r > MAX_R)
     return set_error(ABC_ERR_UNSUPPORTED, "mvn x3: rank %d > %d", r, MAX_R);
-  PlanX3 p = make_plan_x3(M, N, r);
+  PlanX3 p = make_plan_x3(M, N, r, count_dev != nullptr);
   if (ws_bytes < plan_x3_ws(p))
     return set_error(ABC_ERR_WORKSPACE, "mvn x3: workspace %zu < %zu", ws_bytes,
                      plan_x3_ws(p));
@@ -865,10 +921,15 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
   profile_stop(s, prof_channel);
   if (rc) return rc;
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(x3_combine_kernel, dim3((unsigned)ceil_div(M, 256)), dim3(256),
-                     0, s, po, pl, p.nchunk, M, p.Mpad, log_const, cflags,
-                     hint ? (const float*)cand_o : (const float*)nullptr, out,
-                     rescue, nres, count_dev);
+  if (count_dev && !hint)
+    hipLaunchKernelGGL(x3_combine_rows_kernel, dim3((unsigned)ceil_div(M, 4)), dim3(256),
+                       0, s, po, pl, p.nchunk, M, p.Mpad, log_const, cflags, out, rescue,
+                       nres, count_dev);
+  else
+    hipLaunchKernelGGL(x3_combine_kernel, dim3((unsigned)ceil_div(M, 256)), dim3(256),
+                       0, s, po, pl, p.nchunk, M, p.Mpad, log_const, cflags,
+                       hint ? (const float*)cand_o : (const float*)nullptr, out,
+                       rescue, nres, count_dev);
   ABC_LAUNCHED();
   if (hint) {
     // Hinted candidates whose ancestor offset was far below their true
@@ -882,7 +943,7 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
     Carver sub(cv.rest(), cv.rest_bytes());
     double* xs = sub.take<double>((size_t)M * d);
     double* outs = sub.take<double>((size_t)M);
-    const size_t need = plan_x3_ws(make_plan_x3(M, N, r));
+    const size_t need = plan_x3_ws(make_plan_x3(M, N, r, true));
     void* ws2 = sub.take<char>(need);
     if (!sub.ok) return set_error(ABC_ERR_WORKSPACE, "mvn x3: nested rescue workspace");
     hipLaunchKernelGGL(x3_gather_rescued, dim3((unsigned)ceil_div(M * d, 256)),

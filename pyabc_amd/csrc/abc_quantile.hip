@@ -13,22 +13,26 @@
 // fixed-point integers (w * 2^(62 - ceil log2 N) / max w, truncated), so the
 // histograms' sums are exact integers, independent of any order -- the search
 // is deterministic -- and each bin's cumulative weight is known to within N
-// units.  Launches:
-//   1. range: per-block min / max key and max weight;
-//   2. hist (level 1): 4096 bins linear in the key span, counts and
-//      fixed-point weight sums per bin (LDS atomics, integer);
-//   3. pick (level 1, one block): the bins that can hold the knots j, j + 1
-//      (every bin whose cumulative weight interval, widened by the
-//      fixed-point error, reaches alpha * total, plus one bin on each side
-//      that certainly lies below / above it) -> a key segment [lo, hi];
-//   4./5. hist + pick (level 2) inside that segment when it holds more than
-//      WQ_CAP points (both exit at once otherwise);
-//   6. gather: the segment's points (key, index, w) into a list, and the
+// units.  Four kernels (plus one memset of the control block); each
+// single-block step runs in the last block of the multi-block kernel before
+// it (device-scope fence + counter), so there is no one-block launch:
+//   1. range: min / max key and max weight (integer max atomics);
+//   2. hist (level 1): 2048 bins linear in the key span, counts and
+//      fixed-point weight sums per bin (LDS atomics, integer); its last
+//      block picks the bins that can hold the knots j, j + 1 (every bin whose
+//      cumulative weight interval, widened by the fixed-point error, reaches
+//      alpha * total, plus one bin on each side that certainly lies below /
+//      above it) -> a key segment [lo, hi];
+//   3. hist + pick (level 2) inside that segment when it holds more than
+//      WQ_REFINE points (every block exits at once otherwise); level 1 uses
+//      2048 bins (half the global atomics), level 2 4096;
+//   4. gather: the segment's points (key, index, w) into a list, and the
 //      fp64 sums of the weights below the segment and of all weights (fixed
-//      per-thread order + fixed tree: deterministic);
-//   7. final (one block): the list sorted by (key, index) in LDS, cumulative
-//      weights from the sum below, xp and np.interp's rules
-//      (quantile_pick semantics: clamps, exact knot hit, NaN fallbacks).
+//      per-thread order + fixed tree: deterministic); its last block sorts
+//      the list by (key, index) in LDS (rank sort: every point counts the
+//      points before it), forms the cumulative weights from the
+//      sum below, xp and np.interp's rules (quantile_pick semantics: clamps,
+//      exact knot hit, NaN fallbacks).
 // A segment that still holds more than WQ_CAP points after level 2 (ties by
 // the thousand at the knots, e.g. discrete distances) is not decided here:
 // *q = NaN, and the host (gpu.weighted_quantile's readers) reruns the exact
@@ -39,11 +43,15 @@ namespace abc {
 namespace {
 
 constexpr int WQ_T = 1024;
-constexpr int WQ_BITS = 12, WQ_NB = 1 << WQ_BITS;
-constexpr int WQ_CAP = 2048;
+constexpr int WQ_BITS = 12, WQ_NB = 1 << WQ_BITS;   // level 2 (and the buffers)
+constexpr int WQ_BITS1 = 11;                        // level 1: half the global atomics
+constexpr int WQ_REFINE = 256;   // level 1's segment is refined above this many points
+constexpr int WQ_CAP = 2048;     // list capacity (level 2's segment; ties)
+constexpr int WQ_U = 4;          // loads in flight per thread in the streaming loops
 constexpr int WQ_MAXB = 256;
-constexpr int WQ_FT = 1024;  // threads of the final (single-block) kernel (256: 54 vs 35 us)
-static_assert(WQ_MAXB <= WQ_FT, "wq_final_kernel sums one gather block per thread");
+constexpr int WQ_FT = WQ_T;  // the final runs in the last gather block
+static_assert(WQ_MAXB <= WQ_FT, "the final sums one gather block per thread");
+static_assert(WQ_CAP % WQ_FT == 0 && WQ_FT % WQ_REFINE == 0, "rank sort layout");
 
 typedef unsigned long long u64;
 
@@ -57,7 +65,16 @@ __device__ __forceinline__ double qval(u64 k) {
   return __longlong_as_double((long long)b);
 }
 
-struct WqPart { u64 kmin, kmax, wmax; };
+// per-call control block, zeroed by the launcher's one memset: the global
+// key range (kmin stored complemented, so zero is the identity of the max
+// atomics), the last-block counters of the three multi-block stages, the
+// fixed-point total and the list counter
+struct WqCtl {
+  u64 nkmin, kmax, wmax;
+  unsigned int done[4];
+  u64 tot;
+  unsigned int list_n, pad;
+};
 struct WqDesc {
   u64 lo, hi;          // key segment [lo, hi] (inclusive)
   u64 base_w;          // fixed-point weight below lo
@@ -92,30 +109,25 @@ __device__ __forceinline__ T block_reduce(T v, T* sh, Op op) {
 }
 
 struct Range { u64 kmin, kmax; double S; };
-__device__ __forceinline__ Range wq_global_range(const WqPart* part, int nblk, int64_t N) {
-  Range r{~0ull, 0ull, 0.0};
-  u64 wm = 0ull;
-  for (int b = 0; b < nblk; ++b) {
-    r.kmin = part[b].kmin < r.kmin ? part[b].kmin : r.kmin;
-    r.kmax = part[b].kmax > r.kmax ? part[b].kmax : r.kmax;
-    wm = part[b].wmax > wm ? part[b].wmax : wm;
-  }
-  const double wmax = __longlong_as_double((long long)wm);
+__device__ __forceinline__ Range wq_global_range(const WqCtl* ctl, int64_t N) {
+  Range r{~ctl->nkmin, ctl->kmax, 0.0};
+  const double wmax = __longlong_as_double((long long)ctl->wmax);
   r.S = wmax > 0.0 ? ldexp(1.0, 62 - lg_ceil(N)) / wmax : 0.0;
   return r;
 }
 
+template <int BITS = WQ_BITS>
 __device__ __forceinline__ int span_shift(u64 lo, u64 hi) {
   const u64 span = hi - lo;
   const int L = span ? 64 - __clzll(span) : 0;
-  return L > WQ_BITS ? L - WQ_BITS : 0;
+  return L > BITS ? L - BITS : 0;
 }
 
 // ---- 1. range ----------------------------------------------------------------
 __global__ __launch_bounds__(WQ_T) void wq_range_kernel(const double* __restrict__ x,
                                                         const double* __restrict__ w,
                                                         int64_t N, int64_t chunk,
-                                                        WqPart* __restrict__ part,
+                                                        WqCtl* __restrict__ ctl,
                                                         unsigned int* __restrict__ ghc,
                                                         u64* __restrict__ ghw) {
   __shared__ u64 sh[WQ_T / 64];
@@ -128,122 +140,64 @@ __global__ __launch_bounds__(WQ_T) void wq_range_kernel(const double* __restrict
   const int64_t b0 = (int64_t)blockIdx.x * chunk;
   const int64_t b1 = b0 + chunk < N ? b0 + chunk : N;
   u64 mn = ~0ull, mx = 0ull, wm = 0ull;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += WQ_T) {
-    const u64 k = qkey(x[i]);
-    mn = k < mn ? k : mn;
-    mx = k > mx ? k : mx;
-    const u64 wb = (u64)__double_as_longlong(wval(w[i]));  // >= 0: bits order like values
-    wm = wb > wm ? wb : wm;
+  for (int64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += WQ_U * WQ_T) {
+    double xv[WQ_U], wv[WQ_U];
+#pragma unroll
+    for (int u = 0; u < WQ_U; ++u) {
+      const int64_t i = i0 + (int64_t)u * WQ_T;
+      xv[u] = i < b1 ? x[i] : x[i0];
+      wv[u] = i < b1 ? w[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < WQ_U; ++u) {
+      const u64 k = qkey(xv[u]);
+      mn = k < mn ? k : mn;
+      mx = k > mx ? k : mx;
+      const u64 wb = (u64)__double_as_longlong(wval(wv[u]));  // >= 0: bits order like values
+      wm = wb > wm ? wb : wm;
+    }
   }
   auto umin = [](u64 a, u64 b) { return a < b ? a : b; };
   auto umax = [](u64 a, u64 b) { return a > b ? a : b; };
   mn = block_reduce(mn, sh, umin);
   mx = block_reduce(mx, sh, umax);
   wm = block_reduce(wm, sh, umax);
-  // one global range: integer min / max atomics (order-free), initialised
-  // by the launcher's memsets
+  // one global range: integer max atomics (order-free) on the zeroed control
+  // block, the minimum as the max of the complement
   if (threadIdx.x == 0) {
-    atomicMin(reinterpret_cast<unsigned long long*>(&part->kmin), (unsigned long long)mn);
-    atomicMax(reinterpret_cast<unsigned long long*>(&part->kmax), (unsigned long long)mx);
-    atomicMax(reinterpret_cast<unsigned long long*>(&part->wmax), (unsigned long long)wm);
+    atomicMax(reinterpret_cast<unsigned long long*>(&ctl->nkmin), (unsigned long long)~mn);
+    atomicMax(reinterpret_cast<unsigned long long*>(&ctl->kmax), (unsigned long long)mx);
+    atomicMax(reinterpret_cast<unsigned long long*>(&ctl->wmax), (unsigned long long)wm);
   }
 }
 
-// ---- 2. histogram of one level ----------------------------------------------
-// level 1: the whole key range; level 2: the level-1 segment (exits when the
-// level-1 segment fits)
-__global__ __launch_bounds__(WQ_T) void wq_hist_kernel(
-    const double* __restrict__ x, const double* __restrict__ w, int64_t N, int64_t chunk,
-    const WqPart* __restrict__ part, int nblk, const WqDesc* __restrict__ prev,
-    unsigned int* __restrict__ ghc, u64* __restrict__ ghw) {
-  if (prev && prev->ok) return;
-  __shared__ unsigned int cnt[WQ_NB];
-  __shared__ u64 ws[WQ_NB];
-  for (int b = threadIdx.x; b < WQ_NB; b += WQ_T) { cnt[b] = 0u; ws[b] = 0ull; }
-  const Range R = wq_global_range(part, nblk, N);
-  const u64 lo = prev ? prev->lo : R.kmin, hi = prev ? prev->hi : R.kmax;
-  const int sh = span_shift(lo, hi);
+// Last-block hand-over.  Everything one stage hands to its last block is
+// written by agent-scope atomics (histogram adds, list / partial-sum stores
+// through __hip_atomic_store) and read there by agent-scope atomic loads, so
+// no L2 write-back is needed per block: each wave waits for its own memory
+// operations to complete, the block's counter is bumped once, and the block
+// that brings it to the grid size runs the stage's tail (pick / final) after
+// one acquire fence.  The single-block kernels and their launch gaps go.
+__device__ __forceinline__ bool wq_last_block(unsigned int* done) {
+  __shared__ int s_last;
+  __builtin_amdgcn_s_waitcnt(0);   // this wave's atomics / stores completed
   __syncthreads();
-  const int64_t b0 = (int64_t)blockIdx.x * chunk;
-  const int64_t b1 = b0 + chunk < N ? b0 + chunk : N;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += WQ_T) {
-    const u64 k = qkey(x[i]);
-    if (k < lo || k > hi) continue;
-    const int bin = (int)((k - lo) >> sh);
-    atomicAdd(&cnt[bin], 1u);
-    atomicAdd(&ws[bin], wfix(w[i], R.S));
-  }
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             gridDim.x - 1;
   __syncthreads();
-  // into the level's global histogram: integer atomics, so the totals do
-  // not depend on the blocks' order
-  for (int b = threadIdx.x; b < WQ_NB; b += WQ_T) {
-    if (cnt[b]) {
-      atomicAdd(&ghc[b], cnt[b]);
-      atomicAdd(reinterpret_cast<unsigned long long*>(&ghw[b]), (unsigned long long)ws[b]);
-    }
-  }
+  if (!s_last) return false;
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  return true;
 }
 
-// ---- 3. pick the segment of one level ------------------------------------------
-// Per-bin totals (fixed order over blocks; integers), exclusive prefixes, and
-// the segment: from the last non-empty bin whose whole weight interval lies
-// certainly below the target to the first whose interval lies certainly
-// above it (the knots j and j + 1 lie between them, inclusive).  Shared by
-// the multi-block path (cnt / wsum summed from the block histograms) and the
-// final block's slow refinement.
-struct Pick { int b1, b2; };
-__device__ void wq_pick_bins(const unsigned int* cnt, const u64* wsum, u64* pre_w,
-                             long long* pre_c, u64 base_w, double target, double margin,
-                             Pick& pk, u64* s_sh) {
-  // exclusive prefixes: 4 bins per thread, then a block scan of the thread sums
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  constexpr int PER = WQ_NB / WQ_T;
-  u64 sw = 0ull;
-  long long sc = 0;
-#pragma unroll
-  for (int i = 0; i < PER; ++i) { sw += wsum[t * PER + i]; sc += cnt[t * PER + i]; }
-  u64 iw = sw;
-  long long ic = sc;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const u64 a = __shfl_up(iw, o, 64);
-    const long long c = __shfl_up(ic, o, 64);
-    if (lane >= o) { iw += a; ic += c; }
-  }
-  __shared__ long long s_c[WQ_T / 64];
-  if (lane == 63) { s_sh[wv] = iw; s_c[wv] = ic; }
-  __syncthreads();
-  u64 ow = base_w + iw - sw;
-  long long oc = ic - sc;
-  for (int i = 0; i < wv; ++i) { ow += s_sh[i]; oc += s_c[i]; }
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    pre_w[t * PER + i] = ow;
-    pre_c[t * PER + i] = oc;
-    ow += wsum[t * PER + i];
-    oc += cnt[t * PER + i];
-  }
-  __syncthreads();
-  // b1 = last non-empty bin with pre + W + margin <= target (else the first
-  // non-empty bin); b2 = first non-empty bin with pre - margin > target
-  // (else the last non-empty bin)
-  __shared__ int s_b1, s_b2, s_first, s_last;
-  if (t == 0) { s_b1 = -1; s_b2 = WQ_NB; s_first = WQ_NB; s_last = -1; }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int b = t * PER + i;
-    if (cnt[b] == 0u) continue;
-    atomicMin(&s_first, b);
-    atomicMax(&s_last, b);
-    if ((double)(pre_w[b] + wsum[b]) + margin <= target) atomicMax(&s_b1, b);
-    if ((double)pre_w[b] - margin > target) atomicMin(&s_b2, b);
-  }
-  __syncthreads();
-  pk.b1 = s_b1 >= 0 ? s_b1 : s_first;
-  pk.b2 = s_b2 < WQ_NB ? s_b2 : s_last;
-  if (pk.b2 < pk.b1) pk.b2 = pk.b1;
-  __syncthreads();
+template <class T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void seg_keys(u64 lo, u64 hi, int sh, int b1, int b2, u64& slo,
@@ -253,83 +207,170 @@ __device__ __forceinline__ void seg_keys(u64 lo, u64 hi, int sh, int b1, int b2,
   shi = off >= hi - lo ? hi : lo + off;
 }
 
-__global__ __launch_bounds__(WQ_T) void wq_pick_kernel(
-    int64_t N, double alpha, const WqPart* __restrict__ part, int nblk,
-    const unsigned int* __restrict__ ghc, const u64* __restrict__ ghw, int nhb,
-    const WqDesc* __restrict__ prev, WqDesc* __restrict__ out, unsigned int* __restrict__ list_n) {
-  (void)nhb;   // one global histogram per level (integer atomics in wq_hist_kernel)
-  if (prev && prev->ok) {
-    if (threadIdx.x == 0) *out = *prev;
-    return;
+// ---- pick the segment of one level (the last histogram block) --------------
+// Per-bin totals from the level's global histogram (integers), exclusive
+// prefixes by a block scan held in registers (4 bins per thread), and the
+// segment: from the last non-empty bin whose whole weight interval lies
+// certainly below the target to the first whose interval lies certainly
+// above it (the knots j and j + 1 lie between them, inclusive).  Block
+// reductions by wave shuffles (no same-address LDS atomics).
+template <int BITS>
+__device__ void wq_pick_block(int64_t N, double alpha, const WqCtl* ctl,
+                              const unsigned int* ghc, const u64* ghw, u64 lo, u64 hi,
+                              u64 base_w, long long base_c, bool level1, WqCtl* ctl_w,
+                              WqDesc* out) {
+  constexpr int NB = 1 << BITS, PER = NB / WQ_T;
+  __shared__ u64 s_w[WQ_T / 64];
+  __shared__ long long s_c[WQ_T / 64];
+  __shared__ int s_i[4][WQ_T / 64];
+  __shared__ u64 s_bw;
+  __shared__ long long s_bc, s_ec;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  unsigned int c[PER];
+  u64 wsm[PER];
+  u64 sw = 0ull;
+  long long sc = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    c[i] = ld_agent(&ghc[t * PER + i]);
+    wsm[i] = ld_agent(&ghw[t * PER + i]);
+    sw += wsm[i];
+    sc += c[i];
   }
-  __shared__ unsigned int cnt[WQ_NB];
-  __shared__ u64 wsum[WQ_NB], pre_w[WQ_NB];
-  __shared__ long long pre_c[WQ_NB];
-  __shared__ u64 s_sh[WQ_T / 64];
-  const Range R = wq_global_range(part, nblk, N);
-  u64 tw = 0ull;
-  for (int b = threadIdx.x; b < WQ_NB; b += WQ_T) {
-    const unsigned int c = ghc[b];
-    const u64 sm = ghw[b];
-    cnt[b] = c;
-    wsum[b] = sm;
-    tw += sm;
+  // inclusive wave scans, then the waves' totals in order
+  u64 iw = sw;
+  long long ic = sc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u64 a = __shfl_up(iw, o, 64);
+    const long long b = __shfl_up(ic, o, 64);
+    if (lane >= o) { iw += a; ic += b; }
   }
-  auto add = [](u64 a, u64 b) { return a + b; };
-  tw = block_reduce(tw, s_sh, add);
-  // the whole input's fixed-point total: summed at level 1 and kept next to
-  // the list counter for level 2 and the final block
-  long long* tot_slot = reinterpret_cast<long long*>(list_n + 2);
-  const double tot_fx = prev ? __longlong_as_double(*tot_slot) : (double)tw;
-  const u64 lo = prev ? prev->lo : R.kmin, hi = prev ? prev->hi : R.kmax;
-  const u64 base_w = prev ? prev->base_w : 0ull;
-  const long long base_c = prev ? prev->below : 0;
+  if (lane == 63) { s_w[wv] = iw; s_c[wv] = ic; }
+  __syncthreads();
+  u64 tw = 0ull, ow = iw - sw;
+  long long oc = ic - sc;
+  for (int i = 0; i < WQ_T / 64; ++i) {
+    tw += s_w[i];
+    if (i < wv) { ow += s_w[i]; oc += s_c[i]; }
+  }
+  // the whole input's fixed-point total: summed at level 1 and kept in the
+  // control block for level 2
+  const double tot_fx = level1 ? (double)tw : __longlong_as_double((long long)ctl->tot);
   const double target = alpha * tot_fx;
   const double margin = (double)N + ldexp(tot_fx, -48) + 4096.0;
-  Pick pk;
-  wq_pick_bins(cnt, wsum, pre_w, pre_c, base_w, target, margin, pk, s_sh);
-  if (threadIdx.x == 0) {
+  ow += base_w;
+  // b1 = last non-empty bin with pre + W + margin <= target (else the first
+  // non-empty bin); b2 = first non-empty bin with pre - margin > target
+  // (else the last non-empty bin)
+  int cb1 = -1, cb2 = NB, first = NB, last = -1;
+  {
+    u64 pw = ow;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int b = t * PER + i;
+      if (c[i]) {
+        first = min(first, b);
+        last = max(last, b);
+        if ((double)(pw + wsm[i]) + margin <= target) cb1 = max(cb1, b);
+        if ((double)pw - margin > target) cb2 = min(cb2, b);
+      }
+      pw += wsm[i];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cb1 = max(cb1, __shfl_xor(cb1, o, 64));
+    cb2 = min(cb2, __shfl_xor(cb2, o, 64));
+    first = min(first, __shfl_xor(first, o, 64));
+    last = max(last, __shfl_xor(last, o, 64));
+  }
+  if (lane == 0) { s_i[0][wv] = cb1; s_i[1][wv] = cb2; s_i[2][wv] = first; s_i[3][wv] = last; }
+  __syncthreads();
+  for (int i = 0; i < WQ_T / 64; ++i) {
+    cb1 = max(cb1, s_i[0][i]);
+    cb2 = min(cb2, s_i[1][i]);
+    first = min(first, s_i[2][i]);
+    last = max(last, s_i[3][i]);
+  }
+  int b1 = cb1 >= 0 ? cb1 : first;
+  int b2 = cb2 < NB ? cb2 : last;
+  if (b1 >= NB) b1 = 0;      // no point in range (cannot happen: guards)
+  if (b2 < b1) b2 = b1;
+  {
+    u64 pw = ow;
+    long long pc = oc;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int b = t * PER + i;
+      if (b == b1) { s_bw = pw; s_bc = pc; }
+      if (b == b2) s_ec = pc + c[i];
+      pw += wsm[i];
+      pc += c[i];
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
     WqDesc d;
-    seg_keys(lo, hi, span_shift(lo, hi), pk.b1, pk.b2, d.lo, d.hi);
-    d.base_w = pre_w[pk.b1];
-    d.below = base_c + pre_c[pk.b1];
-    long long c = 0;
-    for (int b = pk.b1; b <= pk.b2; ++b) c += cnt[b];
-    d.count = c;
-    d.ok = c <= WQ_CAP ? 1 : 0;
+    seg_keys(lo, hi, span_shift<BITS>(lo, hi), b1, b2, d.lo, d.hi);
+    d.base_w = s_bw;
+    d.below = base_c + s_bc;
+    d.count = s_ec - s_bc;
+    d.ok = d.count <= (level1 ? WQ_REFINE : WQ_CAP) ? 1 : 0;
     d.done = 0;
     *out = d;
-    if (!prev) {
-      list_n[0] = 0u;
-      *tot_slot = __double_as_longlong((double)tw);
-    }
+    if (level1) ctl_w->tot = (u64)__double_as_longlong((double)tw);
   }
 }
 
-// ---- 6. gather the segment + the fp64 sums ----------------------------------
-__global__ __launch_bounds__(WQ_T) void wq_gather_kernel(
+// ---- 2./3. histogram of one level + its pick --------------------------------
+// level 1: the whole key range; level 2: the level-1 segment (every block
+// exits when the level-1 segment fits).  The block's LDS histogram goes into
+// the level's global histogram by integer atomics (totals independent of the
+// blocks' order); the last block picks the segment.
+template <int LEVEL>
+__global__ __launch_bounds__(WQ_T) void wq_hist_kernel(
     const double* __restrict__ x, const double* __restrict__ w, int64_t N, int64_t chunk,
-    const WqDesc* __restrict__ desc, u64* __restrict__ lkey, int* __restrict__ lidx,
-    double* __restrict__ lw, unsigned int* __restrict__ list_n, double* __restrict__ psum) {
-  __shared__ double sh[WQ_T / 64];
-  const WqDesc D = *desc;
+    double alpha, WqCtl* __restrict__ ctl, WqDesc* __restrict__ desc,
+    unsigned int* __restrict__ ghc, u64* __restrict__ ghw) {
+  constexpr int BITS = LEVEL == 1 ? WQ_BITS1 : WQ_BITS, NB = 1 << BITS;
+  const WqDesc* prev = LEVEL == 2 ? desc : nullptr;
+  if (prev && prev->ok) return;
+  __shared__ unsigned int cnt[NB];
+  __shared__ u64 ws[NB];
+  for (int b = threadIdx.x; b < NB; b += WQ_T) { cnt[b] = 0u; ws[b] = 0ull; }
+  const Range R = wq_global_range(ctl, N);
+  const u64 lo = prev ? prev->lo : R.kmin, hi = prev ? prev->hi : R.kmax;
+  const int sh = span_shift<BITS>(lo, hi);
+  __syncthreads();
   const int64_t b0 = (int64_t)blockIdx.x * chunk;
   const int64_t b1 = b0 + chunk < N ? b0 + chunk : N;
-  double below = 0.0, all = 0.0;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += WQ_T) {
-    const u64 k = qkey(x[i]);
-    const double wi = wval(w[i]);
-    all += wi;
-    if (k < D.lo) below += wi;
-    else if (D.ok && k <= D.hi) {
-      const unsigned int pos = atomicAdd(list_n, 1u);
-      if (pos < (unsigned int)WQ_CAP) { lkey[pos] = k; lidx[pos] = (int)i; lw[pos] = wi; }
+  for (int64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += WQ_U * WQ_T) {
+    u64 kv[WQ_U];
+#pragma unroll
+    for (int u = 0; u < WQ_U; ++u) {
+      const int64_t i = i0 + (int64_t)u * WQ_T;
+      kv[u] = i < b1 ? qkey(x[i]) : ~0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < WQ_U; ++u) {
+      const int64_t i = i0 + (int64_t)u * WQ_T;
+      if (i >= b1 || kv[u] < lo || kv[u] > hi) continue;
+      const int bin = (int)((kv[u] - lo) >> sh);
+      atomicAdd(&cnt[bin], 1u);
+      atomicAdd(&ws[bin], wfix(w[i], R.S));
     }
   }
-  auto add = [](double a, double b) { return a + b; };
-  below = block_reduce(below, sh, add);
-  all = block_reduce(all, sh, add);
-  if (threadIdx.x == 0) { psum[2 * blockIdx.x] = below; psum[2 * blockIdx.x + 1] = all; }
+  __syncthreads();
+  for (int b = threadIdx.x; b < NB; b += WQ_T) {
+    if (cnt[b]) {
+      atomicAdd(&ghc[b], cnt[b]);
+      atomicAdd(reinterpret_cast<unsigned long long*>(&ghw[b]), (unsigned long long)ws[b]);
+    }
+  }
+  if (!wq_last_block(&ctl->done[LEVEL - 1])) return;
+  wq_pick_block<BITS>(N, alpha, ctl, ghc, ghw, lo, hi, prev ? prev->base_w : 0ull,
+                      prev ? prev->below : 0, LEVEL == 1, ctl, desc + (LEVEL - 1));
 }
 
 // ---- 7. final ---------------------------------------------------------------
@@ -364,17 +405,61 @@ __device__ __forceinline__ bool kless(u64 ka, int ia, u64 kb, int ib) {
   return ka < kb || (ka == kb && ia < ib);
 }
 
-__global__ __launch_bounds__(WQ_FT) void wq_final_kernel(
-    int64_t N, double alpha, const WqDesc* __restrict__ desc,
-    const u64* __restrict__ gkey, const int* __restrict__ gidx, const double* __restrict__ gw,
-    const double* __restrict__ psum, int nsum, double* __restrict__ q) {
+// ---- 4./5. gather the segment + the fp64 sums, final in the last block -----
+__global__ __launch_bounds__(WQ_T) void wq_gather_final_kernel(
+    const double* __restrict__ x, const double* __restrict__ w, int64_t N, int64_t chunk,
+    double alpha, WqCtl* __restrict__ ctl, const WqDesc* __restrict__ desc,
+    u64* __restrict__ gkey, int* __restrict__ gidx, double* __restrict__ gw,
+    double* __restrict__ psum, double* __restrict__ q) {
+  __shared__ double sh[WQ_T / 64];
+  // the level-1 segment when it fits, else level 2's
+  const WqDesc D = desc[0].ok ? desc[0] : desc[1];
+  {
+    const int64_t b0 = (int64_t)blockIdx.x * chunk;
+    const int64_t b1 = b0 + chunk < N ? b0 + chunk : N;
+    double below = 0.0, all = 0.0;
+    for (int64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += WQ_U * WQ_T) {
+      double xv[WQ_U], wv[WQ_U];
+#pragma unroll
+      for (int u = 0; u < WQ_U; ++u) {
+        const int64_t i = i0 + (int64_t)u * WQ_T;
+        xv[u] = i < b1 ? x[i] : 0.0;
+        wv[u] = i < b1 ? w[i] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < WQ_U; ++u) {
+      const int64_t i = i0 + (int64_t)u * WQ_T;
+      if (i >= b1) continue;
+      const u64 k = qkey(xv[u]);
+      const double wi = wval(wv[u]);
+      all += wi;
+      if (k < D.lo) below += wi;
+      else if (D.ok && k <= D.hi) {
+        const unsigned int pos = atomicAdd(&ctl->list_n, 1u);
+        if (pos < (unsigned int)WQ_CAP) {
+          st_agent(&gkey[pos], k);
+          st_agent(&gidx[pos], (int)i);
+          st_agent(&gw[pos], wi);
+        }
+      }
+      }
+    }
+    auto add = [](double a, double b) { return a + b; };
+    below = block_reduce(below, sh, add);
+    all = block_reduce(all, sh, add);
+    if (threadIdx.x == 0) {
+      st_agent(&psum[2 * blockIdx.x], below);
+      st_agent(&psum[2 * blockIdx.x + 1], all);
+    }
+  }
+  if (!wq_last_block(&ctl->done[2])) return;
+  const int nsum = gridDim.x;
   __shared__ u64 skey[WQ_CAP];
   __shared__ int sidx[WQ_CAP];
   __shared__ double sw[WQ_CAP];
   __shared__ Knot kn[WQ_CAP];
   __shared__ double dsh[WQ_FT / 64];
   const int t = threadIdx.x;
-  const WqDesc D = *desc;
   if (!D.ok) {   // the knots sit in more than WQ_CAP points (ties): not decided
     if (t == 0) *q = NAN;
     return;
@@ -383,7 +468,8 @@ __global__ __launch_bounds__(WQ_FT) void wq_final_kernel(
   __shared__ double s_bt[2][WQ_FT / 64];
   __shared__ double s_below, s_total;
   {
-    double bl = t < nsum ? psum[2 * t] : 0.0, al = t < nsum ? psum[2 * t + 1] : 0.0;
+    double bl = t < nsum ? ld_agent(&psum[2 * t]) : 0.0;
+    double al = t < nsum ? ld_agent(&psum[2 * t + 1]) : 0.0;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       bl += __shfl_xor(bl, o, 64);
@@ -401,32 +487,55 @@ __global__ __launch_bounds__(WQ_FT) void wq_final_kernel(
   }
   const double below = s_below, total = s_total;
   const int m = (int)D.count;
-  int M = 1;
-  while (M < m) M <<= 1;
-  for (int i = t; i < M; i += WQ_FT) {
-    const bool in = i < m;
-    skey[i] = in ? gkey[i] : ~0ull;
-    sidx[i] = in ? gidx[i] : 0x7FFFFFFF;
-    sw[i] = in ? gw[i] : 0.0;
+  for (int i = t; i < m; i += WQ_FT) {
+    skey[i] = ld_agent(&gkey[i]);
+    sidx[i] = ld_agent(&gidx[i]);
+    sw[i] = ld_agent(&gw[i]);
   }
   __syncthreads();
-  // bitonic sort by (key, index): the stable order of the reference's sort
-  for (int size = 2; size <= M; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = t; i < M; i += WQ_FT) {
-        const int jx = i ^ stride;
-        if (jx > i) {
-          const bool asc = (i & size) == 0;
-          if (kless(skey[jx], sidx[jx], skey[i], sidx[i]) == asc) {
-            const u64 a = skey[i]; skey[i] = skey[jx]; skey[jx] = a;
-            const int b = sidx[i]; sidx[i] = sidx[jx]; sidx[jx] = b;
-            const double c = sw[i]; sw[i] = sw[jx]; sw[jx] = c;
-          }
-        }
+  // rank sort by (key, index) -- the stable order of the reference's sort:
+  // each listed point counts the points before it (LDS broadcast reads, no
+  // dependent stages; up to WQ_REFINE points the count is split over
+  // WQ_FT / WQ_REFINE groups of the list and summed by integer LDS atomics),
+  // then the list is rewritten in rank order.  The ranks are exact integers,
+  // so the order -- and the fixed-order prefix below -- never depends on the
+  // list's (atomic) fill order.
+  {
+    __shared__ int srank[WQ_CAP];
+    const int G = m <= WQ_REFINE ? WQ_FT / WQ_REFINE : 1;
+    const int per_g = WQ_FT / G, g = t / per_g, e0 = t % per_g;
+    const int jn = (m + G - 1) / G, jlo = g * jn, jhi = min(m, jlo + jn);
+    for (int e = t; e < m; e += WQ_FT) srank[e] = 0;
+    __syncthreads();
+    for (int e = e0; e < m; e += per_g) {
+      const u64 ke = skey[e];
+      const int ie = sidx[e];
+      int r = 0;
+      for (int j = jlo; j < jhi; ++j) r += kless(skey[j], sidx[j], ke, ie) ? 1 : 0;
+      if (G == 1) srank[e] = r;
+      else atomicAdd(&srank[e], r);
+    }
+    __syncthreads();
+    constexpr int PT = WQ_CAP / WQ_FT;
+    u64 k[PT];
+    int ix[PT], rk[PT];
+    double wv[PT];
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const int e = t + q * WQ_FT;
+      if (e < m) { k[q] = skey[e]; ix[q] = sidx[e]; wv[q] = sw[e]; rk[q] = srank[e]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      if (t + q * WQ_FT < m) {
+        skey[rk[q]] = k[q];
+        sidx[rk[q]] = ix[q];
+        sw[rk[q]] = wv[q];
       }
-      __syncthreads();
     }
   }
+  __syncthreads();
   // cumulative weights: the fp64 sum below + an inclusive prefix in a fixed
   // order (each thread a run of consecutive elements, then the thread sums)
   {
@@ -472,18 +581,21 @@ using namespace abc;
 extern "C" size_t abc_weighted_quantile_workspace(int64_t N) {
   const int nb = wq_blocks(N > 0 ? N : 1);
   size_t off = 0;
-  size_only<WqPart>(off, 1);
+  size_only<WqCtl>(off, 1);
   size_only<unsigned int>(off, (size_t)2 * WQ_NB);
   size_only<u64>(off, (size_t)2 * WQ_NB);
   size_only<WqDesc>(off, 2);
   size_only<u64>(off, WQ_CAP);
   size_only<int>(off, WQ_CAP);
   size_only<double>(off, WQ_CAP);
-  size_only<unsigned int>(off, 4);
   size_only<double>(off, (size_t)2 * nb);
   return off + 256;
 }
 
+// Launches: one memset (the control block), range, level-1 histogram (its
+// last block picks), level-2 histogram (exits at once when level 1 fits; its
+// last block picks), gather (its last block sorts the list and
+// interpolates).  No single-block kernel.
 extern "C" int abc_weighted_quantile(const double* points, const double* w, int64_t N,
                                      double alpha, double* q, void* ws, size_t ws_bytes,
                                      void* stream) {
@@ -495,38 +607,27 @@ extern "C" int abc_weighted_quantile(const double* points, const double* w, int6
   const int nb = wq_blocks(N);
   const int64_t chunk = ceil_div(N, nb);
   Carver cv(ws, ws_bytes);
-  WqPart* part = cv.take<WqPart>(1);
+  WqCtl* ctl = cv.take<WqCtl>(1);
   unsigned int* ghc = cv.take<unsigned int>((size_t)2 * WQ_NB);   // level 1 | level 2
   u64* ghw = cv.take<u64>((size_t)2 * WQ_NB);
   WqDesc* desc = cv.take<WqDesc>(2);
   u64* lkey = cv.take<u64>(WQ_CAP);
   int* lidx = cv.take<int>(WQ_CAP);
   double* lw = cv.take<double>(WQ_CAP);
-  unsigned int* list_n = cv.take<unsigned int>(4);   // [0]: count; [2..3]: total (fixed)
   double* psum = cv.take<double>((size_t)2 * nb);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "quantile: carve");
-  ABC_HIP(hipMemsetAsync(&part->kmin, 0xFF, sizeof(u64), s));
-  ABC_HIP(hipMemsetAsync(&part->kmax, 0, 2 * sizeof(u64), s));
-  hipLaunchKernelGGL(wq_range_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, part,
+  ABC_HIP(hipMemsetAsync(ctl, 0, sizeof(WqCtl), s));
+  hipLaunchKernelGGL(wq_range_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, ctl,
                      ghc, ghw);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_hist_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, part, 1,
-                     (const WqDesc*)nullptr, ghc, ghw);
+  hipLaunchKernelGGL(wq_hist_kernel<1>, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk,
+                     alpha, ctl, desc, ghc, ghw);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_pick_kernel, dim3(1), dim3(WQ_T), 0, s, N, alpha, part, 1, ghc, ghw, 1,
-                     (const WqDesc*)nullptr, desc, list_n);
+  hipLaunchKernelGGL(wq_hist_kernel<2>, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk,
+                     alpha, ctl, desc, ghc + WQ_NB, ghw + WQ_NB);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_hist_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, part, 1,
-                     (const WqDesc*)desc, ghc + WQ_NB, ghw + WQ_NB);
-  ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_pick_kernel, dim3(1), dim3(WQ_T), 0, s, N, alpha, part, 1,
-                     ghc + WQ_NB, ghw + WQ_NB, 1, (const WqDesc*)desc, desc + 1, list_n);
-  ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_gather_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk,
-                     (const WqDesc*)(desc + 1), lkey, lidx, lw, list_n, psum);
-  ABC_LAUNCHED();
-  hipLaunchKernelGGL(wq_final_kernel, dim3(1), dim3(WQ_FT), 0, s, N, alpha,
-                     (const WqDesc*)(desc + 1), lkey, lidx, lw, psum, nb, q);
+  hipLaunchKernelGGL(wq_gather_final_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk,
+                     alpha, ctl, (const WqDesc*)desc, lkey, lidx, lw, psum, q);
   ABC_LAUNCHED();
   return ABC_OK;
 }

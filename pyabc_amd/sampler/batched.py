@@ -181,7 +181,11 @@ class BatchedGPUSampler(Sampler):
         # last_stats["records_truncated"] is True
         self.record_device_budget_bytes = record_device_budget_bytes
         self._acc_rate = None
+        self._acc_trend = 1.0
         self.last_stats = {}
+        # set by ABCSMC.run: host reads of the previous generation, run once
+        # the first fused round is queued (the GPU has work while they wait)
+        self.on_first_launch = None
 
     def _base_seed(self, device):
         if self.seed is None:
@@ -497,15 +501,30 @@ class BatchedGPUSampler(Sampler):
                         for k in kinds)
                 and src is not None and all(0 <= int(v) < self.LAZY_KT for v in src[:4]))
 
+    # candidates per rank a first round may spend on spare: about what one
+    # more round costs in fixed time (launch, scan, host read and the
+    # loop's host work, ~0.2 ms) at ~2e10 candidates/s
+    FIRST_ROUND_SPARE = 4_000_000
+
     def _fused_size(self, need, ws, rate, measured, S, record):
         """Candidates per rank for the next fused round: need / rate, with a
-        6% margin once the rate was measured in this generation (the previous
-        generation's rate is optimistic as eps shrinks, so the first round
-        rarely overshoots), capped by the launch and record budgets."""
+        6% margin once the rate was measured in this generation, capped by
+        the launch and record budgets.  The generation's first round takes
+        the previous generation's rate times its last drop (eps shrinks, so
+        the rate keeps falling) plus a spare of up to 10%, bounded by what a
+        second round would cost: small early generations then finish in one
+        round, large ones add little.  Round sizes never change the result
+        (candidates are keyed by their global index; the first `need`
+        accepted in index order are kept)."""
         if self.batch_size is not None:
             return int(self.batch_size)
         r = rate if rate else 0.5
-        b = need / max(r, 1e-12) * (1.06 if measured else 1.0) / ws + 4096
+        if measured:
+            mult = 1.06
+        else:
+            r *= self._acc_trend if rate else 1.0
+            mult = 1.0 + min(0.1, self.FIRST_ROUND_SPARE * ws * max(r, 1e-12) / max(need, 1))
+        b = need / max(r, 1e-12) * mult / ws + 4096
         cap = self.max_fused_batch_size
         if record:
             cap = min(cap, max(self.record_budget_bytes // (8 * S), 4096))
@@ -594,6 +613,9 @@ class BatchedGPUSampler(Sampler):
                                   eps_dev=thr[0], eps_scale=thr[1])
             else:
                 idx, cnt = fr.run(lo, B, spec.eps, cap=need, filter=filt, rec_x=rx)
+            hook, self.on_first_launch = self.on_first_launch, None
+            if hook is not None:
+                hook()
             if ws == 1:
                 # one read: the count and the index of the need-th accepted
                 kk = min(need, B)
@@ -659,7 +681,10 @@ class BatchedGPUSampler(Sampler):
             tot_B += ws * B
             tot_cnt += int(counts.sum())
             rate, measured = max(int(counts.sum()) / float(ws * B), 1e-12), True
-        self._acc_rate = max(tot_cnt / float(max(tot_B, 1)), 1e-12)
+        new_rate = max(tot_cnt / float(max(tot_B, 1)), 1e-12)
+        if self._acc_rate:
+            self._acc_trend = min(1.0, max(0.5, new_rate / self._acc_rate))
+        self._acc_rate = new_rate
         if n_acc < n:
             ok = False
         out = self._assemble(spec, cols["theta"], cols["lp"], cols["dist"],

@@ -539,6 +539,15 @@ class ABCSMC:
             self.sampler.max_nr_recorded = self.max_nr_recorded_particles
         t_max = t0 + max_nr_populations - 1
         t = t0
+        # host reads deferred past the next generation's first launch (the
+        # ESS line of generation t): a sampler with an on_first_launch hook
+        # runs them once its first round is queued, so the host never waits
+        # for the transition density while the GPU runs dry behind it
+        pending = []
+
+        def flush():
+            while pending:
+                pending.pop(0)()
         while t <= t_max:
             # the threshold is read after the sample: the fused rounds take
             # it on the device (GenerationSpec.eps_device), so the first round
@@ -548,9 +557,16 @@ class ABCSMC:
             pop_size = self.population_size(t)
             max_eval = (np.inf if min_acceptance_rate == 0.
                         else pop_size / min_acceptance_rate)
-            sample = self.sampler.sample_until_n_accepted(
-                pop_size, simulate_one, max_eval,
-                show_progress=self.show_progress)
+            if pending and hasattr(self.sampler, "on_first_launch"):
+                self.sampler.on_first_launch = flush
+            try:
+                sample = self.sampler.sample_until_n_accepted(
+                    pop_size, simulate_one, max_eval,
+                    show_progress=self.show_progress)
+            finally:
+                if hasattr(self.sampler, "on_first_launch"):
+                    self.sampler.on_first_launch = None
+                flush()
             current_eps = self.eps(t)
             logger.info(f"t: {t}, eps: {current_eps}.")
             if not sample.ok:
@@ -568,12 +584,18 @@ class ABCSMC:
             ess_read = self._ess_async(population)
             self._prepare_next_iteration(t + 1, sample, population,
                                          acceptance_rate)
-            ess = ess_read()
-            logger.info(f"Acceptance rate: {pop_size} / {n_sim} = "
-                        f"{acceptance_rate:.4e}, ESS={ess:.4e}.")
-            self.generation_log.append(dict(
-                t=t, eps=float(current_eps), n_sim=int(n_sim), ess=float(ess),
-                seconds=(datetime.datetime.now() - t_start).total_seconds()))
+            entry = dict(t=t, eps=float(current_eps), n_sim=int(n_sim), ess=None,
+                         seconds=(datetime.datetime.now() - t_start).total_seconds())
+            self.generation_log.append(entry)
+
+            def log_ess(entry=entry, ess_read=ess_read, pop_size=pop_size,
+                        n_sim=n_sim, rate=acceptance_rate):
+                entry["ess"] = ess = float(ess_read())
+                logger.info(f"Acceptance rate: {pop_size} / {n_sim} = "
+                            f"{rate:.4e}, ESS={ess:.4e}.")
+            pending.append(log_ess)
+            if not hasattr(self.sampler, "on_first_launch"):
+                flush()
             if self.generation_callback is not None:
                 self.generation_callback(t)
             if current_eps <= minimum_epsilon:
@@ -587,6 +609,7 @@ class ABCSMC:
                 logger.info("Stopping: minimum acceptance rate.")
                 break
             t += 1
+        flush()
         self.history.done()
         return self.history
 
@@ -690,6 +713,10 @@ class ABCSMC:
 
     def _adapt_population_size(self, t):
         if t == 0:
+            return
+        if type(self.population_size).update is PopulationStrategy.update:
+            # the strategy ignores the transitions (ConstantPopulationSize):
+            # no copies of them, no model-probability table
             return
         w = np.array(list(self.history.model_probabilities_dict(
             self.history.max_t).values()))

@@ -359,9 +359,17 @@ class MultivariateNormalTransition(Transition):
 class _LazyFrame:
     """DataFrame view of a device population, materialised on first use."""
 
+    _index_cache = {}
+
     def __init__(self, Xd, columns):
         self._Xd = Xd
-        self.columns = pd.Index(columns)
+        key = tuple(columns)
+        idx = _LazyFrame._index_cache.get(key)
+        if idx is None:
+            # one pandas Index per column set (building one costs ~0.1 ms,
+            # once per fit otherwise)
+            idx = _LazyFrame._index_cache[key] = pd.Index(columns)
+        self.columns = idx
         self._df = None
 
     def _frame(self):
@@ -374,9 +382,10 @@ class _LazyFrame:
 
     def __deepcopy__(self, memo):
         # the device population is immutable after fit: share it, and do not
-        # materialise the host frame just to copy it
-        new = _LazyFrame(self._Xd, list(self.columns))
-        new._df = self._df
+        # materialise the host frame just to copy it (the column Index is
+        # immutable too)
+        new = _LazyFrame.__new__(_LazyFrame)
+        new._Xd, new.columns, new._df = self._Xd, self.columns, self._df
         return new
 
     def __getattr__(self, item):

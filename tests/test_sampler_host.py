@@ -47,8 +47,14 @@ def test_lazy_capable_priors_and_min_stats():
 
 def test_fused_round_sizing():
     s = BatchedGPUSampler(seed=1)
-    # need / rate (+6% once measured) / ranks + 4096, capped by the launch budget
-    assert s._fused_size(1000, 1, 0.01, False, 10, False) == 1000 * 100 + 4096
+    # need / rate (+6% once measured) / ranks + 4096, capped by the launch budget;
+    # a first round: rate x the last drop, spare min(10%, 4e6 candidates per rank)
+    assert s._fused_size(1000, 1, 0.01, False, 10, False) == int(1000 * 100 * 1.1 + 4096)
+    s._acc_trend = 0.8
+    n, r = 10 ** 7, 0.01
+    assert s._fused_size(n, 2, r, False, 10, False) == \
+        int(n / (r * 0.8) * (1 + 4e6 * 2 * r * 0.8 / n) / 2 + 4096)
+    s._acc_trend = 1.0
     assert s._fused_size(1000, 2, 0.01, True, 10, False) == int(1000 * 100 * 1.06 / 2 + 4096)
     assert s._fused_size(10 ** 9, 1, 1e-6, True, 10, False) == s.max_fused_batch_size
     # record_rejected: rows of S doubles within record_budget_bytes
