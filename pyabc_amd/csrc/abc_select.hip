@@ -15,7 +15,7 @@
 //   col_bracket_kernel  one streaming, coalesced read of the whole matrix
 //                       (each thread owns one column of a row band) counts
 //                       the keys below each column's window and compacts
-//                       the window (~12% of the column) into scratch;
+//                       the window (~9% of the column) into scratch;
 //   col_select_kernel   one 1024-thread workgroup per column selects the
 //                       rank-k key inside the window with 12-bit MSD digits:
 //     level 0: histogram of bits 63..52 (LDS atomics), pick the bin holding
@@ -50,13 +50,13 @@ __device__ __forceinline__ double key2f_s(uint64_t k) {
 
 // sample bracketing: columns with R >= BR_MIN first take SMP evenly spaced
 // keys, sort them in LDS and keep only the keys between the sample order
-// statistics BR_MARG places either side of the wanted rank(s) (5.7 sigma of
+// statistics BR_MARG places either side of the wanted rank(s) (5.75 sigma of
 // the sample rank at the median).  One streaming pass counts the keys below
 // the window and compacts the window into scratch; the radix levels then run
-// on ~12% of the column.  When the rank is not inside the window (a sample
+// on ~9% of the column.  When the rank is not inside the window (a sample
 // that misrepresents the column) the full radix select runs instead.
-constexpr int SMP = 2 * SEL_T;
-constexpr int BR_MARG = 128;
+constexpr int SMP = 4 * SEL_T;
+constexpr int BR_MARG = 184;
 constexpr int64_t BR_MIN = 4 * SMP;
 constexpr int BR_U = 8;  // keys in flight per thread in the bracket pass
 
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(SEL_T) void col_sample_kernel(
 // (heavy ties: a constant column is all window) sends the rest straight to
 // scratch, one returning global atomic per key.  The order of the compacted
 // keys is not deterministic; the selection does not depend on it.
-constexpr int BK_T = 256, BK_U = 8, BK_ROWS = 96, BK_CAP = 4096;
+constexpr int BK_T = 256, BK_U = 16, BK_ROWS = 160, BK_CAP = 4096;
 template <bool DEV>
 __global__ __launch_bounds__(BK_T) void col_bracket_kernel(
     const double* __restrict__ X, int64_t R, int S, const double* __restrict__ med,
@@ -379,8 +379,14 @@ int column_mad_select(const double* X, int64_t R, int S, double* out, void* ws,
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "column_mad: workspace carve");
   const int CB = S < BK_T ? S : BK_T;
   const int ctiles = (int)ceil_div(S, CB);
-  // expected window keys per band ~12.5% x 96 x 256 = 3072 < BK_CAP (measured
-  // at c4: 96 rows 1.17 ms per MAD, 64 rows 1.44, 128 rows 1.17-1.28)
+  // expected window keys per band 2 BR_MARG / SMP = 9% x 160 x 256 = 3680 <
+  // BK_CAP.  Measured at c4 (same box, tools/ab_mad.sh): SMP 2048 / 96 rows /
+  // 8 loads in flight 1.12 ms per MAD; 16 in flight 1.12; SMP 4096 / 128 rows
+  // 1.05; SMP 4096 / 160 rows / 16 in flight 1.03.  Without the compaction
+  // the bracket pass streams at 253 us (the colsum rate); with it 367 us.
+  // Per-column LDS segments flushed 64 keys a store over 64-column tiles
+  // were slower (470 us: a block then reads 512-B pieces of 512 rows
+  // instead of whole 2-KB rows)
   const int64_t rpb = BK_ROWS;
   const unsigned nb = (unsigned)ceil_div(R, rpb);
   for (int pass = 0; pass < 2; ++pass) {
