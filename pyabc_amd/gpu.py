@@ -24,11 +24,18 @@ class NoDeviceError(RuntimeError):
     pass
 
 
+_have_device = False
+
+
 def require_device():
-    """The GPU path needs a HIP device and the native library: fail loudly."""
-    if torch is None or not torch.cuda.is_available():
-        raise NoDeviceError("pyabc_amd GPU path needs an MI355X (HIP device)")
-    nat.load()
+    """The GPU path needs a HIP device and the native library: fail loudly.
+    (The availability check runs once: it reads the environment each time.)"""
+    global _have_device
+    if not _have_device:
+        if torch is None or not torch.cuda.is_available():
+            raise NoDeviceError("pyabc_amd GPU path needs an MI355X (HIP device)")
+        nat.load()
+        _have_device = True
     return torch.device("cuda", torch.cuda.current_device())
 
 
@@ -447,6 +454,15 @@ class CandidateRound:
                      p(idx.contiguous()), n, p(theta), p(lp), p(anc), p(x), p(dist),
                      stream_ptr())
         return theta, lp, anc, x, dist
+
+    def regen_into(self, idx0, idx_ptr, n, ptrs):
+        """regen into raw device addresses (theta, lp, anc, x, dist rows of
+        n candidates; idx_ptr: their int64 indices) -- the sampler's pooled
+        per-generation rows, whose views it builds once per generation."""
+        import ctypes as C
+        if n:
+            nat.call("abc_candidates_regen", C.addressof(self.spec), int(idx0), idx_ptr,
+                     int(n), *ptrs, stream_ptr())
 
 
 def _ptr(t):

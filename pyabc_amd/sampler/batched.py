@@ -183,9 +183,10 @@ class BatchedGPUSampler(Sampler):
         self._acc_rate = None
         self._acc_trend = 1.0
         self.last_stats = {}
-        # set by ABCSMC.run: host reads of the previous generation, run once
-        # the first fused round is queued (the GPU has work while they wait)
-        self.on_first_launch = None
+        # set by ABCSMC.run: host reads of the previous generation (its ESS
+        # line), run once this generation's transition density is queued --
+        # the longest kernel, so the host work overlaps it
+        self.on_density_queued = None
 
     def _base_seed(self, device):
         if self.seed is None:
@@ -576,7 +577,10 @@ class BatchedGPUSampler(Sampler):
         cols = {k: [] for k in ("theta", "lp", "dist", "x", "anc")}
         rec_x, rec_keeps, keeps = [], [], []
         arena, arena_off = None, 0
-        kept, kept_off = None, 0
+        # kept rows: pooled buffers filled through raw addresses (one set of
+        # views per buffer, built after the loop)
+        kept, kept_off, kept_segs = None, 0, []
+        row_bytes = (8 * fr.d, 8, 8, 8 * S, 8)
         rec_left = self._record_limit(S)
         cut = None
         n_acc = n_eval = base = rounds = 0
@@ -613,9 +617,6 @@ class BatchedGPUSampler(Sampler):
                                   eps_dev=thr[0], eps_scale=thr[1])
             else:
                 idx, cnt = fr.run(lo, B, spec.eps, cap=need, filter=filt, rec_x=rx)
-            hook, self.on_first_launch = self.on_first_launch, None
-            if hook is not None:
-                hook()
             if ws == 1:
                 # one read: the count and the index of the need-th accepted
                 kk = min(need, B)
@@ -652,15 +653,15 @@ class BatchedGPUSampler(Sampler):
             if k_mine:
                 # kept rows regenerated straight into one per-generation
                 # buffer (rows of later rounds follow): no concatenation
-                if kept is None or kept_off + k_mine > kept[0].shape[0]:
-                    kept = self._kept_buffers(max(n - n_acc, k_mine), fr.d, S, dev)
+                if kept is None or kept_off + k_mine > kept[1]:
+                    if kept is not None and kept_off:
+                        kept_segs.append((kept[0], kept_off))
+                    views = self._kept_buffers(max(n - n_acc, k_mine), fr.d, S, dev)
+                    kept = (views, views[0].shape[0], [v.data_ptr() for v in views])
                     kept_off = 0
-                th, lp, anc, x, dist = fr.regen(
-                    lo, idx[:k_mine], out=tuple(a[kept_off:kept_off + k_mine] for a in kept))
+                fr.regen_into(lo, idx.data_ptr(), k_mine,
+                              [a + kept_off * b for a, b in zip(kept[2], row_bytes)])
                 kept_off += k_mine
-                for k, v in zip(("theta", "lp", "dist", "x", "anc"),
-                                (th, lp, dist, x, anc)):
-                    cols[k].append(v)
             if record and cut is not None and rx is not None:
                 rec_x.append(rx)            # trimmed in _finish_cut
                 rec_keeps.append(None)
@@ -681,6 +682,12 @@ class BatchedGPUSampler(Sampler):
             tot_B += ws * B
             tot_cnt += int(counts.sum())
             rate, measured = max(int(counts.sum()) / float(ws * B), 1e-12), True
+        if kept is not None and kept_off:
+            kept_segs.append((kept[0], kept_off))
+        for views, cnt in kept_segs:
+            th, lp, anc, x, dist = (v[:cnt] for v in views)
+            for k, v in zip(("theta", "lp", "dist", "x", "anc"), (th, lp, dist, x, anc)):
+                cols[k].append(v)
         new_rate = max(tot_cnt / float(max(tot_B, 1)), 1e-12)
         if self._acc_rate:
             self._acc_trend = min(1.0, max(0.5, new_rate / self._acc_rate))
@@ -922,6 +929,9 @@ class BatchedGPUSampler(Sampler):
             anc = (cat(acc_anc) if acc_anc and
                    len(acc_anc) == len(acc_theta) else None)
             lt = spec.transition.logpdf_device(theta, hint=anc)
+            hook, self.on_density_queued = self.on_density_queued, None
+            if hook is not None:
+                hook()
             hl = host_prior_logpdf(theta, getattr(spec, "host_prior", None))
             if hl is not None:
                 lp = lp + hl      # the host-scipy leg's density factors

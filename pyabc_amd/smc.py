@@ -539,10 +539,10 @@ class ABCSMC:
             self.sampler.max_nr_recorded = self.max_nr_recorded_particles
         t_max = t0 + max_nr_populations - 1
         t = t0
-        # host reads deferred past the next generation's first launch (the
-        # ESS line of generation t): a sampler with an on_first_launch hook
-        # runs them once its first round is queued, so the host never waits
-        # for the transition density while the GPU runs dry behind it
+        # host reads deferred into the next generation (the ESS line of
+        # generation t): a sampler with an on_density_queued hook runs them
+        # once that generation's transition density is queued, so the host
+        # never waits for a density while the GPU runs dry behind it
         pending = []
 
         def flush():
@@ -557,15 +557,15 @@ class ABCSMC:
             pop_size = self.population_size(t)
             max_eval = (np.inf if min_acceptance_rate == 0.
                         else pop_size / min_acceptance_rate)
-            if pending and hasattr(self.sampler, "on_first_launch"):
-                self.sampler.on_first_launch = flush
+            if pending and hasattr(self.sampler, "on_density_queued"):
+                self.sampler.on_density_queued = flush
             try:
                 sample = self.sampler.sample_until_n_accepted(
                     pop_size, simulate_one, max_eval,
                     show_progress=self.show_progress)
             finally:
-                if hasattr(self.sampler, "on_first_launch"):
-                    self.sampler.on_first_launch = None
+                if hasattr(self.sampler, "on_density_queued"):
+                    self.sampler.on_density_queued = None
                 flush()
             current_eps = self.eps(t)
             logger.info(f"t: {t}, eps: {current_eps}.")
@@ -594,7 +594,7 @@ class ABCSMC:
                 logger.info(f"Acceptance rate: {pop_size} / {n_sim} = "
                             f"{rate:.4e}, ESS={ess:.4e}.")
             pending.append(log_ess)
-            if not hasattr(self.sampler, "on_first_launch"):
+            if not hasattr(self.sampler, "on_density_queued"):
                 flush()
             if self.generation_callback is not None:
                 self.generation_callback(t)

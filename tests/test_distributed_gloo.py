@@ -177,6 +177,19 @@ class _FusedRound:
             o.copy_(r.reshape(o.shape))
         return tuple(out)
 
+    def regen_into(self, lo, idx_ptr, n, ptrs):
+        """The sampler's raw-address path (host tensors here): the rows are
+        written at the addresses it computed, so its offsets are checked."""
+        import ctypes
+        if not n:
+            return
+        i = np.ctypeslib.as_array((ctypes.c_int64 * n).from_address(idx_ptr)).copy()
+        th, lp, anc, x, d = self._rows(lo, int(i.max()) + 1)
+        for ptr, a, dt in zip(ptrs, (th, lp, anc, x, d),
+                              (np.float64, np.float64, np.int64, np.float64, np.float64)):
+            r = np.ascontiguousarray(a[i], dtype=dt)
+            ctypes.memmove(ptr, r.ctypes.data, r.nbytes)
+
 
 def _run(n, eps, batch, record, fused=False):
     """fused: False (staged distance + compaction), True (fused rounds) or

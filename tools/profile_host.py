@@ -39,7 +39,12 @@ def main():
           f"per gen {[round(1e3 * g['seconds'], 2) for g in abc.generation_log[-a.gens:]]}")
     st = pstats.Stats(pr)
     st.sort_stats("cumulative").print_stats(a.top)
-    st.sort_stats("tottime").print_stats(a.top)
+    # microseconds per generation (pstats prints milliseconds at best)
+    rows = sorted(st.stats.items(), key=lambda kv: -kv[1][2])[:a.top]
+    print(f"{'own us/gen':>10} {'cum us/gen':>10} {'calls/gen':>9}  function")
+    for (f, line, name), (cc, nc, tt, ct, _) in rows:
+        print(f"{1e6 * tt / a.gens:10.1f} {1e6 * ct / a.gens:10.1f} {nc / a.gens:9.1f}  "
+              f"{os.path.basename(f)}:{line}({name})")
 
 
 if __name__ == "__main__":
