@@ -136,8 +136,8 @@ int abc_normalize_weights(double* w, int64_t N, double* stats, void* ws,
  *   its MFMA work).  Invalid rows (outside [0, N) or w <= 0) send the
  *   candidate to the fp64 rescue path.  With hints, candidates whose hinted
  *   offset proves too far below their maximum are re-run through the exact
- *   (unhinted) pass on a gathered subset: the call then reads that count
- *   back (one stream synchronisation). */
+ *   (unhinted) pass on a gathered subset, launched device-sized (waves past
+ *   the subset's device-side count leave): no host read. */
 size_t abc_mvn_packed_bytes(int64_t N, int r, int prec);
 int abc_mvn_pack_population(const double* X, const double* w, int64_t N, int d,
                             const double* mu, const double* U, int r,
@@ -324,11 +324,14 @@ int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0,
                          void* ws, size_t ws_bytes, void* stream);
 /* Rows of the kept candidates: for i < n, candidate idx0 + idx[i] ->
  * theta [n x d], prior log-density [n], ancestor [n] (nullable; -1 at t = 0),
- * sum stats x [n x S], distance [n]; bit-identical to the staged kernels. */
+ * sum stats x [n x S], distance [n]; bit-identical to the staged kernels.
+ * n_dev (nullable, device int64): the rows are the first min(n, *n_dev) --
+ * a launch sized on the device (abc_candidates_round's count), queued before
+ * the host has read that count. */
 int abc_candidates_regen(const abc_candidate_spec* spec, int64_t idx0,
-                         const int64_t* idx, int64_t n, double* theta,
-                         double* prior_logpdf, int64_t* ancestor, double* x,
-                         double* dist, void* stream);
+                         const int64_t* idx, int64_t n, const int64_t* n_dev,
+                         double* theta, double* prior_logpdf, int64_t* ancestor,
+                         double* x, double* dist, void* stream);
 
 /* Proposals only, candidates idx0 .. idx0 + B - 1: theta [B x d], prior
  * log-density [B] (-inf when the proposal gave up; may be null -- the

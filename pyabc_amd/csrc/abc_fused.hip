@@ -332,11 +332,15 @@ __global__ __launch_bounds__(256) void bits_write_kernel(
 template <int D, int MODE>
 __global__ __launch_bounds__(256) void fused_regen_kernel(
     RoundArgs A, int64_t idx0, const int64_t* __restrict__ idx, int64_t n,
-    double* __restrict__ theta, double* __restrict__ lp, int64_t* __restrict__ anc,
-    double* __restrict__ x, double* __restrict__ dist) {
+    const int64_t* __restrict__ n_dev, double* __restrict__ theta, double* __restrict__ lp,
+    int64_t* __restrict__ anc, double* __restrict__ x, double* __restrict__ dist) {
   constexpr int DM = D > 0 ? D : 64;
   __shared__ BlockConsts C;
   __shared__ double stage[FR_T][XCH + 1];
+  // device-sized launch: blocks past the round's count leave at once
+  // (uniform per block, before any barrier)
+  if (n_dev && *n_dev < n) n = *n_dev > 0 ? *n_dev : 0;
+  if ((int64_t)blockIdx.x * FR_T >= n) return;
   stage_block_consts<D, MODE>(C, A.P, &A.M, nullptr);
   const int d = D > 0 ? D : A.P.d;
   const int64_t i0 = (int64_t)blockIdx.x * FR_T;
@@ -854,9 +858,9 @@ extern "C" int abc_candidates_propose(const abc_candidate_spec* spec, int64_t id
 }
 
 extern "C" int abc_candidates_regen(const abc_candidate_spec* spec, int64_t idx0,
-                                    const int64_t* idx, int64_t n, double* theta,
-                                    double* prior_logpdf, int64_t* ancestor, double* x,
-                                    double* dist, void* stream) {
+                                    const int64_t* idx, int64_t n, const int64_t* n_dev,
+                                    double* theta, double* prior_logpdf, int64_t* ancestor,
+                                    double* x, double* dist, void* stream) {
   const int rc = check_spec(spec);
   if (rc != ABC_OK) return rc;
   ABC_CHECK_ARG(n >= 0, "candidates_regen: n < 0");
@@ -866,7 +870,7 @@ extern "C" int abc_candidates_regen(const abc_candidate_spec* spec, int64_t idx0
   hipStream_t s = as_stream(stream);
   profile_start(s, ABC_PROF_REGEN);
   ABC_FUSED_DISPATCH(fused_regen_kernel, dim3((unsigned)ceil_div(n, 256)), s, A, idx0, idx, n,
-                     theta, prior_logpdf, ancestor, x, dist);
+                     n_dev, theta, prior_logpdf, ancestor, x, dist);
   profile_stop(s, ABC_PROF_REGEN);
   ABC_LAUNCHED();
   return ABC_OK;

@@ -451,18 +451,20 @@ class CandidateRound:
             dist = torch.empty(n, dtype=F64, device=dev)
         if n:
             nat.call("abc_candidates_regen", C.addressof(self.spec), int(idx0),
-                     p(idx.contiguous()), n, p(theta), p(lp), p(anc), p(x), p(dist),
+                     p(idx.contiguous()), n, None, p(theta), p(lp), p(anc), p(x), p(dist),
                      stream_ptr())
         return theta, lp, anc, x, dist
 
-    def regen_into(self, idx0, idx_ptr, n, ptrs):
+    def regen_into(self, idx0, idx_ptr, n, ptrs, n_dev=None):
         """regen into raw device addresses (theta, lp, anc, x, dist rows of
         n candidates; idx_ptr: their int64 indices) -- the sampler's pooled
-        per-generation rows, whose views it builds once per generation."""
+        per-generation rows, whose views it builds once per generation.
+        n_dev (device int64 [1]): the rows are the first min(n, n_dev[0]),
+        so the launch can be queued before the host has read that count."""
         import ctypes as C
         if n:
             nat.call("abc_candidates_regen", C.addressof(self.spec), int(idx0), idx_ptr,
-                     int(n), *ptrs, stream_ptr())
+                     int(n), p(n_dev), *ptrs, stream_ptr())
 
 
 def _ptr(t):

@@ -617,6 +617,21 @@ class BatchedGPUSampler(Sampler):
                                   eps_dev=thr[0], eps_scale=thr[1])
             else:
                 idx, cnt = fr.run(lo, B, spec.eps, cap=need, filter=filt, rec_x=rx)
+            spec_regen = False
+            if ws == 1:
+                # the kept rows' regeneration is queued before the count read,
+                # sized on the device (min(count, need) rows into the pooled
+                # buffer), so the GPU is busy while the host reads the count
+                if kept is None or kept_off + need > kept[1]:
+                    if kept is not None and kept_off:
+                        kept_segs.append((kept[0], kept_off))
+                    views = self._kept_buffers(need, fr.d, S, dev)
+                    kept = (views, views[0].shape[0], [v.data_ptr() for v in views])
+                    kept_off = 0
+                fr.regen_into(lo, idx.data_ptr(), min(need, B),
+                              [a + kept_off * b for a, b in zip(kept[2], row_bytes)],
+                              n_dev=cnt)
+                spec_regen = True
             if ws == 1:
                 # one read: the count and the index of the need-th accepted
                 kk = min(need, B)
@@ -650,7 +665,9 @@ class BatchedGPUSampler(Sampler):
                     rec_all[c_rank + 1:] = 0
             else:
                 evaluated = ws * B
-            if k_mine:
+            if k_mine and spec_regen:
+                kept_off += k_mine          # regenerated before the count read
+            elif k_mine:
                 # kept rows regenerated straight into one per-generation
                 # buffer (rows of later rounds follow): no concatenation
                 if kept is None or kept_off + k_mine > kept[1]:

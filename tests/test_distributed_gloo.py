@@ -177,10 +177,13 @@ class _FusedRound:
             o.copy_(r.reshape(o.shape))
         return tuple(out)
 
-    def regen_into(self, lo, idx_ptr, n, ptrs):
+    def regen_into(self, lo, idx_ptr, n, ptrs, n_dev=None):
         """The sampler's raw-address path (host tensors here): the rows are
-        written at the addresses it computed, so its offsets are checked."""
+        written at the addresses it computed, so its offsets are checked;
+        n_dev: the round's count (rows = min(n, count), as on the device)."""
         import ctypes
+        if n_dev is not None:
+            n = min(int(n), int(n_dev.reshape(-1)[0]))
         if not n:
             return
         i = np.ctypeslib.as_array((ctypes.c_int64 * n).from_address(idx_ptr)).copy()
