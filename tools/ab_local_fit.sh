@@ -1,6 +1,6 @@
 #!/bin/bash
 # c5 LocalTransition fit kernel averages (rocprofv3) for the in-tree library
-# and variants given as arguments (built with tools/build_variant.sh).
+# and variants given as arguments (built with tools/build_src_variant.sh).
 export TMPDIR=/tmp PYTHONPATH=$PWD
 mkdir -p gpurun_out
 for L in pyabc_amd/libabcgpu.so "$@"; do
