@@ -419,6 +419,58 @@ def test_stochastic_abc_gave_up_proposals():
 
 
 @gpu_mark
+def test_prior_logpdf_wide_vs_scipy():
+    """abc_prior_logpdf above d = 64 (the StochasticAcceptor's temperature
+    records need the prior density of every recorded theta): d = 80, mixed
+    families, points inside and outside the supports, vs scipy (1e-12)."""
+    from scipy import stats
+    from pyabc_amd import gpu
+    d, B = 80, 777
+    rng = np.random.default_rng(17)
+    kinds = np.array([0, 1, 2, 3] * (d // 4), dtype=np.int32)
+    params = np.zeros((d, 4))
+    params[:, 0] = rng.uniform(-1, 1, d)
+    params[:, 1] = rng.uniform(0.5, 2, d)
+    theta = rng.normal(0, 2, (B, d))
+    lp = gpu.prior_logpdf(gpu.as_dev(theta), gpu.as_dev(kinds, dtype=gpu.torch.int32),
+                          gpu.as_dev(params.ravel())).cpu().numpy()
+    fam = {0: stats.norm, 1: stats.uniform, 2: stats.expon, 3: stats.laplace}
+    ref = sum(fam[int(kinds[k])].logpdf(theta[:, k], params[k, 0], params[k, 1])
+              for k in range(d))
+    fin = np.isfinite(ref)
+    assert 0 < fin.sum() < B
+    np.testing.assert_array_equal(np.isfinite(lp), fin)
+    np.testing.assert_allclose(lp[fin], ref[fin], rtol=1e-12)
+
+
+@gpu_mark
+def test_stochastic_abc_wide_records():
+    """d = 80 under a StochasticAcceptor and a Temperature: generation 1
+    weighs the records of generation 0 with the prior density on the device
+    (above d = 64) and both transition densities; the populations are finite
+    and normalised and the temperatures stay >= 1."""
+    import pyabc_amd as pa
+    d = 80
+    names = [f"p{i:02d}" for i in range(d)]
+    keys = [f"y{i:02d}" for i in range(d)]
+    model = pa.LinearGaussianModel(names, keys, src=list(range(d)), sigma=[0.0] * d)
+    prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
+    abc = pa.ABCSMC(model, prior, pa.IndependentNormalKernel(var=[4.0] * d),
+                    population_size=400, sampler=pa.BatchedGPUSampler(seed=23),
+                    eps=pa.Temperature(), acceptor=pa.StochasticAcceptor())
+    abc.new("sqlite://", {k: 0.3 for k in keys})
+    h = abc.run(max_nr_populations=3)
+    assert h.max_t >= 1
+    for t in range(h.max_t + 1):
+        df, w = h.get_distribution(0, t)
+        assert df.shape[1] == d and np.isfinite(df.to_numpy()).all()
+        assert np.isfinite(w).all() and (w >= 0).all()
+        np.testing.assert_allclose(w.sum(), 1.0, rtol=1e-12)
+    temps = abc.eps.temperatures
+    assert all(np.isfinite(v) and v >= 1.0 for v in temps.values())
+
+
+@gpu_mark
 def test_stochastic_abc_per_particle_and_pdf_norms():
     """test_acceptor.py:72-128 on the per-particle path (array-valued sum
     stats, user model) for every pdf normalisation."""
