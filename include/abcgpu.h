@@ -111,8 +111,9 @@ int abc_normalize_weights(double* w, int64_t N, double* stats, void* ws,
                           size_t ws_bytes, void* stream);
 
 /* ---- MultivariateNormalTransition.pdf (multivariatenormal.py:99-113) -----
- * density(x_i) = sum_j w_j N(x_i - X_j; 0, Sigma).  Host supplies the fp64
- * eigen-whitening of Sigma (scipy _PSD semantics): U [d x r], mean mu [d].
+ * density(x_i) = sum_j w_j N(x_i - X_j; 0, Sigma).  The caller supplies the
+ * fp64 whitening of Sigma (scipy _PSD semantics; abc_mvn_fit computes it on
+ * the device): U [d x r], mean mu [d].
  * pack: builds the MFMA A-operand image of the population once per fit:
  *   y_j = (X_j - mu) U,  c_j = log(w_j) + log_w_shift - |y_j|^2 / 2
  * (log_w_shift = -log max w keeps every exponent <= 0; log_w_shift_dev,

@@ -7,7 +7,7 @@
 //
 // Reference: pyabc/transition/multivariatenormal.py:99-113,
 //   dens(x_i) = sum_j w_j N(x_i - X_j; 0, Sigma),
-// restated with the host's fp64 eigen-whitening U (U U^T = Sigma^-1) and the
+// restated with the fit's fp64 whitening U (U U^T = Sigma^-1; abc_mvn_fit) and the
 // log2 scaling folded into the coordinates (q = sqrt(log2 e)):
 //   y_j = q (X_j - mu) U,  z_i = q (x_i - mu) U
 //   s_ij = c_j - m_i + z_i . y_j              (log2 units, s_ij <= 0)
