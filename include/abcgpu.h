@@ -37,10 +37,11 @@ extern "C" {
 #define ABC_ERR_UNSUPPORTED (-5)
 #define ABC_ERR_COMM (-6)      /* RCCL missing or a collective failed */
 
-/* Largest parameter dimension d the proposal, prior-density and
- * LocalTransition entry points accept (one cap for all of them; the
- * runtime-d LocalTransition fit stages a member row of d + 1 doubles in LDS,
- * abc_local_wide.hip).  The fused candidate round takes d <= 64. */
+/* Largest parameter dimension d the proposal, prior-density, weighted-
+ * moments, direct MVN density and LocalTransition entry points accept (one
+ * cap for all of them; the runtime-d LocalTransition fit stages a member row
+ * of d + 1 doubles in LDS, abc_local_wide.hip).  The fused candidate round,
+ * the MVN pack / MFMA density and abc_mvn_fit take d <= 64. */
 #define ABC_MAX_D 2048
 
 /* Precision of the transition-density kernel. */
@@ -90,7 +91,8 @@ int abc_profile_channel(int channel, double* total_ms, int64_t* launches);
  * out[0] = sum w, out[1] = sum w^2, out[2 .. 2+d) = weighted mean
  * (sum w x / sum w), out[2+d .. 2+d+d*d) = sum w (x-mean)(x-mean)^T / sum w,
  * out[2+d+d*d] = max w (out holds 3 + d + d*d doubles).
- * Deterministic two-pass fp64 (per-block partials, fixed-order combine). */
+ * Deterministic two-pass fp64 (per-block partials, fixed-order combine);
+ * d <= ABC_MAX_D (above 64: one column / one covariance entry per thread). */
 size_t abc_weighted_moments_workspace(int64_t N, int d);
 int abc_weighted_moments(const double* X, const double* w, int64_t N, int d,
                          double* out, void* ws, size_t ws_bytes, void* stream);
@@ -182,7 +184,8 @@ int abc_mvn_logpdf(const double* x, int64_t M, int d, const void* packed,
                    void* stream);
 /* Direct-difference fp64 VALU path: any r, and scipy's singular-covariance
  * support mask (pairs with |(x_i - X_j) V| >= support_tol get density 0;
- * V [d x nv] null-space basis, nv = d - r). */
+ * V [d x nv] null-space basis, nv = d - r); d <= ABC_MAX_D (the
+ * MultivariateNormalTransition density above d = 64). */
 int abc_mvn_logpdf_direct(const double* x, int64_t M, const double* X,
                           const double* w, int64_t N, int d, const double* U,
                           int r, const double* V, int nv, double support_tol,

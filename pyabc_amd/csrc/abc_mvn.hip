@@ -314,6 +314,67 @@ __global__ __launch_bounds__(256) void mvn_direct_kernel(
   }
 }
 
+// d > 64: the candidate row in LDS (dynamic, d doubles), the differences
+// recomputed per whitening column from the population row (in cache); the
+// same per-pair arithmetic and (max, sum) reduction as mvn_direct_kernel
+__global__ __launch_bounds__(256) void mvn_direct_wide_kernel(
+    const double* __restrict__ x, int64_t M, const double* __restrict__ X,
+    const double* __restrict__ w, int64_t N, int d,
+    const double* __restrict__ U, int r, const double* __restrict__ V, int nv,
+    double tol, double log_const, double* __restrict__ out) {
+  extern __shared__ double xs[];
+  __shared__ double sm[4], sl[4];
+  const int64_t i = blockIdx.x;
+  if (i >= M) return;
+  for (int q = threadIdx.x; q < d; q += blockDim.x) xs[q] = x[i * d + q];
+  __syncthreads();
+  double m = -INFINITY, l = 0.0;
+  for (int64_t j = threadIdx.x; j < N; j += blockDim.x) {
+    const double wj = w[j];
+    if (!(wj > 0.0)) continue;
+    const double* Xj = X + j * d;
+    if (nv > 0) {
+      double res = 0.0;
+      for (int k = 0; k < nv; ++k) {
+        double p = 0.0;
+        for (int q = 0; q < d; ++q) p += (xs[q] - Xj[q]) * V[q * nv + k];
+        res += p * p;
+      }
+      if (!(sqrt(res) < tol)) continue;
+    }
+    double maha = 0.0;
+    for (int k = 0; k < r; ++k) {
+      double p = 0.0;
+      for (int q = 0; q < d; ++q) p += (xs[q] - Xj[q]) * U[q * r + k];
+      maha += p * p;
+    }
+    const double s = log(wj) - 0.5 * maha;
+    if (s > m) { l = l * exp(m - s) + 1.0; m = s; }
+    else l += exp(s - m);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    double mo = __shfl_xor(m, o, 64), lo = __shfl_xor(l, o, 64);
+    double mx = fmax(m, mo);
+    double s = 0.0;
+    if (l > 0.0) s += l * exp(m - mx);
+    if (lo > 0.0) s += lo * exp(mo - mx);
+    m = (l > 0.0 || lo > 0.0) ? mx : m;
+    l = s;
+  }
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { sm[wv] = m; sl[wv] = l; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double mx = -INFINITY;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k)
+      if (sl[k] > 0.0) mx = fmax(mx, sm[k]);
+    double s = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k)
+      if (sl[k] > 0.0) s += sl[k] * exp(sm[k] - mx);
+    out[i] = (s > 0.0) ? mx + log(s) + log_const : -INFINITY;
+  }
+}
+
 struct Plan {
   int KB, CT, nchunk;
   int64_t MT, NT, MTpad, groups, tiles_per_chunk, Mpad;
@@ -500,12 +561,17 @@ extern "C" int abc_mvn_logpdf_direct(const double* x, int64_t M,
                                      const double* V, int nv,
                                      double support_tol, double log_const,
                                      double* out, void* stream) {
-  ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= 64, "direct: bad M/N/d");
+  ABC_CHECK_ARG(M >= 0 && N >= 1 && d >= 1 && d <= ABC_MAX_D, "direct: bad M/N/d");
   ABC_CHECK_ARG(r >= 0 && r <= d && nv >= 0 && nv <= d, "direct: bad r/nv");
   if (M == 0) return ABC_OK;
   ABC_CHECK_ARG(x && X && w && out && (r == 0 || U) && (nv == 0 || V), "direct: null pointer");
-  hipLaunchKernelGGL(mvn_direct_kernel, dim3((unsigned)M), dim3(256), 0, as_stream(stream),
-                     x, M, X, w, N, d, U, r, V, nv, support_tol, log_const, out);
+  if (d > 64)
+    hipLaunchKernelGGL(mvn_direct_wide_kernel, dim3((unsigned)M), dim3(256),
+                       sizeof(double) * (size_t)d, as_stream(stream), x, M, X, w, N, d, U, r, V,
+                       nv, support_tol, log_const, out);
+  else
+    hipLaunchKernelGGL(mvn_direct_kernel, dim3((unsigned)M), dim3(256), 0, as_stream(stream),
+                       x, M, X, w, N, d, U, r, V, nv, support_tol, log_const, out);
   ABC_LAUNCHED();
   return ABC_OK;
 }

@@ -117,11 +117,54 @@ __global__ void moments2_final(const double* __restrict__ part, int nblk,
                                int d, double* __restrict__ out) {
   const int npair = d * d;
   const double sw = out[0];
-  for (int c = threadIdx.x; c < npair; c += blockDim.x) {
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < npair; c += gridDim.x * blockDim.x) {
     double s = 0.0;
     for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * npair + c];
     out[2 + d + c] = s / sw;
   }
+}
+
+// ---- wide path (d > 64): one column / one (a, b) entry per thread ---------
+// Rows are read straight from X (a block's threads read consecutive columns
+// of the same row: coalesced; the pair pass re-reads a row from cache).
+// Fixed block counts and combine order, as above.
+__global__ __launch_bounds__(256) void moments1_wide(const double* __restrict__ X,
+                                                     const double* __restrict__ w,
+                                                     int64_t N, int d,
+                                                     double* __restrict__ part) {
+  const int ncol = 2 + d;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= ncol) return;
+  double acc = 0.0;
+  for (int64_t r = blockIdx.x; r < N; r += gridDim.x) {
+    const double wr = w[r];
+    acc += (c == 0) ? wr : (c == 1 ? wr * wr : wr * X[r * d + (c - 2)]);
+  }
+  part[(int64_t)blockIdx.x * ncol + c] = acc;
+}
+
+__global__ __launch_bounds__(256) void moments2_wide(const double* __restrict__ X,
+                                                     const double* __restrict__ w,
+                                                     int64_t N, int d,
+                                                     const double* __restrict__ mom,
+                                                     double* __restrict__ part) {
+  const int64_t npair = (int64_t)d * d;
+  const int64_t pidx = (int64_t)blockIdx.y * 256 + threadIdx.x;
+  if (pidx >= npair) return;
+  const int a = (int)(pidx / d), b = (int)(pidx % d);
+  const double ma = mom[2 + a], mb = mom[2 + b];
+  double acc = 0.0;
+  for (int64_t r = blockIdx.x; r < N; r += gridDim.x)
+    acc += w[r] * (X[r * d + a] - ma) * (X[r * d + b] - mb);
+  part[(int64_t)blockIdx.x * npair + pidx] = acc;
+}
+
+// row blocks of the wide path: the pair partials stay <= 2^24 doubles
+int wide_blocks(int64_t N, int d) {
+  const int64_t cap = ((int64_t)1 << 24) / ((int64_t)d * d);
+  int64_t nb = cap < MOM_BLOCKS ? cap : MOM_BLOCKS;
+  if (nb < 1) nb = 1;
+  return (int)(N < nb ? N : nb);
 }
 
 // ---- fast path: d fixed at compile time, one row per thread ----------------
@@ -421,10 +464,10 @@ __global__ void wscale_kernel(double* __restrict__ w, int64_t N,
 using namespace abc;
 
 extern "C" size_t abc_weighted_moments_workspace(int64_t N, int d) {
-  (void)N;
+  const int64_t nb2 = d > 64 ? wide_blocks(N > 0 ? N : 1, d) : MOM_BLOCKS;
   size_t off = 0;
   size_only<double>(off, (size_t)MOM_BLOCKS * (2 + d));
-  size_only<double>(off, (size_t)MOM_BLOCKS * d * d);
+  size_only<double>(off, (size_t)nb2 * d * d);
   size_only<double>(off, (size_t)MOM_BLOCKS);
   size_only<double>(off, (size_t)d * d);
   return off + 256;
@@ -433,13 +476,13 @@ extern "C" size_t abc_weighted_moments_workspace(int64_t N, int d) {
 extern "C" int abc_weighted_moments(const double* X, const double* w,
                                     int64_t N, int d, double* out, void* ws,
                                     size_t ws_bytes, void* stream) {
-  ABC_CHECK_ARG(N >= 1 && d >= 1 && d <= 64, "moments: bad N=%lld d=%d", (long long)N, d);
+  ABC_CHECK_ARG(N >= 1 && d >= 1 && d <= ABC_MAX_D, "moments: bad N=%lld d=%d", (long long)N, d);
   ABC_CHECK_ARG(X && w && out && ws, "moments: null pointer");
   if (ws_bytes < abc_weighted_moments_workspace(N, d))
     return set_error(ABC_ERR_WORKSPACE, "moments: workspace too small");
   Carver cv(ws, ws_bytes);
   double* p1 = cv.take<double>((size_t)MOM_BLOCKS * (2 + d));
-  double* p2 = cv.take<double>((size_t)MOM_BLOCKS * d * d);
+  double* p2 = cv.take<double>((size_t)(d > 64 ? wide_blocks(N, d) : MOM_BLOCKS) * d * d);
   double* pmax = cv.take<double>((size_t)MOM_BLOCKS);
   double* tri = cv.take<double>((size_t)d * d);
   hipStream_t s = as_stream(stream);
@@ -451,6 +494,23 @@ extern "C" int abc_weighted_moments(const double* X, const double* w,
     ABC_MOM_CASE(12) ABC_MOM_CASE(16)
 #undef ABC_MOM_CASE
     default: break;
+  }
+  if (d > 64) {
+    const int nb = wide_blocks(N, d);
+    hipLaunchKernelGGL(moments1_wide, dim3(nb, (unsigned)ceil_div(2 + d, 256)), dim3(256), 0, s,
+                       X, w, N, d, p1);
+    ABC_LAUNCHED();
+    hipLaunchKernelGGL(moments1_final, dim3(1), dim3(256), 0, s, p1, nb, d, out);
+    ABC_LAUNCHED();
+    hipLaunchKernelGGL(moments2_wide, dim3(nb, (unsigned)ceil_div((int64_t)d * d, 256)), dim3(256),
+                       0, s, X, w, N, d, out, p2);
+    ABC_LAUNCHED();
+    hipLaunchKernelGGL(moments2_final, dim3((unsigned)ceil_div((int64_t)d * d, 256)), dim3(256), 0,
+                       s, p2, nb, d, out);
+    ABC_LAUNCHED();
+    hipLaunchKernelGGL(mom1_max_generic, dim3(1), dim3(256), 0, s, w, N, out + 2 + d + d * d);
+    ABC_LAUNCHED();
+    return ABC_OK;
   }
   const int nblk = (int)(ceil_div(N, MOM_ROWS) < MOM_BLOCKS ? ceil_div(N, MOM_ROWS) : MOM_BLOCKS);
   const size_t lds = sizeof(double) * (MOM_ROWS * d + MOM_ROWS);

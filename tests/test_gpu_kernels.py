@@ -738,6 +738,40 @@ def test_step_golden(dev):
     np.testing.assert_allclose(wts[acc], gg["weight"][acc], rtol=2e-6)
 
 
+@pytest.mark.parametrize("d,N,M", [(65, 300, 7), (80, 1000, 33), (130, 257, 5)])
+def test_wide_moments_and_direct_density(dev, d, N, M):
+    """MultivariateNormalTransition above d = 64: abc_weighted_moments' wide
+    path vs numpy (sum w, mean, biased covariance, max w: 1e-12) and the
+    direct fp64 density kernel vs the oracle's MVN mixture (1e-10), full rank
+    and singular (rank d - 5: scipy's support mask)."""
+    from pyabc_amd import gpu
+    rng = np.random.default_rng(d)
+    X = rng.normal(0, 1, (N, d)) * rng.uniform(0.5, 2, d)
+    w = rng.uniform(0.1, 1, N)
+    sw, sw2, mean, cov_b, wmax = gpu.weighted_moments(T(X), T(w), with_max=True)
+    np.testing.assert_allclose([sw, sw2, wmax], [w.sum(), (w ** 2).sum(), w.max()], rtol=1e-12)
+    mu = (w[:, None] * X).sum(0) / w.sum()
+    np.testing.assert_allclose(mean, mu, rtol=1e-12, atol=1e-14)
+    C = ((X - mu).T * w) @ (X - mu) / w.sum()
+    np.testing.assert_allclose(cov_b, C, rtol=1e-11, atol=1e-13 * np.abs(C).max())
+    wn = w / w.sum()
+    x = X[rng.integers(0, N, M)] + 0.3 * rng.normal(0, 1, (M, d))
+    for rank in (d, d - 5):
+        B = rng.normal(0, 1, (d, rank))
+        cov = B @ B.T / rank + (np.eye(d) * 0.5 if rank == d else 0.0)
+        from pyabc_amd.transition.multivariatenormal import psd_whitening
+        psd = psd_whitening(cov)
+        Xs = X if rank == d else mu + (X - mu) @ B @ np.linalg.pinv(B)   # on the subspace
+        xs = x if rank == d else mu + (x - mu) @ B @ np.linalg.pinv(B)
+        U, V = psd["U"], psd.get("V")
+        nv = 0 if V is None or psd["rank"] == d else V.shape[1]
+        log_norm = -0.5 * (psd["rank"] * np.log(2 * np.pi) + psd["log_pdet"])
+        got = gpu.mvn_logpdf_direct(T(xs), T(Xs), T(wn), T(U),
+                                    T(V) if nv else None, psd["tol"], log_norm).cpu().numpy()
+        ref = np.log(oracle.mvn_pdf(xs, Xs, wn, cov))
+        np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-10)
+
+
 def test_gather_rows_batch(dev):
     """One-launch gather of several column groups (fp64 matrices, fp64
     vectors, int64 ancestors) == index_select, for ragged sizes."""

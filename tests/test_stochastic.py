@@ -432,6 +432,12 @@ def test_prior_logpdf_wide_vs_scipy():
     params[:, 0] = rng.uniform(-1, 1, d)
     params[:, 1] = rng.uniform(0.5, 2, d)
     theta = rng.normal(0, 2, (B, d))
+    inside = kinds == 1      # uniform [loc, loc + scale]: mostly inside
+    theta[:, inside] = params[inside, 0] + params[inside, 1] * rng.uniform(0, 1, (B, inside.sum()))
+    expo = kinds == 2        # expon: support [loc, inf)
+    theta[:, expo] = params[expo, 0] + rng.exponential(1.0, (B, expo.sum()))
+    theta[:10, np.nonzero(inside)[0][0]] = params[inside, 0][0] - 1.0   # outside
+    theta[10:20, np.nonzero(expo)[0][0]] = params[expo, 0][0] - 0.5     # outside
     lp = gpu.prior_logpdf(gpu.as_dev(theta), gpu.as_dev(kinds, dtype=gpu.torch.int32),
                           gpu.as_dev(params.ravel())).cpu().numpy()
     fam = {0: stats.norm, 1: stats.uniform, 2: stats.expon, 3: stats.laplace}
