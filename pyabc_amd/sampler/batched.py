@@ -618,6 +618,7 @@ class BatchedGPUSampler(Sampler):
             else:
                 idx, cnt = fr.run(lo, B, spec.eps, cap=need, filter=filt, rec_x=rx)
             spec_regen = False
+            pair = self._queue_pair(cnt, idx, min(need, B) - 1) if ws == 1 else None
             if ws == 1:
                 # the kept rows' regeneration is queued before the count read,
                 # sized on the device (min(count, need) rows into the pooled
@@ -634,9 +635,7 @@ class BatchedGPUSampler(Sampler):
                 spec_regen = True
             if ws == 1:
                 # one read: the count and the index of the need-th accepted
-                kk = min(need, B)
-                both = torch.cat([cnt.view(1), idx[kk - 1:kk]]).cpu()
-                cnt_local, pos_hint = int(both[0]), int(both[1])
+                cnt_local, pos_hint = self._wait_pair(pair)
             else:
                 cnt_local = cnt
             counts = dd.allgather_counts(cnt_local, dev)
@@ -733,6 +732,29 @@ class BatchedGPUSampler(Sampler):
             recorded = out.sum_stats
         return ColumnarSample(out, recorded, spec.sum_stat_keys, record,
                               ok and n_acc == n)
+
+    def _queue_pair(self, cnt, idx, k):
+        """Queue the round's (count, idx[k]) into a cached pinned pair (two
+        async copies, no concatenation kernel, no allocation) and an event;
+        _wait_pair reads it.  Work queued after the event (the kept rows'
+        regeneration) runs while the host waits."""
+        torch = gpu.torch
+        if cnt.device.type != "cuda":              # host tensors (test doubles)
+            return (int(cnt.reshape(-1)[0]), int(idx[k]))
+        hp = getattr(self, "_pair_host", None)
+        if hp is None:
+            hp = self._pair_host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+            self._pair_ev = torch.cuda.Event()
+        hp[0:1].copy_(cnt.reshape(1), non_blocking=True)
+        hp[1:2].copy_(idx[k:k + 1], non_blocking=True)
+        self._pair_ev.record()
+        return None
+
+    def _wait_pair(self, queued):
+        if queued is not None:
+            return queued
+        self._pair_ev.synchronize()
+        return int(self._pair_host[0]), int(self._pair_host[1])
 
     # population columns of the fused rounds are carved from pooled device
     # arenas: a generation's new population (kept by the History) would
