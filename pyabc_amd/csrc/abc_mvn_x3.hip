@@ -191,21 +191,32 @@ __device__ __forceinline__ double whiten(const double* __restrict__ P, int64_t r
 }
 
 // max |y_j|^2 / 2 over the rows with w > 0 (atomicMax on the bit pattern of
-// a non-negative double, which is monotone).
+// a non-negative double, which is monotone).  Grid-stride over at most
+// POP_RANGE_BLOCKS blocks, one atomic per block: one per wave on the single
+// address serialised ~16k atomics per c3 population (0.2 ms).
+constexpr int POP_RANGE_BLOCKS = 1024;
 __global__ __launch_bounds__(256) void pop_range_kernel(
     const double* __restrict__ X, const double* __restrict__ w, int64_t N,
     int d, const double* __restrict__ mu, const double* __restrict__ U, int r,
     Header* __restrict__ hdr) {
-  const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ double wm[4];
   double h = 0.0;
-  if (row < N && w[row] > 0.0) {
-    double v[MAX_R];
-    h = whiten(X, row, d, mu, U, r, v);
+  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < N;
+       row += (int64_t)gridDim.x * blockDim.x) {
+    if (w[row] > 0.0) {
+      double v[MAX_R];
+      h = fmax(h, whiten(X, row, d, mu, U, r, v));
+    }
   }
   h = wave_max(h);
-  if ((threadIdx.x & 63) == 0 && h > 0.0)
-    atomicMax((unsigned long long*)&hdr->maxsq,
-              (unsigned long long)__double_as_longlong(h));
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    h = fmax(fmax(wm[0], wm[1]), fmax(wm[2], wm[3]));
+    if (h > 0.0)
+      atomicMax((unsigned long long*)&hdr->maxsq,
+                (unsigned long long)__double_as_longlong(h));
+  }
 }
 
 __global__ void x3_setup_kernel(Header* __restrict__ hdr, int r,
@@ -857,7 +868,9 @@ int x3_pack_population(const double* X, const double* w, int64_t N, int d,
   Header* hdr = (Header*)packed;
   ABC_HIP(hipMemsetAsync(hdr, 0, HDR, s));
   if (N > 0) {
-    hipLaunchKernelGGL(pop_range_kernel, dim3((unsigned)ceil_div(N, 256)), dim3(256),
+    const int64_t nb = ceil_div(N, 256);
+    hipLaunchKernelGGL(pop_range_kernel,
+                       dim3((unsigned)(nb < POP_RANGE_BLOCKS ? nb : POP_RANGE_BLOCKS)), dim3(256),
                        0, s, X, w, N, d, mu, U, r, hdr);
     ABC_LAUNCHED();
   }
