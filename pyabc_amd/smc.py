@@ -109,13 +109,22 @@ class GenerationSpec:
                                                        "propose_device"):
             why.append("transition has no device kernel")
         prior = abc.parameter_priors[0]
-        spec = prior.device_spec() if hasattr(prior, "device_spec") else None
+        # the prior's device form and host components, computed once per
+        # run() (ABCSMC.run resets the cache; the prior does not change
+        # during a run)
+        cached = abc.__dict__.get("_prior_spec_cache")
+        if cached is not None and cached[0] is prior:
+            spec, host = cached[1], cached[2]
+        else:
+            spec = prior.device_spec() if hasattr(prior, "device_spec") else None
+            host = prior.host_components() if spec is not None else []
+            abc.__dict__["_prior_spec_cache"] = (prior, spec, host)
         if spec is None:
             why.append("prior component without a batched form (not a scipy "
                        "RV, or a discrete / non-frozen scipy distribution "
                        "outside the device families)")
         # components without a device sampler: host-scipy density / draws
-        self.host_prior = prior.host_components() if spec is not None else []
+        self.host_prior = host
         self.why_not = "; ".join(why)
         self.batched_capable = not why
         if self.batched_capable:
@@ -529,6 +538,7 @@ class ABCSMC:
         self.min_acceptance_rate = min_acceptance_rate
         t0 = self.history.max_t + 1
         self.history.start_time = datetime.datetime.now()
+        self.__dict__.pop("_prior_spec_cache", None)
         self._fit_transitions(t0)
         self._adapt_population_size(t0)
         self._initialize_dist_eps_acc(t0)
