@@ -309,6 +309,31 @@ def test_fused_edges(dev):
     assert torch.equal(rec, ref["x"]) and int(cnt.cpu()) == ref["n"]
 
 
+def test_regen_device_sized(dev):
+    """abc_candidates_regen sized on the device (the sampler queues it before
+    reading the round's count): rows = min(n, *n_dev), identical to the
+    host-sized regeneration; rows past them untouched; count 0 writes
+    nothing."""
+    from pyabc_amd import gpu
+    c = _case(4, 6, seed=3)
+    fr = _round(c)
+    lo, B = 77, 20_000
+    for eps, cap in ((1.2, 50), (1.2, 100_000), (-1.0, 10)):
+        idx, cnt = fr.run(lo, B, eps, cap=cap)
+        n = min(int(cnt.cpu()), cap)
+        ref = fr.regen(lo, idx[:n]) if n else None
+        outs = (torch.full((cap, 4), 7.0, dtype=torch.float64, device=dev),
+                torch.full((cap,), 7.0, dtype=torch.float64, device=dev),
+                torch.full((cap,), 7, dtype=torch.int64, device=dev),
+                torch.full((cap, 6), 7.0, dtype=torch.float64, device=dev),
+                torch.full((cap,), 7.0, dtype=torch.float64, device=dev))
+        fr.regen_into(lo, idx.data_ptr(), min(cap, B), [o.data_ptr() for o in outs], n_dev=cnt)
+        for o, r in zip(outs, ref if ref else (None,) * 5):
+            if n:
+                assert torch.equal(o[:n], r)
+            assert bool((o[n:] == 7).all())
+
+
 def test_fused_vs_oracle_replay(dev):
     """Accept set against the numpy oracle's replay of the same streams
     (theta, x to 1e-12; masks equal away from |d - eps| < 1e-12)."""
