@@ -3,6 +3,7 @@
 # edited copy (a same-box A/B of a kernel change, no build-time switches in
 # the product sources):
 #   bash tools/build_src_variant.sh ab/libv.so ab/abc_mvn_x3.v1.hip abc_mvn_x3.hip
+# VARIANT_FLAGS in the environment: extra compiler flags for the edited file.
 # Further arguments: edited headers, copied next to the source (they shadow
 # the csrc headers of the same name).
 set -e
@@ -10,7 +11,7 @@ OUT=$1; VSRC=$2; SRC=$3; shift 3
 mkdir -p "$(dirname "$OUT")"
 python -m pyabc_amd.build > /dev/null
 OBJS=$(ls pyabc_amd/_build/*.o | grep -v "/$SRC.o")
-EXTRA=$(python3 -c "import pyabc_amd.build as b; print(' '.join(b.EXTRA.get('$SRC', [])))")
+EXTRA="$(python3 -c "import pyabc_amd.build as b; print(' '.join(b.EXTRA.get('$SRC', [])))") $VARIANT_FLAGS"
 T=$(mktemp -d)
 cp "$VSRC" $T/$SRC
 for h in "$@"; do cp "$h" $T/; done
