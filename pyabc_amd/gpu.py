@@ -73,17 +73,41 @@ class HostFuture:
     waits for that copy only (no device-wide sync), so the host can keep
     queueing work while the value is produced."""
 
-    def __init__(self, t):
+    # events are reused once waited on: a torch.cuda.Event creates its HIP
+    # event at its first record (~35 us of host time, several per generation)
+    _events = {}
+
+    def __init__(self, t, _record=True):
         self._h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
         self._h.copy_(t, non_blocking=True)
-        self._ev = torch.cuda.Event()
-        self._ev.record()
+        self._dev = t.device.index if t.is_cuda else torch.cuda.current_device()
+        self._pooled = _record
+        self._ev = None
+        if _record:
+            pool = HostFuture._events.setdefault(self._dev, [])
+            self._ev = pool.pop() if pool else torch.cuda.Event()
+            self._ev.record(torch.cuda.current_stream(self._dev))
         self._v = None
+
+    @classmethod
+    def group(cls, ts):
+        """Futures of several tensors behind one event record (each record
+        costs ~30 us of host time on this stack)."""
+        futs = [cls(t, _record=False) for t in ts]
+        if futs:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(futs[-1]._dev))
+            for f in futs:
+                f._ev = ev
+        return futs
 
     def get(self):
         if self._v is None:
             self._ev.synchronize()
             self._v = self._h.numpy().copy()
+            pool = HostFuture._events.setdefault(self._dev, [])
+            if self._pooled and len(pool) < 64:
+                pool.append(self._ev)
             self._h = self._ev = None
         return self._v
 

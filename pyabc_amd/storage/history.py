@@ -55,8 +55,7 @@ class _Gen:
             return self.to_host
         from .. import gpu
         c = pop.columns
-        futs = [gpu.HostFuture(a) for a in (c.theta, c.weights, c.distances,
-                                             c.sum_stats)]
+        futs = gpu.HostFuture.group((c.theta, c.weights, c.distances, c.sum_stats))
         names, keys = list(c.param_names), list(c.sum_stat_keys)
 
         def get():
