@@ -297,7 +297,14 @@ typedef struct abc_candidate_spec {
   uint32_t generation;
   const void* anc_table;       /* abc_ancestor_table of (X, cdf); required
                                   with X (the guide field is then unused) */
+  const double* support_box;   /* [d x (lo, hi)] from abc_prior_support_box
+                                  (nullable: each call computes it)        */
 } abc_candidate_spec;
+/* The prior's support box [d x (lo, hi)] the proposal's re-draw loop tests
+ * (smc.py:654-656: a proposal with prior density 0 is re-drawn), computed
+ * once per generation instead of once per round (device, 2 d doubles). */
+int abc_prior_support_box(const int32_t* prior_kind, const double* prior_params, int d,
+                          double* box, void* stream);
 /* Ancestor table of a population for the fused rounds: the rows X_j with
  * their weight-scan value in 128-byte-aligned records, and a guide over
  * 4 N scan bins (abc_candidate.h).  Same ancestors as the cdf / guide
@@ -319,7 +326,10 @@ int abc_ancestor_table(const double* X, const double* cdf, int64_t N, int d,
  * allows the exact early-rejection mode (first 4 statistics, p in {1,2,inf},
  * no rec_x; for the shared-L transition with every coordinate beyond the
  * 4th provably inside the support, only theta_0..3 of the first attempt):
- * the same accept set at lower cost when few candidates pass. */
+ * the same accept set at lower cost when few candidates pass.
+ * Workspace: abc_candidates_workspace(B) bytes whose first 256 bytes are
+ * zero before the first call (e.g. hipMemset at allocation); every call
+ * leaves them zero again (the round's tile ticket counter). */
 size_t abc_candidates_workspace(int64_t B);
 int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0,
                          int64_t B, double eps, const double* eps_dev,

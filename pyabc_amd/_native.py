@@ -56,6 +56,7 @@ SIGNATURES = {
     "abc_compact_workspace": (SZ, [I64]),
     "abc_accept_compact": (I32, [P, I64, D, P, P, P, SZ, P]),
     "abc_candidates_workspace": (SZ, [I64]),
+    "abc_prior_support_box": (I32, [P, P, I32, P, P]),
     "abc_candidates_round": (I32, [P, I64, I64, D, P, D, I32, I64, P, P, P, P, SZ, P]),
     "abc_candidates_regen": (I32, [P, I64, P, I64, P, P, P, P, P, P, P]),
     "abc_pnorm_accept": (I32, [P, I64, I32, P, P, D, D, P, I32, I64, P, P, P, SZ, P]),
@@ -106,7 +107,8 @@ class CandidateSpec(C.Structure):
                 ("prior_kind", P), ("prior_params", P), ("max_attempts", C.c_int),
                 ("src", P), ("a", P), ("sigma", P),
                 ("x0", P), ("wf", P), ("p", D),
-                ("seed", U64), ("generation", U32), ("anc_table", P)]
+                ("seed", U64), ("generation", U32), ("anc_table", P),
+                ("support_box", P)]
 
 
 # C error codes (include/abcgpu.h)

@@ -102,29 +102,24 @@ __device__ __forceinline__ double evaluate_staged(const RoundArgs& A, const Bloc
   return att <= A.P.max_attempts ? dist : NAN;
 }
 
+// One tile of the round: candidates tile0 + [0, cpt * FR_T) (cpt per thread,
+// FR_CPT or FR_CPT_TAIL), its accept words into bits.  The block's constants
+// C are staged; every thread calls it (barriers inside).
+struct TileLds {
+  uint32_t* tbits;   // [FR_TILE / 32]
+  uint16_t* queue;   // [FR_TILE] (early-reject mode)
+  int& qn;
+};
 template <int D, int MODE, bool FILTER, int PK>
-__device__ __forceinline__ void round_body(
-    RoundArgs A, int64_t idx0, int64_t B, double eps_host,
-    uint64_t* __restrict__ bits, int64_t* __restrict__ tile_cnt,
-    double* __restrict__ rec_x) {
-  // the threshold read on the device (the host's float(q) * multiplier, one
-  // IEEE product either way)
-  const double eps = A.eps_dev ? (*A.eps_dev) * A.eps_scale : eps_host;
-  constexpr bool filter = FILTER;
+__device__ __forceinline__ void tile_body(const RoundArgs& A, const BlockConsts& C, double eps,
+                                          int64_t idx0, int64_t B, int64_t tile0, int cpt,
+                                          uint64_t* __restrict__ bits,
+                                          double* __restrict__ rec_x, TileLds T) {
   constexpr int DM = D > 0 ? D : 64;
-  __shared__ BlockConsts C;
-  stage_block_consts<D, MODE, true>(C, A.P, &A.M, A.box);
-  __shared__ uint32_t tbits[FR_TILE / 32];
-  __shared__ uint16_t queue[FR_TILE];
-  __shared__ int qn;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int d = D > 0 ? D : A.P.d;
-  const int64_t tile0 = (int64_t)blockIdx.x * FR_TILE;
-  if (tid < FR_TILE / 32) tbits[tid] = 0u;
-  if (tid == 0) {
-    qn = 0;
-    if (FILTER) C.lazy = lazy_filter_ok<D, MODE>(C, A.P, A.M) ? 1 : 0;
-  }
+  const int tn = cpt * FR_T;                  // candidates of the tile
+  if (tid < tn / 32) T.tbits[tid] = 0u;
+  if (tid == 0) T.qn = 0;
   __syncthreads();
   double th[DM];
   int64_t j;
@@ -138,7 +133,7 @@ __device__ __forceinline__ void round_body(
         // candidates at a time (lazy_head_group); a head outside the
         // support (attempt 0 may be re-drawn) survives
 #pragma unroll 1
-        for (int it = 0; it < FR_CPT; it += FR_CG) {
+        for (int it = 0; it < cpt; it += FR_CG) {
           uint64_t gs[FR_CG];
           bool keep[FR_CG];
 #pragma unroll
@@ -148,8 +143,8 @@ __device__ __forceinline__ void round_body(
           for (int c = 0; c < FR_CG; ++c) {
             const int loc = (it + c) * FR_T + tid;
             if (keep[c] && tile0 + loc < B) {
-              const int pos = atomicAdd(&qn, 1);
-              queue[pos] = (uint16_t)loc;
+              const int pos = atomicAdd(&T.qn, 1);
+              T.queue[pos] = (uint16_t)loc;
             }
           }
         }
@@ -157,7 +152,7 @@ __device__ __forceinline__ void round_body(
       }
     }
 #pragma unroll 1
-    for (int it = 0; it < (lazy_done ? 0 : FR_CPT); ++it) {
+    for (int it = 0; it < (lazy_done ? 0 : cpt); ++it) {
       const int loc = it * FR_T + tid;
       const int64_t b = tile0 + loc;
       if (b < B) {
@@ -171,8 +166,8 @@ __device__ __forceinline__ void round_body(
           s = sim_pnorm_range<PK>(A.M, C, th, 1, g, A.P.gen, A.P.seed, 0, 4, 0.0, nullptr);
         }
         if (att <= A.P.max_attempts && !(pnorm_finish<PK>(s, A.M.p) > eps)) {
-          const int pos = atomicAdd(&qn, 1);
-          queue[pos] = (uint16_t)loc;
+          const int pos = atomicAdd(&T.qn, 1);
+          T.queue[pos] = (uint16_t)loc;
         }
       }
     }
@@ -180,50 +175,254 @@ __device__ __forceinline__ void round_body(
   }
   // full evaluation: every candidate of the tile, or the phase-A survivors
   // (dense over the block's waves)
-  const int n = filter ? qn : FR_TILE;
+  const int n = FILTER ? T.qn : tn;
 #pragma unroll 1
   for (int i = tid; i < n; i += FR_T) {
-    const int loc = filter ? (int)queue[i] : i;
+    const int loc = FILTER ? (int)T.queue[i] : i;
     const int64_t b = tile0 + loc;
     if (b < B) {
       double* xr = rec_x ? rec_x + b * A.M.S : nullptr;
       const double dist = evaluate_full<D, MODE, PK>(A, C, (uint64_t)(idx0 + b), th, j, att,
                                                   xr);
-      if (dist <= eps) atomicOr(&tbits[loc >> 5], 1u << (loc & 31));
+      if (dist <= eps) atomicOr(&T.tbits[loc >> 5], 1u << (loc & 31));
     }
   }
   __syncthreads();
-  // accept words of the tile + its count (wave 0)
-  if (wave == 0) {
-    int c = 0;
-    if (lane < FR_WORDS) {
-      const uint64_t w = (uint64_t)tbits[2 * lane] | ((uint64_t)tbits[2 * lane + 1] << 32);
-      const int64_t word = tile0 / 64 + lane;
-      if (word * 64 < B) bits[word] = w;
-      c = __popcll(w);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if (lane == 0) tile_cnt[blockIdx.x] = c;
+  // accept words of the tile (wave 0)
+  if (wave == 0 && lane < tn / 64) {
+    const uint64_t w = (uint64_t)T.tbits[2 * lane] | ((uint64_t)T.tbits[2 * lane + 1] << 32);
+    const int64_t word = tile0 / 64 + lane;
+    if (word * 64 < B) bits[word] = w;
   }
 }
 
-// the plain and the early-reject round as separate kernels (a runtime
-// switch would give both the register allocation of the larger one), each
-// for p == 2 and for any p (pnorm_acc)
-#define ABC_ROUND_KERNEL(NAME, FILTER, PK, REC)                                       \
-  template <int D, int MODE>                                                          \
-  __global__ __launch_bounds__(FR_T) void NAME(RoundArgs A, int64_t idx0, int64_t B,  \
-                                               double eps, uint64_t* bits,            \
-                                               int64_t* tile_cnt, double* rec_x) {    \
-    round_body<D, MODE, FILTER, PK>(A, idx0, B, eps, bits, tile_cnt,                  \
-                                    REC ? rec_x : nullptr);                           \
+// ---- the round: tiles handed out by a ticket counter -------------------------
+// Blocks are placed on the 8 XCDs round-robin by block index, so a grid of
+// one tile per block gives every XCD the same number of tiles however fast
+// it runs: a block-level trace of round 5's kernel
+// (profiles/r06_fused_block_trace.log) shows the XCDs' median tile times
+// 99-104 us at c3's shape and their last tiles ending up to 450 us apart
+// (5% of a full round), and at 3.4e7 candidates (a rank's share of c3 on
+// 8 GPUs) the last block-wave another 6.5%.  Here a resident grid of blocks
+// takes tiles from a counter until none are left, so faster XCDs take more;
+// the last tiles are FR_CPT_TAIL candidates per thread (a quarter tile), so
+// the blocks run out of work within a short tile of each other.  The
+// tickets are exact -- ntiles + grid grabs per launch, one failing grab per
+// block -- so the counter wraps back to zero at the last grab (atomicInc):
+// no reset between launches.  Tile t covers the same candidates whichever
+// block takes it; the accept bits do not depend on the schedule.
+constexpr int FR_CPT_TAIL = 2;
+constexpr int FR_TILE_TAIL = FR_T * FR_CPT_TAIL;
+
+struct TilePlan {
+  int64_t nbig, ntiles;        // full tiles first, then tail tiles
+  unsigned int grid;
+};
+__host__ __device__ inline void tile_span(int64_t t, int64_t nbig, int64_t& tile0, int& cpt) {
+  if (t < nbig) { tile0 = t * FR_TILE; cpt = FR_CPT; }
+  else { tile0 = nbig * FR_TILE + (t - nbig) * FR_TILE_TAIL; cpt = FR_CPT_TAIL; }
+}
+
+template <int D, int MODE, bool FILTER, int PK>
+__device__ __forceinline__ void round_body(RoundArgs A, int64_t idx0, int64_t B,
+                                           double eps_host, uint64_t* __restrict__ bits,
+                                           unsigned int* __restrict__ ticket,
+                                           int64_t nbig, int64_t ntiles,
+                                           double* __restrict__ rec_x) {
+  // the threshold read on the device (the host's float(q) * multiplier, one
+  // IEEE product either way)
+  const double eps = A.eps_dev ? (*A.eps_dev) * A.eps_scale : eps_host;
+  __shared__ BlockConsts C;
+  __shared__ uint32_t tbits[FR_TILE / 32];
+  __shared__ uint16_t queue[FR_TILE];
+  __shared__ int qn;
+  __shared__ int64_t s_tile;
+  const TileLds T{tbits, queue, qn};
+  stage_block_consts<D, MODE, true>(C, A.P, &A.M, A.box);
+  if (FILTER) {
+    if (threadIdx.x == 0) C.lazy = lazy_filter_ok<D, MODE>(C, A.P, A.M) ? 1 : 0;
   }
-ABC_ROUND_KERNEL(fused_round_plain, false, 0, true)
-ABC_ROUND_KERNEL(fused_round_plain_p2, false, 2, true)
-ABC_ROUND_KERNEL(fused_round_filter, true, 0, false)
-ABC_ROUND_KERNEL(fused_round_filter_p2, true, 2, false)
+  const unsigned int limit = (unsigned int)(ntiles + gridDim.x - 1);
+#pragma unroll 1
+  for (;;) {
+    if (threadIdx.x == 0) s_tile = (int64_t)atomicInc(ticket, limit);
+    __syncthreads();
+    const int64_t t = s_tile;
+    if (t >= ntiles) break;            // block-uniform: one failing grab per block
+    int64_t tile0;
+    int cpt;
+    tile_span(t, nbig, tile0, cpt);
+    tile_body<D, MODE, FILTER, PK>(A, C, eps, idx0, B, tile0, cpt, bits, rec_x, T);
+    __syncthreads();                   // s_tile and the tile's LDS are reused
+  }
+}
+
+// The plain round's tile loop flattened into its candidate loop (one loop:
+// a tile boundary is a block-uniform branch in it).  With the tile loop
+// nested around the candidate loop the compiler keeps ~20 more VGPRs live
+// (101 vs 80 at d = 10: 4 instead of 6 waves per SIMD).
+template <int D, int MODE, int PK>
+__device__ __forceinline__ void round_plain_body(RoundArgs A, int64_t idx0, int64_t B,
+                                                 double eps_host, uint64_t* __restrict__ bits,
+                                                 unsigned int* __restrict__ ticket,
+                                                 int64_t nbig, int64_t ntiles,
+                                                 double* __restrict__ rec_x) {
+  const double eps = A.eps_dev ? (*A.eps_dev) * A.eps_scale : eps_host;
+  constexpr int DM = D > 0 ? D : 64;
+  __shared__ BlockConsts C;
+  __shared__ uint32_t tbits[FR_TILE / 32];
+  __shared__ int64_t s_tile;
+  stage_block_consts<D, MODE, true>(C, A.P, &A.M, A.box);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned int limit = (unsigned int)(ntiles + gridDim.x - 1);
+  int64_t tile0 = 0;
+  int cpt = 0, it = 0;
+  bool started = false;
+#pragma unroll 1
+  for (;;) {
+    if (it == cpt) {                      // block-uniform: the tile is done
+      __syncthreads();
+      if (started && wave == 0 && lane < cpt * (FR_T / 64)) {
+        const uint64_t w = (uint64_t)tbits[2 * lane] | ((uint64_t)tbits[2 * lane + 1] << 32);
+        const int64_t word = tile0 / 64 + lane;
+        if (word * 64 < B) bits[word] = w;
+      }
+      if (tid == 0) s_tile = (int64_t)atomicInc(ticket, limit);
+      __syncthreads();                    // tbits read, s_tile written
+      // the ticket into scalar registers (an LDS read is a per-lane value)
+      const int64_t t = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
+                                       (int)(s_tile >> 32)) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile));
+      if (t >= ntiles) break;             // one failing grab per block
+      tile_span(t, nbig, tile0, cpt);
+      if (tid < FR_TILE / 32) tbits[tid] = 0u;
+      __syncthreads();
+      it = 0;
+      started = true;
+    }
+    const int loc = it * FR_T + tid;
+    const int64_t b = tile0 + loc;
+    if (b < B) {
+      double th[DM];
+      int64_t j;
+      int att;
+      double* xr = rec_x ? rec_x + b * A.M.S : nullptr;
+      const double dist = evaluate_full<D, MODE, PK>(A, C, (uint64_t)(idx0 + b), th, j, att, xr);
+      if (dist <= eps) atomicOr(&tbits[loc >> 5], 1u << (loc & 31));
+    }
+    ++it;
+  }
+}
+
+// Minimum waves per SIMD the compiler must allow (__launch_bounds__' second
+// argument): the plain p = 2 round at d = 10 with a population (c2 / c3 / c5
+// shapes) takes 100 VGPRs unconstrained (4 waves) but fits 80 (6 waves, as in
+// round 5's one-tile-per-block kernel) without spilling; every other
+// instantiation is left to the compiler (a bound there spills).
+__host__ __device__ constexpr int fr_min_waves(bool filter, int D, int MODE, int PK) {
+  return (!filter && PK == 2 && D == 10 && MODE != PROP_PRIOR) ? 6 : 1;
+}
+
+#define ABC_ROUND_KERNEL(NAME, FILTER, PK)                                                \
+  template <int D, int MODE>                                                              \
+  __global__ __launch_bounds__(FR_T, fr_min_waves(FILTER, D, MODE, PK))                   \
+  void NAME(RoundArgs A, int64_t idx0, int64_t B,                                         \
+                                               double eps, uint64_t* bits,                \
+                                               unsigned int* ticket, int64_t nbig,        \
+                                               int64_t ntiles, double* rec_x) {           \
+    if (FILTER)                                                                           \
+      round_body<D, MODE, true, PK>(A, idx0, B, eps, bits, ticket, nbig, ntiles, nullptr);\
+    else                                                                                  \
+      round_plain_body<D, MODE, PK>(A, idx0, B, eps, bits, ticket, nbig, ntiles, rec_x);  \
+  }
+ABC_ROUND_KERNEL(fused_round_plain, false, 0)
+ABC_ROUND_KERNEL(fused_round_plain_p2, false, 2)
+ABC_ROUND_KERNEL(fused_round_filter, true, 0)
+ABC_ROUND_KERNEL(fused_round_filter_p2, true, 2)
 #undef ABC_ROUND_KERNEL
+
+// ---- accept words -> ordered positions -------------------------------------
+// The accept words are cut into ranges of whole words (<= RG_MAX ranges);
+// each range's accepted count goes to rtot[range], and bits_write_ranges
+// (one wave per range) sums the counts of the ranges before its own --
+// at most RG_MAX reads per wave, from L2 -- and writes the positions of its
+// set bits; the wave of the last range writes the round's total.  One short
+// launch after the producer when the producer is the plain round (it counts
+// its own ranges), two otherwise; round 5 ran a three-kernel scan of
+// per-tile counts and a per-word writer after it.
+constexpr int RG_MAX = 2048;    // ranges at most
+constexpr int RG_T = 256;
+
+// range totals of accept words written by another kernel (the early-reject
+// round, the user-model tail): one block per range of wpr words
+__global__ __launch_bounds__(RG_T) void bits_range_sum_kernel(
+    const uint64_t* __restrict__ bits, int64_t nwords, int64_t wpr,
+    int64_t* __restrict__ rtot) {
+  __shared__ int ws[RG_T / 64];
+  const int64_t w0 = (int64_t)blockIdx.x * wpr;
+  const int64_t w1 = w0 + wpr < nwords ? w0 + wpr : nwords;
+  int c = 0;
+  for (int64_t w = w0 + threadIdx.x; w < w1; w += RG_T) c += __popcll(bits[w]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t tot = 0;
+    for (int q = 0; q < RG_T / 64; ++q) tot += ws[q];
+    rtot[blockIdx.x] = tot;
+  }
+}
+
+// One wave per range: its offset (the totals of the ranges before it), then
+// the range's words loaded up front (WB per lane in flight) and taken 64 at
+// a time -- popcount prefix across the lanes, the set bits' positions
+// written while below cap.
+constexpr int WB = 32;
+__global__ __launch_bounds__(256) void bits_write_ranges(
+    const uint64_t* __restrict__ bits, int64_t nwords, int64_t wpr, int nranges,
+    const int64_t* __restrict__ rtot, int64_t cap, int64_t* __restrict__ idx,
+    int64_t* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nranges) return;
+  int64_t off = 0;
+  for (int q = lane; q < r; q += 64) off += rtot[q];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) off += __shfl_xor(off, o, 64);
+  const int64_t mine = rtot[r];
+  if (r == nranges - 1 && lane == 0) *count = off + mine;
+  if (off >= cap || mine == 0) return;    // wave-uniform
+  const int64_t w0 = (int64_t)r * wpr;
+  const int64_t w1 = w0 + wpr < nwords ? w0 + wpr : nwords;
+  for (int64_t b0 = w0; b0 < w1 && off < cap; b0 += 64 * WB) {
+    uint64_t w[WB];
+#pragma unroll
+    for (int q = 0; q < WB; ++q) {
+      const int64_t wd = b0 + 64 * q + lane;
+      w[q] = wd < w1 ? bits[wd] : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < WB; ++q) {
+      if (b0 + 64 * q >= w1 || off >= cap) break;   // wave-uniform
+      const int c = __popcll(w[q]);
+      int incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += u;
+      }
+      int64_t pos = off + (incl - c);
+      uint64_t m = w[q];
+      const int64_t wd = b0 + 64 * q + lane;
+      while (m != 0ull && pos < cap) {
+        idx[pos++] = wd * 64 + (__ffsll((long long)m) - 1);
+        m &= m - 1;
+      }
+      off += __shfl(incl, 63, 64);
+    }
+  }
+}
 
 // one wave per dimension (support_bounds_wave): ~1 us instead of the ~40 us
 // of one thread's 126 dependent bisection steps
@@ -234,98 +433,60 @@ __global__ __launch_bounds__(64) void support_box_kernel(const int32_t* __restri
   if (k < d) support_bounds_wave(kind[k], params + 4 * k, box + 2 * k);
 }
 
-// ---- order-preserving compaction of the accept bits -----------------------
-// exclusive scan of the tile counts in place, total -> *count: per block of
-// SC_N tiles a local scan (scan_partial: block sums), one block scans the
-// block sums (scan_top), then each block adds its offset (scan_apply)
-constexpr int SC_T = 256, SC_PER = 4, SC_N = SC_T * SC_PER;
-
-__device__ __forceinline__ int64_t block_exscan(int64_t v, int64_t* sh, int64_t& total) {
-  const int t = threadIdx.x;
-  sh[t] = v;
-  __syncthreads();
-  for (int o = 1; o < SC_T; o <<= 1) {
-    const int64_t add = (t >= o) ? sh[t - o] : 0;
-    __syncthreads();
-    sh[t] += add;
-    __syncthreads();
-  }
-  total = sh[SC_T - 1];
-  const int64_t ex = sh[t] - v;
-  __syncthreads();
-  return ex;
+// resident blocks of a kernel on the current device (cached per kernel)
+template <class K>
+int resident_blocks(K kernel, int block) {
+  struct Entry { const void* k; int dev; int n; };
+  static Entry cache[64];
+  static int ncache = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return RG_MAX;
+  for (int i = 0; i < ncache; ++i)
+    if (cache[i].k == (const void*)kernel && cache[i].dev == dev) return cache[i].n;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      per_cu < 1 || cus < 1)
+    return 1024;
+  const int n = per_cu * cus;
+  if (ncache < 64) cache[ncache++] = Entry{(const void*)kernel, dev, n};
+  return n;
 }
 
-__global__ __launch_bounds__(SC_T) void scan_partial(const int64_t* __restrict__ cnt,
-                                                     int64_t n, int64_t* __restrict__ bsum) {
-  __shared__ int64_t sh[SC_T];
-  const int64_t b0 = (int64_t)blockIdx.x * SC_N + threadIdx.x * SC_PER;
-  int64_t v = 0;
-#pragma unroll
-  for (int k = 0; k < SC_PER; ++k)
-    if (b0 + k < n) v += cnt[b0 + k];
-  int64_t tot;
-  block_exscan(v, sh, tot);
-  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+struct Ranges { int64_t nwords, wpr; int n; };
+// nwords accept words in at most `most` ranges of at least `least` words
+inline Ranges make_ranges(int64_t B, int64_t most, int64_t least) {
+  Ranges r;
+  r.nwords = ceil_div(B, 64);
+  if (most > RG_MAX) most = RG_MAX;
+  int64_t n = ceil_div(r.nwords, least);
+  n = n < most ? n : most;
+  n = n < 1 ? 1 : n;
+  r.wpr = ceil_div(r.nwords, n);
+  r.n = (int)ceil_div(r.nwords, r.wpr);
+  return r;
 }
 
-__global__ __launch_bounds__(SC_T) void scan_top(int64_t* __restrict__ bsum, int64_t nb,
-                                                 int64_t* __restrict__ count) {
-  __shared__ int64_t sh[SC_T];
-  const int64_t per = (nb + SC_T - 1) / SC_T;
-  const int64_t b0 = threadIdx.x * per;
-  int64_t v = 0;
-  for (int64_t k = 0; k < per; ++k)
-    if (b0 + k < nb) v += bsum[b0 + k];
-  int64_t tot;
-  int64_t off = block_exscan(v, sh, tot);
-  for (int64_t k = 0; k < per; ++k)
-    if (b0 + k < nb) { const int64_t x = bsum[b0 + k]; bsum[b0 + k] = off; off += x; }
-  if (threadIdx.x == 0) *count = tot;
+// the round's tile schedule: full tiles, then tail tiles for about two
+// resident block-waves; the grid is the resident capacity (at most one
+// block per tile)
+inline TilePlan plan_tiles(int64_t B, int resident) {
+  TilePlan p;
+  const int64_t tail = 2 * (int64_t)resident * FR_TILE_TAIL;
+  p.nbig = B > tail ? (B - tail) / FR_TILE : 0;
+  p.ntiles = p.nbig + ceil_div(B - p.nbig * FR_TILE, FR_TILE_TAIL);
+  p.grid = (unsigned int)(p.ntiles < resident ? p.ntiles : resident);
+  return p;
 }
 
-__global__ __launch_bounds__(SC_T) void scan_apply(int64_t* __restrict__ cnt, int64_t n,
-                                                   const int64_t* __restrict__ boff) {
-  __shared__ int64_t sh[SC_T];
-  const int64_t b0 = (int64_t)blockIdx.x * SC_N + threadIdx.x * SC_PER;
-  int64_t c[SC_PER];
-  int64_t v = 0;
-#pragma unroll
-  for (int k = 0; k < SC_PER; ++k) {
-    c[k] = b0 + k < n ? cnt[b0 + k] : 0;
-    v += c[k];
-  }
-  int64_t tot;
-  int64_t off = block_exscan(v, sh, tot) + boff[blockIdx.x];
-#pragma unroll
-  for (int k = 0; k < SC_PER; ++k)
-    if (b0 + k < n) { cnt[b0 + k] = off; off += c[k]; }
-}
-
-// one lane per 64-bit word: positions of the set bits, in increasing order,
-// for output slots < cap
-__global__ __launch_bounds__(256) void bits_write_kernel(
-    const uint64_t* __restrict__ bits, int64_t nwords,
-    const int64_t* __restrict__ tile_off, int64_t cap, int64_t* __restrict__ idx) {
-  const int64_t wd = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  uint64_t w = wd < nwords ? bits[wd] : 0ull;
-  // exclusive popcount prefix among the FR_WORDS words of this tile
-  // (tiles are FR_WORDS = 32 aligned words: half a wave)
-  int c = __popcll(w);
-  int incl = c;
-#pragma unroll
-  for (int o = 1; o < FR_WORDS; o <<= 1) {
-    const int v = __shfl_up(incl, o, 64);
-    if ((lane & (FR_WORDS - 1)) >= o) incl += v;
-  }
-  if (wd >= nwords || w == 0ull) return;
-  int64_t pos = tile_off[wd / FR_WORDS] + (incl - c);
-  while (w != 0ull && pos < cap) {
-    const int bit = __ffsll((long long)w) - 1;
-    idx[pos++] = wd * 64 + bit;
-    w &= w - 1;
-  }
+template <int D, int MODE>
+void launch_round(bool filt, bool p2, const RoundArgs& A, int64_t idx0, int64_t B, double eps,
+                  uint64_t* bits, unsigned int* ticket, double* rec_x, hipStream_t s) {
+  auto k = filt ? (p2 ? fused_round_filter_p2<D, MODE> : fused_round_filter<D, MODE>)
+                : (p2 ? fused_round_plain_p2<D, MODE> : fused_round_plain<D, MODE>);
+  const TilePlan p = plan_tiles(B, resident_blocks(k, FR_T));
+  hipLaunchKernelGGL(k, dim3(p.grid), dim3(FR_T), 0, s, A, idx0, B, eps, bits, ticket, p.nbig,
+                     p.ntiles, rec_x);
 }
 
 // ---- regeneration of kept rows ----------------------------------------------
@@ -418,7 +579,7 @@ template <bool WIDE>
 __global__ __launch_bounds__(FR_T) void pnorm_accept_kernel(
     const double* __restrict__ x, int64_t B, int S, const double* __restrict__ x0,
     const double* __restrict__ wf, double p, double eps, const int32_t* __restrict__ att,
-    int max_attempts, uint64_t* __restrict__ bits, int64_t* __restrict__ tile_cnt) {
+    int max_attempts, uint64_t* __restrict__ bits) {
   __shared__ uint32_t tbits[FR_TILE / 32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t tile0 = (int64_t)blockIdx.x * FR_TILE;
@@ -522,38 +683,31 @@ __global__ __launch_bounds__(FR_T) void pnorm_accept_kernel(
     }
   }
   __syncthreads();
-  if (wave == 0) {
-    int c = 0;
-    if (lane < FR_WORDS) {
-      const uint64_t w = (uint64_t)tbits[2 * lane] | ((uint64_t)tbits[2 * lane + 1] << 32);
-      const int64_t word = tile0 / 64 + lane;
-      if (word * 64 < B) bits[word] = w;
-      c = __popcll(w);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-    if (lane == 0) tile_cnt[blockIdx.x] = c;
+  if (wave == 0 && lane < FR_WORDS) {
+    const uint64_t w = (uint64_t)tbits[2 * lane] | ((uint64_t)tbits[2 * lane + 1] << 32);
+    const int64_t word = tile0 / 64 + lane;
+    if (word * 64 < B) bits[word] = w;
   }
 }
 
-// accept bits + tile counts -> exclusive tile offsets, *count, and the first
-// cap positions (the fused round's compaction)
-int compact_accept_bits(const uint64_t* bits, int64_t* tcnt, int64_t nt, int64_t* bsum,
-                        int64_t B, int64_t cap, int64_t* idx, int64_t* count, hipStream_t s) {
-  const int64_t nb = ceil_div(nt, SC_N);
-  hipLaunchKernelGGL(scan_partial, dim3((unsigned)nb), dim3(SC_T), 0, s, tcnt, nt, bsum);
+// *count and the positions of the first cap accepted from the range totals
+int write_ranges(const uint64_t* bits, const Ranges& rg, const int64_t* rtot, int64_t cap,
+                 int64_t* idx, int64_t* count, hipStream_t s) {
+  hipLaunchKernelGGL(bits_write_ranges, dim3((unsigned)ceil_div(rg.n, 4)), dim3(256), 0, s,
+                     bits, rg.nwords, rg.wpr, rg.n, rtot, cap, idx, count);
   ABC_LAUNCHED();
-  hipLaunchKernelGGL(scan_top, dim3(1), dim3(SC_T), 0, s, bsum, nb, count);
-  ABC_LAUNCHED();
-  hipLaunchKernelGGL(scan_apply, dim3((unsigned)nb), dim3(SC_T), 0, s, tcnt, nt, bsum);
-  ABC_LAUNCHED();
-  if (cap > 0) {
-    const int64_t nwords = ceil_div(B, 64);
-    hipLaunchKernelGGL(bits_write_kernel, dim3((unsigned)ceil_div(nwords, 256)), dim3(256), 0,
-                       s, bits, nwords, tcnt, cap, idx);
-    ABC_LAUNCHED();
-  }
   return ABC_OK;
+}
+
+// accept words written by another kernel -> *count and the first cap
+// positions (range sums, then the writer)
+int compact_accept_bits(const uint64_t* bits, int64_t* rtot, int64_t B, int64_t cap,
+                        int64_t* idx, int64_t* count, hipStream_t s) {
+  const Ranges rg = make_ranges(B, RG_MAX, RG_T);
+  hipLaunchKernelGGL(bits_range_sum_kernel, dim3((unsigned)rg.n), dim3(RG_T), 0, s, bits,
+                     rg.nwords, rg.wpr, rtot);
+  ABC_LAUNCHED();
+  return write_ranges(bits, rg, rtot, cap, idx, count, s);
 }
 
 // ---- ancestor table (abc_candidate.h) ---------------------------------------
@@ -692,18 +846,61 @@ int check_spec(const abc_candidate_spec* s) {
 #define ABC_FUSED_CASE(KERNEL, DD, GRID, STREAM, ...)                          \
   case DD: { ABC_FUSED_CASE_BODY(KERNEL, DD, GRID, STREAM, __VA_ARGS__) }
 
+// the same dispatch for a host launcher template FN<D, MODE>(args...)
+#define ABC_FUSED_CALL(FN, ...)                                                \
+  do {                                                                         \
+    const int mode_ = spec->X == nullptr ? PROP_PRIOR                          \
+                      : (spec->per_particle_L ? PROP_LOCAL : PROP_MVN);        \
+    switch (spec->d) {                                                         \
+      ABC_FUSED_CALL_CASE(FN, 1, __VA_ARGS__)                                  \
+      ABC_FUSED_CALL_CASE(FN, 2, __VA_ARGS__)                                  \
+      ABC_FUSED_CALL_CASE(FN, 3, __VA_ARGS__)                                  \
+      ABC_FUSED_CALL_CASE(FN, 4, __VA_ARGS__)                                  \
+      ABC_FUSED_CALL_CASE(FN, 5, __VA_ARGS__)                                  \
+      ABC_FUSED_CALL_CASE(FN, 6, __VA_ARGS__)                                  \
+      ABC_FUSED_CALL_CASE(FN, 8, __VA_ARGS__)                                  \
+      ABC_FUSED_CALL_CASE(FN, 10, __VA_ARGS__)                                 \
+      ABC_FUSED_CALL_CASE(FN, 12, __VA_ARGS__)                                 \
+      ABC_FUSED_CALL_CASE(FN, 16, __VA_ARGS__)                                 \
+      default:                                                                 \
+        ABC_FUSED_CALL_BODY(FN, 0, __VA_ARGS__)                                \
+    }                                                                          \
+  } while (0)
+#define ABC_FUSED_CALL_BODY(FN, DD, ...)                                       \
+  if (mode_ == PROP_MVN) FN<DD, PROP_MVN>(__VA_ARGS__);                        \
+  else if (mode_ == PROP_LOCAL) FN<DD, PROP_LOCAL>(__VA_ARGS__);               \
+  else FN<DD, PROP_PRIOR>(__VA_ARGS__);                                        \
+  break;
+#define ABC_FUSED_CALL_CASE(FN, DD, ...)                                       \
+  case DD: { ABC_FUSED_CALL_BODY(FN, DD, __VA_ARGS__) }
+
 }  // namespace
 }  // namespace abc
 
 using namespace abc;
 
+// workspace: tile ticket (zero before the first call; every round leaves it
+// zero) | range totals | prior support box | accept bits
+struct RoundWs {
+  unsigned int* ticket; int64_t* rtot; double* box; uint64_t* bits; bool ok;
+};
+inline RoundWs carve_round_ws(void* ws, size_t ws_bytes, int64_t B) {
+  Carver c(ws, ws_bytes);
+  RoundWs w;
+  w.ticket = c.take<unsigned int>(64);
+  w.rtot = c.take<int64_t>(RG_MAX);
+  w.box = c.take<double>(128);
+  w.bits = c.take<uint64_t>((size_t)ceil_div(B > 0 ? B : 1, FR_TILE) * FR_WORDS);
+  w.ok = c.ok;
+  return w;
+}
+
 extern "C" size_t abc_candidates_workspace(int64_t B) {
-  const int64_t nt = ceil_div(B > 0 ? B : 1, FR_TILE);
   size_t off = 0;
-  size_only<uint64_t>(off, (size_t)nt * FR_WORDS);  // accept bits
-  size_only<int64_t>(off, (size_t)nt);              // tile counts / offsets
-  size_only<double>(off, 128);                      // prior support box
-  size_only<int64_t>(off, (size_t)ceil_div(nt, SC_N));  // scan block sums
+  size_only<unsigned int>(off, 64);
+  size_only<int64_t>(off, RG_MAX);
+  size_only<double>(off, 128);
+  size_only<uint64_t>(off, (size_t)ceil_div(B > 0 ? B : 1, FR_TILE) * FR_WORDS);
   return off + 256;
 }
 
@@ -761,36 +958,24 @@ extern "C" int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0
   const int filt = (filter && rec_x == nullptr && spec->S > 4 &&
                     (p == 1.0 || p == 2.0 || p == INFINITY)) ? 1 : 0;
   const int64_t nt = ceil_div(B, FR_TILE);
-  Carver c(ws, ws_bytes);
-  uint64_t* bits = c.take<uint64_t>((size_t)nt * FR_WORDS);
-  int64_t* tcnt = c.take<int64_t>((size_t)nt);
-  double* box = c.take<double>(128);
-  int64_t* bsum = c.take<int64_t>((size_t)ceil_div(nt, SC_N));
-  if (!c.ok) return set_error(ABC_ERR_WORKSPACE, "candidates_round: workspace");
-  hipLaunchKernelGGL(support_box_kernel, dim3((unsigned)spec->d), dim3(64), 0, s,
-                     spec->prior_kind, spec->prior_params, spec->d, box);
-  ABC_LAUNCHED();
+  ABC_CHECK_ARG(nt < (1ll << 31), "candidates_round: too many tiles");
+  const RoundWs w = carve_round_ws(ws, ws_bytes, B);
+  if (!w.ok) return set_error(ABC_ERR_WORKSPACE, "candidates_round: workspace");
+  const double* box = spec->support_box;
+  if (!box) {
+    hipLaunchKernelGGL(support_box_kernel, dim3((unsigned)spec->d), dim3(64), 0, s,
+                       spec->prior_kind, spec->prior_params, spec->d, w.box);
+    ABC_LAUNCHED();
+    box = w.box;
+  }
   RoundArgs A = round_args(spec, box);
   A.eps_dev = eps_dev;
   A.eps_scale = eps_scale;
-  ABC_CHECK_ARG(nt < (1ll << 31), "candidates_round: too many tiles");
   profile_start(s, ABC_PROF_CANDIDATES);
-  const bool p2 = p == 2.0;
-  if (filt && p2)
-    ABC_FUSED_DISPATCH(fused_round_filter_p2, dim3((unsigned)nt), s, A, idx0, B, eps, bits,
-                       tcnt, rec_x);
-  else if (filt)
-    ABC_FUSED_DISPATCH(fused_round_filter, dim3((unsigned)nt), s, A, idx0, B, eps, bits, tcnt,
-                       rec_x);
-  else if (p2)
-    ABC_FUSED_DISPATCH(fused_round_plain_p2, dim3((unsigned)nt), s, A, idx0, B, eps, bits,
-                       tcnt, rec_x);
-  else
-    ABC_FUSED_DISPATCH(fused_round_plain, dim3((unsigned)nt), s, A, idx0, B, eps, bits, tcnt,
-                       rec_x);
+  ABC_FUSED_CALL(launch_round, filt != 0, p == 2.0, A, idx0, B, eps, w.bits, w.ticket, rec_x, s);
   profile_stop(s, ABC_PROF_CANDIDATES);
   ABC_LAUNCHED();
-  return compact_accept_bits(bits, tcnt, nt, bsum, B, cap, idx, count, s);
+  return compact_accept_bits(w.bits, w.rtot, B, cap, idx, count, s);
 }
 
 extern "C" int abc_pnorm_accept(const double* x, int64_t B, int S, const double* x0,
@@ -811,22 +996,29 @@ extern "C" int abc_pnorm_accept(const double* x, int64_t B, int S, const double*
   ABC_CHECK_ARG(x && x0 && wf, "pnorm_accept: null pointer");
   const int64_t nt = ceil_div(B, FR_TILE);
   ABC_CHECK_ARG(nt < (1ll << 31), "pnorm_accept: too many tiles");
-  Carver c(ws, ws_bytes);
-  uint64_t* bits = c.take<uint64_t>((size_t)nt * FR_WORDS);
-  int64_t* tcnt = c.take<int64_t>((size_t)nt);
-  c.take<double>(128);
-  int64_t* bsum = c.take<int64_t>((size_t)ceil_div(nt, SC_N));
-  if (!c.ok) return set_error(ABC_ERR_WORKSPACE, "pnorm_accept: workspace");
+  const RoundWs w = carve_round_ws(ws, ws_bytes, B);
+  if (!w.ok) return set_error(ABC_ERR_WORKSPACE, "pnorm_accept: workspace");
+  uint64_t* bits = w.bits;
   // the same row / wave split as abc_pnorm (the same bits per row)
   if (S <= 32)
     hipLaunchKernelGGL(pnorm_accept_kernel<false>, dim3((unsigned)nt), dim3(FR_T),
                        (size_t)pa_chunk_rows(S) * (S + 1) * sizeof(double), s, x, B, S, x0, wf, p, eps,
-                       attempts, max_attempts, bits, tcnt);
+                       attempts, max_attempts, bits);
   else
     hipLaunchKernelGGL(pnorm_accept_kernel<true>, dim3((unsigned)nt), dim3(FR_T), 0, s, x, B,
-                       S, x0, wf, p, eps, attempts, max_attempts, bits, tcnt);
+                       S, x0, wf, p, eps, attempts, max_attempts, bits);
   ABC_LAUNCHED();
-  return compact_accept_bits(bits, tcnt, nt, bsum, B, cap, idx, count, s);
+  return compact_accept_bits(bits, w.rtot, B, cap, idx, count, s);
+}
+
+extern "C" int abc_prior_support_box(const int32_t* prior_kind, const double* prior_params,
+                                     int d, double* box, void* stream) {
+  ABC_CHECK_ARG(d >= 1 && d <= 64, "prior_support_box: bad d");
+  ABC_CHECK_ARG(prior_kind && prior_params && box, "prior_support_box: null pointer");
+  hipLaunchKernelGGL(support_box_kernel, dim3((unsigned)d), dim3(64), 0, as_stream(stream),
+                     prior_kind, prior_params, d, box);
+  ABC_LAUNCHED();
+  return ABC_OK;
 }
 
 extern "C" size_t abc_candidates_propose_workspace() { return 128 * sizeof(double) + 256; }
@@ -845,9 +1037,13 @@ extern "C" int abc_candidates_propose(const abc_candidate_spec* spec, int64_t id
   hipStream_t s = as_stream(stream);
   Carver c(ws, ws_bytes);
   double* box = c.take<double>(128);
-  hipLaunchKernelGGL(support_box_kernel, dim3((unsigned)spec->d), dim3(64), 0, s,
-                     spec->prior_kind, spec->prior_params, spec->d, box);
-  ABC_LAUNCHED();
+  if (spec->support_box) {
+    box = const_cast<double*>(spec->support_box);
+  } else {
+    hipLaunchKernelGGL(support_box_kernel, dim3((unsigned)spec->d), dim3(64), 0, s,
+                       spec->prior_kind, spec->prior_params, spec->d, box);
+    ABC_LAUNCHED();
+  }
   const RoundArgs A = round_args(spec, box);
   const int64_t nb = ceil_div(B, (int64_t)FR_T * FP_CPT);
   ABC_CHECK_ARG(nb < (1ll << 31), "candidates_propose: too many blocks");

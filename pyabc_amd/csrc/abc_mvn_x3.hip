@@ -725,20 +725,22 @@ void launch_pack(int r, dim3 grid, hipStream_t s, const double* P, const double*
 
 // rows of the rescued candidates (x [M x d] -> xs [n x d]) and their
 // densities back (outs [n] -> out at the rescued positions)
+// (the first min(*nres, cap) list entries: the nested pass's capacity)
 __global__ void x3_gather_rescued(const int64_t* __restrict__ rescue,
-                                  const unsigned int* __restrict__ nres,
+                                  const unsigned int* __restrict__ nres, int64_t cap,
                                   const double* __restrict__ x, int d,
                                   double* __restrict__ xs) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (int64_t)*nres * d) return;
+  const int64_t n = (int64_t)*nres < cap ? (int64_t)*nres : cap;
+  if (e >= n * d) return;
   xs[e] = x[rescue[e / d] * d + e % d];
 }
 __global__ void x3_scatter_rescued(const int64_t* __restrict__ rescue,
-                                   const unsigned int* __restrict__ nres,
+                                   const unsigned int* __restrict__ nres, int64_t cap,
                                    const double* __restrict__ outs,
                                    double* __restrict__ out) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q < (int64_t)*nres) out[rescue[q]] = outs[q];
+  if (q < (int64_t)*nres && q < cap) out[rescue[q]] = outs[q];
 }
 
 // candidate tiles (32 columns) per wave for KB MFMA instructions per tile
@@ -885,16 +887,44 @@ int x3_pack_population(const double* X, const double* w, int64_t N, int d,
   return ABC_OK;
 }
 
+// Rows the nested exact pass of a hinted call takes at most (0.04% of the
+// candidates are rescued at c3: ~400 of 1e6); list entries past it take the
+// fp64 rescue kernel instead.  The nested 'fine' plan keeps up to 256
+// population chunks of partials per row, so sizing it for all M reserved
+// ~4 GB at M = N = 1e6 for a handful of rows; at this cap it is ~70 MB.
+constexpr int64_t X3_NEST_CAP = 16384;
+inline int64_t x3_nest_rows(int64_t M) { return M < X3_NEST_CAP ? M : X3_NEST_CAP; }
+
 // the main launch's plan, then (hinted calls) room for the nested exact
-// pass over up to all M candidates: their rows, results and its own plan
+// pass over up to X3_NEST_CAP rescued candidates: their rows, results and
+// its own plan
 size_t x3_logpdf_workspace(int64_t M, int64_t N, int r) {
   const size_t main = plan_x3_ws(make_plan_x3(M, N, r));
-  const int64_t m1 = M > 0 ? M : 1;
+  const int64_t m1 = x3_nest_rows(M > 0 ? M : 1);
   size_t nested = 0;
   size_only<double>(nested, (size_t)m1 * 64);           // rows (d <= 64)
   size_only<double>(nested, (size_t)m1);                // results
-  size_only<char>(nested, plan_x3_ws(make_plan_x3(M, N, r, true)));  // the nested plan
+  size_only<char>(nested, plan_x3_ws(make_plan_x3(m1, N, r, true)));  // the nested plan
   return main + nested + 256;
+}
+
+// fp64 rescue of the list entries [q_begin, *nres) (count on the device):
+// launch pairs over slot ranges of the main plan's partial arrays (free once
+// combined); pairs past the count exit at once
+static void x3_rescue_fp64(const PlanX3& p, int64_t q_begin, int64_t M, const double* x, int d,
+                    const void* packed, int64_t N, const double* mu, const double* U, int r,
+                    double log_const, const int64_t* rescue, const unsigned int* nres,
+                    double* po, double* pl, double* out, hipStream_t s) {
+  const int ns = rescue_slices(N);
+  const int64_t cap = (int64_t)p.nchunk * p.Mpad / ns;
+  for (int64_t q0 = q_begin; q0 < M; q0 += cap) {
+    hipLaunchKernelGGL(x3_rescue_kernel, dim3((unsigned)ns, (unsigned)RS_GY), dim3(64), 0, s,
+                       rescue, nres, q0, cap, x, d, mu, U, r,
+                       (const double*)x3_Y(packed, N, r),
+                       (const double*)x3_lw(packed, N, r), N, po, pl);
+    hipLaunchKernelGGL(x3_rescue_final, dim3((unsigned)ceil_div(cap < M ? cap : M, 256)),
+                       dim3(256), 0, s, rescue, nres, q0, cap, ns, po, pl, log_const, out);
+  }
 }
 
 // count_dev (nullable): a device-sized launch -- only the first *count_dev
@@ -952,39 +982,36 @@ int x3_logpdf(const double* x, int64_t M, int d, const void* packed,
     // is launched for all M and its waves past the count leave at once, so
     // the call never waits for the GPU.  A candidate's result is independent
     // of M, of its slot in the list and of the list's length (chunking by N
-    // only), so sharded runs keep identical bits.
+    // only), so sharded runs keep identical bits.  The nested pass takes the
+    // first X3_NEST_CAP entries; any beyond (more than 16384 rescued rows in
+    // one call, never seen on the configs) take the fp64 rescue, equally
+    // within the parity bar but not bitwise the nested pass's values.
+    const int64_t Mn = x3_nest_rows(M);
     Carver sub(cv.rest(), cv.rest_bytes());
-    double* xs = sub.take<double>((size_t)M * d);
-    double* outs = sub.take<double>((size_t)M);
-    const size_t need = plan_x3_ws(make_plan_x3(M, N, r, true));
+    double* xs = sub.take<double>((size_t)Mn * d);
+    double* outs = sub.take<double>((size_t)Mn);
+    const size_t need = plan_x3_ws(make_plan_x3(Mn, N, r, true));
     void* ws2 = sub.take<char>(need);
     if (!sub.ok) return set_error(ABC_ERR_WORKSPACE, "mvn x3: nested rescue workspace");
-    hipLaunchKernelGGL(x3_gather_rescued, dim3((unsigned)ceil_div(M * d, 256)),
-                       dim3(256), 0, s, rescue, nres, x, d, xs);
+    hipLaunchKernelGGL(x3_gather_rescued, dim3((unsigned)ceil_div(Mn * d, 256)),
+                       dim3(256), 0, s, rescue, nres, Mn, x, d, xs);
     ABC_LAUNCHED();
-    const int rc2 = x3_logpdf(xs, M, d, packed, X, w, N, mu, U, r, log_const, log_norm,
+    const int rc2 = x3_logpdf(xs, Mn, d, packed, X, w, N, mu, U, r, log_const, log_norm,
                               outs, nullptr, ws2, need, s, ABC_PROF_RESCUE, nres);
     if (rc2) return rc2;
-    hipLaunchKernelGGL(x3_scatter_rescued, dim3((unsigned)ceil_div(M, 256)), dim3(256), 0,
-                       s, rescue, nres, outs, out);
+    hipLaunchKernelGGL(x3_scatter_rescued, dim3((unsigned)ceil_div(Mn, 256)), dim3(256), 0,
+                       s, rescue, nres, Mn, outs, out);
     ABC_LAUNCHED();
+    if (M > Mn) {
+      x3_rescue_fp64(p, Mn, M, x, d, packed, N, mu, U, r, log_const, rescue, nres, po, pl,
+                     out, s);
+      ABC_LAUNCHED();
+    }
     return ABC_OK;
   }
-  // fp64 rescue of the listed candidates (count on the device): launch
-  // pairs over slot ranges of the partial arrays' capacity; pairs past the
-  // count exit at once
-  const int ns = rescue_slices(N);
-  const int64_t cap = (int64_t)p.nchunk * p.Mpad / ns;
-  for (int64_t q0 = 0; q0 < M; q0 += cap) {
-    hipLaunchKernelGGL(x3_rescue_kernel, dim3((unsigned)ns, (unsigned)RS_GY), dim3(64), 0, s,
-                       rescue, nres, q0, cap, x, d, mu, U, r,
-                       (const double*)x3_Y(packed, N, r),
-                       (const double*)x3_lw(packed, N, r), N, po, pl);
-    ABC_LAUNCHED();
-    hipLaunchKernelGGL(x3_rescue_final, dim3((unsigned)ceil_div(cap < M ? cap : M, 256)),
-                       dim3(256), 0, s, rescue, nres, q0, cap, ns, po, pl, log_const, out);
-    ABC_LAUNCHED();
-  }
+  // fp64 rescue of the listed candidates
+  x3_rescue_fp64(p, 0, M, x, d, packed, N, mu, U, r, log_const, rescue, nres, po, pl, out, s);
+  ABC_LAUNCHED();
   return ABC_OK;
 }
 

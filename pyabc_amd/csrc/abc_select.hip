@@ -380,7 +380,7 @@ int column_mad_select(const double* X, int64_t R, int S, double* out, void* ws,
   const int CB = S < BK_T ? S : BK_T;
   const int ctiles = (int)ceil_div(S, CB);
   // expected window keys per band 2 BR_MARG / SMP = 9% x 160 x 256 = 3680 <
-  // BK_CAP.  Measured at c4 (same box, tools/ab_mad.sh): SMP 2048 / 96 rows /
+  // BK_CAP.  Measured at c4 (same box, tools/ab.sh mad): SMP 2048 / 96 rows /
   // 8 loads in flight 1.12 ms per MAD; 16 in flight 1.12; SMP 4096 / 128 rows
   // 1.05; SMP 4096 / 160 rows / 16 in flight 1.03.  Without the compaction
   // the bracket pass streams at 253 us (the colsum rate); with it 367 us.

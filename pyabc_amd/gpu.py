@@ -62,7 +62,9 @@ def workspace(nbytes, slot="main"):
     buf = _ws.get(key)
     nbytes = max(int(nbytes), 256)
     if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(int(nbytes * 1.25) + 256, dtype=torch.uint8,
+        # zero-filled once: abc_candidates_round's tile ticket counter lives
+        # in its first bytes, and every round leaves it zero
+        buf = torch.zeros(int(nbytes * 1.25) + 256, dtype=torch.uint8,
                           device=f"cuda:{dev}")
         _ws[key] = buf
     return buf
@@ -412,6 +414,11 @@ class CandidateRound:
             anc_table = ancestor_table(X, cdf)
             self._keep.append(anc_table)
         s.anc_table = _ptr(anc_table) if X is not None else None
+        # the prior's support box, once per generation (not per round)
+        self._box = torch.empty(2 * self.d, dtype=F64, device=prior_params.device)
+        nat.call("abc_prior_support_box", _ptr(prior_kind), _ptr(prior_params), self.d,
+                 _ptr(self._box), stream_ptr())
+        s.support_box = _ptr(self._box)
         self.device = prior_params.device
 
     def run(self, idx0, B, eps, cap, filter=True, rec_x=None, idx_out=None,

@@ -32,6 +32,11 @@ def test_size_queries_are_pure_host():
     assert nat.query("abc_mvn_packed_bytes", 1000, 10, nat.ABC_PREC_F64) == \
         63 * 64 * 3 * 8
     assert nat.query("abc_mvn_logpdf_workspace", 4096, 4096, 10, 0) > 0
+    # the x3 call at c3 (M = N = 1e6, r = 10): the main plan (candidate
+    # image, 32 chunks of partials) plus the nested rescue pass capped at
+    # 16384 rows -- not a nested plan sized for all M (~4 GB)
+    nb = nat.query("abc_mvn_logpdf_workspace", 10 ** 6, 10 ** 6, 10, nat.ABC_PREC_X3)
+    assert 0.5e9 < nb < 0.8e9, nb
     assert nat.query("abc_sort_pairs_workspace", 10 ** 6) > 32 * 10 ** 6
     # LocalTransition fit: d <= 5 carries the deferred collect's queue (256
     # row indices per particle) beside the dense moments' buffers

@@ -260,6 +260,30 @@ def test_mvn_x3_hinted_offsets(dev):
         t.logpdf_device(th, hint=torch.zeros(3, dtype=torch.int64, device=dev))
 
 
+def test_mvn_x3_rescue_overflow(dev):
+    """More rescued rows than the nested exact pass holds (X3_NEST_CAP =
+    16384, abc_mvn_x3.hip): every hint invalid, so all M = 20000 candidates
+    are rescued; the first 16384 list entries take the nested x3 pass, the
+    rest the fp64 rescue kernel.  Both match the oracle within the hinted
+    bar (2e-6)."""
+    import pandas as pd
+    from pyabc_amd.transition import MultivariateNormalTransition
+    rng = np.random.default_rng(5)
+    N, d, M = 3000, 10, 20_000
+    X = 0.8 + np.sqrt(0.2) * rng.standard_normal((N, d))
+    w = np.exp(0.5 * rng.standard_normal(N))
+    w /= w.sum()
+    t = MultivariateNormalTransition()
+    t.fit(pd.DataFrame(X, columns=[f"p{k}" for k in range(d)]), w.copy())
+    assert t._prec == 2
+    th, _, _, _ = t.propose_device(M)
+    ref = oracle.mvn_logpdf(th.cpu().numpy(), X, w, t.cov)
+    for h in (-1, N + 7):
+        hint = torch.full((M,), h, dtype=torch.int64, device=dev)
+        lp = t.logpdf_device(th, hint=hint).cpu().numpy()
+        np.testing.assert_allclose(np.exp(lp - ref), 1.0, rtol=2e-6, err_msg=f"hint {h}")
+
+
 @pytest.mark.parametrize("tag,kw", [("k50", dict(k=50, k_fraction=None)),
                                     ("default", dict())])
 def test_local_golden(dev, tag, kw):

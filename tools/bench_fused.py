@@ -28,6 +28,10 @@ def main():
     ap.add_argument("--wsigma", type=float, default=0.0,
                     help="lognormal importance weights, ESS/N = exp(-wsigma^2) "
                          "(c3's last generations: ~1e-2)")
+    ap.add_argument("--chain", type=int, default=1,
+                    help="rounds queued back to back per timed repetition (the "
+                         "per-round time is their mean: no host gap or clock "
+                         "ramp between rounds)")
     ap.add_argument("--staged", action="store_true")
     ap.add_argument("--sort-weights", action="store_true",
                     help="population rows in descending weight order (probe of a "
@@ -72,11 +76,13 @@ def main():
             for r in range(a.reps + 1):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                idx, cnt = fr.run(r * a.B, a.B, eps, cap=1 << 20, filter=filt)
+                for q in range(a.chain):
+                    idx, cnt = fr.run((r * a.chain + q) * a.B, a.B, eps, cap=1 << 20,
+                                      filter=filt)
                 e1.record()
                 e1.synchronize()
                 if r:
-                    ts.append(e0.elapsed_time(e1))
+                    ts.append(e0.elapsed_time(e1) / a.chain)
             c = int(cnt.cpu())
             ms = float(np.median(ts))
             print(f"rate {rate:g} eps {eps:.4f} filter={filt}: B={a.B} {ms:.2f} ms "
