@@ -342,6 +342,15 @@ int abc_candidates_round(const abc_candidate_spec* spec, int64_t idx0,
  * n_dev (nullable, device int64): the rows are the first min(n, *n_dev) --
  * a launch sized on the device (abc_candidates_round's count), queued before
  * the host has read that count. */
+/* Multi-rank round cutoff on the device: counts [nranks] (device int64, the
+ * round's accept counts of every rank, all-gathered in rank order) ->
+ * *keep (device int64) = how many of rank `rank`'s accepted candidates are
+ * among the first `need` accepted in global order.  Lets a rank queue
+ * abc_candidates_regen (n_dev = keep) before the host reads the counts;
+ * the reference takes the first n by evaluation index
+ * (pyabc/sampler/multicore_evaluation_parallel.py:133-135). */
+int abc_round_keep(const int64_t* counts, int nranks, int rank, int64_t need, int64_t* keep,
+                   void* stream);
 int abc_candidates_regen(const abc_candidate_spec* spec, int64_t idx0,
                          const int64_t* idx, int64_t n, const int64_t* n_dev,
                          double* theta, double* prior_logpdf, int64_t* ancestor,

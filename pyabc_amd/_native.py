@@ -57,6 +57,7 @@ SIGNATURES = {
     "abc_accept_compact": (I32, [P, I64, D, P, P, P, SZ, P]),
     "abc_candidates_workspace": (SZ, [I64]),
     "abc_prior_support_box": (I32, [P, P, I32, P, P]),
+    "abc_round_keep": (I32, [P, I32, I32, I64, P, P]),
     "abc_candidates_round": (I32, [P, I64, I64, D, P, D, I32, I64, P, P, P, P, SZ, P]),
     "abc_candidates_regen": (I32, [P, I64, P, I64, P, P, P, P, P, P, P]),
     "abc_pnorm_accept": (I32, [P, I64, I32, P, P, D, D, P, I32, I64, P, P, P, SZ, P]),

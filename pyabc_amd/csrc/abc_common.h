@@ -33,6 +33,27 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Resident blocks of a kernel on the current device: the occupancy query x
+// CUs, cached per kernel and device (grids of ticket-scheduled kernels).
+template <class K>
+int resident_blocks(K kernel, int block, int fallback = 1024) {
+  struct Entry { const void* k; int dev; int n; };
+  static Entry cache[64];
+  static int ncache = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fallback;
+  for (int i = 0; i < ncache; ++i)
+    if (cache[i].k == (const void*)kernel && cache[i].dev == dev) return cache[i].n;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      per_cu < 1 || cus < 1)
+    return fallback;
+  const int n = per_cu * cus;
+  if (ncache < 64) cache[ncache++] = Entry{(const void*)kernel, dev, n};
+  return n;
+}
+
 // Carve consecutive 256-B aligned regions out of a caller workspace.
 struct Carver {
   char* base; size_t cap; size_t off = 0; bool ok = true;

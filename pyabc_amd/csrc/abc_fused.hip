@@ -433,26 +433,6 @@ __global__ __launch_bounds__(64) void support_box_kernel(const int32_t* __restri
   if (k < d) support_bounds_wave(kind[k], params + 4 * k, box + 2 * k);
 }
 
-// resident blocks of a kernel on the current device (cached per kernel)
-template <class K>
-int resident_blocks(K kernel, int block) {
-  struct Entry { const void* k; int dev; int n; };
-  static Entry cache[64];
-  static int ncache = 0;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return RG_MAX;
-  for (int i = 0; i < ncache; ++i)
-    if (cache[i].k == (const void*)kernel && cache[i].dev == dev) return cache[i].n;
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      per_cu < 1 || cus < 1)
-    return 1024;
-  const int n = per_cu * cus;
-  if (ncache < 64) cache[ncache++] = Entry{(const void*)kernel, dev, n};
-  return n;
-}
-
 struct Ranges { int64_t nwords, wpr; int n; };
 // nwords accept words in at most `most` ranges of at least `least` words
 inline Ranges make_ranges(int64_t B, int64_t most, int64_t least) {
@@ -520,6 +500,23 @@ __global__ __launch_bounds__(256) void fused_regen_kernel(
   lp[i] = att <= A.P.max_attempts ? prior_logpdf(A.P.kind, A.P.params, d, th) : -INFINITY;
   if (anc) anc[i] = j;
   dist[i] = dd;
+}
+
+// ---- the multi-rank cutoff on the device -------------------------------------
+// keep[0] = how many of this rank's accepted candidates the round keeps: the
+// first `need` accepted in global order (ranks in order), counts gathered
+// from every rank (dd.cutoff on the host computes the same numbers)
+__global__ void round_keep_kernel(const int64_t* __restrict__ counts, int rank, int64_t need,
+                                  int64_t* __restrict__ keep) {
+  if (threadIdx.x != 0) return;
+  int64_t left = need > 0 ? need : 0, k = 0;
+  for (int q = 0; q <= rank; ++q) {
+    const int64_t c = counts[q] > 0 ? counts[q] : 0;
+    const int64_t take = c < left ? c : left;
+    if (q == rank) k = take;
+    left -= take;
+  }
+  *keep = k;
 }
 
 // ---- proposals only (the staged path of models without a fused simulator) --
@@ -1017,6 +1014,16 @@ extern "C" int abc_prior_support_box(const int32_t* prior_kind, const double* pr
   ABC_CHECK_ARG(prior_kind && prior_params && box, "prior_support_box: null pointer");
   hipLaunchKernelGGL(support_box_kernel, dim3((unsigned)d), dim3(64), 0, as_stream(stream),
                      prior_kind, prior_params, d, box);
+  ABC_LAUNCHED();
+  return ABC_OK;
+}
+
+extern "C" int abc_round_keep(const int64_t* counts, int nranks, int rank, int64_t need,
+                              int64_t* keep, void* stream) {
+  ABC_CHECK_ARG(counts && keep && nranks >= 1 && rank >= 0 && rank < nranks,
+                "round_keep: bad arguments");
+  hipLaunchKernelGGL(round_keep_kernel, dim3(1), dim3(64), 0, as_stream(stream), counts, rank,
+                     need, keep);
   ABC_LAUNCHED();
   return ABC_OK;
 }

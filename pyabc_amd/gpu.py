@@ -498,6 +498,15 @@ class CandidateRound:
                      int(n), p(n_dev), *ptrs, stream_ptr())
 
 
+def round_keep(counts, need, rank, out=None):
+    """abc_round_keep: this rank's kept rows of a round (device int64 [1])
+    from the all-gathered per-rank accept counts (device int64 [ws])."""
+    out = torch.empty(1, dtype=I64, device=counts.device) if out is None else out
+    nat.call("abc_round_keep", p(counts), int(counts.numel()), int(rank), int(need), p(out),
+             stream_ptr())
+    return out
+
+
 def _ptr(t):
     return None if t is None else p(t)
 

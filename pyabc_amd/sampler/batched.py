@@ -587,7 +587,7 @@ class BatchedGPUSampler(Sampler):
         ok = True
         rate, measured = self._acc_rate, False
         tot_B = tot_cnt = 0
-        filtered = 0
+        filtered = reruns = 0
         while n_acc < n:
             if self.check_max_eval and n_eval >= max_eval:
                 ok = False
@@ -617,35 +617,45 @@ class BatchedGPUSampler(Sampler):
                                   eps_dev=thr[0], eps_scale=thr[1])
             else:
                 idx, cnt = fr.run(lo, B, spec.eps, cap=need, filter=filt, rec_x=rx)
-            spec_regen = False
             pair = self._queue_pair(cnt, idx, min(need, B) - 1) if ws == 1 else None
             if ws == 1:
-                # the kept rows' regeneration is queued before the count read,
-                # sized on the device (min(count, need) rows into the pooled
-                # buffer), so the GPU is busy while the host reads the count
-                if kept is None or kept_off + need > kept[1]:
-                    if kept is not None and kept_off:
-                        kept_segs.append((kept[0], kept_off))
-                    views = self._kept_buffers(need, fr.d, S, dev)
-                    kept = (views, views[0].shape[0], [v.data_ptr() for v in views])
-                    kept_off = 0
-                fr.regen_into(lo, idx.data_ptr(), min(need, B),
-                              [a + kept_off * b for a, b in zip(kept[2], row_bytes)],
-                              n_dev=cnt)
-                spec_regen = True
+                n_keep = cnt
+            else:
+                # several ranks: the round's counts are all-gathered on the
+                # device and this rank's share of the first `need` accepted
+                # (global order) is computed there, so the regeneration is
+                # queued before any host read, as on one rank
+                gathered = dd.allgather_counts_device(cnt)
+                n_keep = gpu.round_keep(gathered, need, rank)
+                pair = self._queue_counts(gathered)
+            # the kept rows' regeneration is queued before the count read,
+            # sized on the device (the kept rows into the pooled buffer), so
+            # the GPU is busy while the host reads the count
+            if kept is None or kept_off + min(need, B) > kept[1]:
+                if kept is not None and kept_off:
+                    kept_segs.append((kept[0], kept_off))
+                views = self._kept_buffers(min(need, B), fr.d, S, dev)
+                kept = (views, views[0].shape[0], [v.data_ptr() for v in views])
+                kept_off = 0
+            fr.regen_into(lo, idx.data_ptr(), min(need, B),
+                          [a + kept_off * b for a, b in zip(kept[2], row_bytes)],
+                          n_dev=n_keep)
             if ws == 1:
                 # one read: the count and the index of the need-th accepted
                 cnt_local, pos_hint = self._wait_pair(pair)
+                counts = dd.allgather_counts(cnt_local, dev)
             else:
-                cnt_local = cnt
-            counts = dd.allgather_counts(cnt_local, dev)
+                # the gathered counts, for the host's bookkeeping
+                counts = self._wait_counts(pair)
             if thr is not None:
                 spec.eps_device = None
                 if np.isnan(thr[2].get()[0]):
                     # the select left the quantile undecided (knots in a tie
                     # run): the round ran at a NaN threshold and accepted
                     # nothing; run the same candidates again at the host
-                    # value (the sort-based rerun, gpu.resolve_quantile)
+                    # value (the sort-based rerun, gpu.resolve_quantile).
+                    # Every rank holds the same quantile, so all re-run
+                    reruns += 1
                     spec.eps
                     continue
             keep = dd.cutoff(counts, need)
@@ -664,20 +674,7 @@ class BatchedGPUSampler(Sampler):
                     rec_all[c_rank + 1:] = 0
             else:
                 evaluated = ws * B
-            if k_mine and spec_regen:
-                kept_off += k_mine          # regenerated before the count read
-            elif k_mine:
-                # kept rows regenerated straight into one per-generation
-                # buffer (rows of later rounds follow): no concatenation
-                if kept is None or kept_off + k_mine > kept[1]:
-                    if kept is not None and kept_off:
-                        kept_segs.append((kept[0], kept_off))
-                    views = self._kept_buffers(max(n - n_acc, k_mine), fr.d, S, dev)
-                    kept = (views, views[0].shape[0], [v.data_ptr() for v in views])
-                    kept_off = 0
-                fr.regen_into(lo, idx.data_ptr(), k_mine,
-                              [a + kept_off * b for a, b in zip(kept[2], row_bytes)])
-                kept_off += k_mine
+            kept_off += k_mine              # regenerated before the count read
             if record and cut is not None and rx is not None:
                 rec_x.append(rx)            # trimmed in _finish_cut
                 rec_keeps.append(None)
@@ -722,6 +719,7 @@ class BatchedGPUSampler(Sampler):
         self.last_stats = dict(rounds=rounds, evaluations=int(n_eval),
                                accepted=int(n_acc), fused=True,
                                candidates=int(tot_B), filtered_rounds=filtered,
+                               quantile_reruns=reruns,
                                records_truncated=self._records_truncated)
         recorded = None
         if record:
@@ -757,6 +755,28 @@ class BatchedGPUSampler(Sampler):
             return queued
         self._pair_ev.synchronize()
         return int(self._pair_host[0]), int(self._pair_host[1])
+
+    def _queue_counts(self, gathered):
+        """Queue the all-gathered round counts [ws] into a cached pinned
+        buffer and an event (the multi-rank _queue_pair); _wait_counts
+        reads them."""
+        torch = gpu.torch
+        if not gathered.is_cuda:
+            return gathered.numpy().copy()
+        ws = gathered.numel()
+        hc = getattr(self, "_counts_host", None)
+        if hc is None or hc.numel() != ws:
+            hc = self._counts_host = torch.empty(ws, dtype=torch.int64, pin_memory=True)
+            self._counts_ev = torch.cuda.Event()
+        hc.copy_(gathered, non_blocking=True)
+        self._counts_ev.record(torch.cuda.current_stream(gathered.device))
+        return None
+
+    def _wait_counts(self, queued):
+        if queued is not None:
+            return queued
+        self._counts_ev.synchronize()
+        return self._counts_host.numpy().copy()
 
     # population columns of the fused rounds are carved from pooled device
     # arenas: a generation's new population (kept by the History) would

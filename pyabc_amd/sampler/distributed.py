@@ -8,7 +8,8 @@ global index, the first-n-accepted cutoff -- and so the whole population --
 is identical for 1, 2, 4 or 8 ranks.
 
 Collectives per generation (all RCCL over xGMI on the GPU box):
-  * all_gather of per-round accept counts (R int64) -> global cutoff,
+  * all_gather of per-round accept counts (R int64) -> global cutoff
+    (computed on the device before the host reads the counts),
   * ONE all_gather of the accepted rows (theta, weight, distance, sum stats
     packed column-wise) -> the next population, replicated on every rank;
     row counts come from the cutoff every rank already holds,
@@ -52,6 +53,21 @@ def allgather_counts(count, device):
     out = [torch.empty_like(t) for _ in range(ws)]
     dist.all_gather(out, t)
     return torch.cat(out).cpu().numpy()      # one host read
+
+
+def allgather_counts_device(count):
+    """A 1-element device count per rank -> device int64 tensor [world] in
+    rank order, with no host read (RCCL gathers on the stream; gloo stages
+    through the host inside the collective).  The multi-rank fused round
+    computes its cutoff from it on the device (gpu.round_keep) and reads it
+    on the host only afterwards."""
+    rank, ws = world()
+    t = count.reshape(1).to(torch.int64)
+    if ws == 1:
+        return t
+    out = torch.empty(ws, dtype=torch.int64, device=t.device)
+    all_gather_flat(out, t)
+    return out
 
 
 def cutoff(counts, needed):

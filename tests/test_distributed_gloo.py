@@ -84,10 +84,18 @@ class _TailDistance(_Distance):
         return torch.ones(D, dtype=torch.float64), 2.0
 
 
+class _Fut:
+    def __init__(self, v):
+        self.v = v
+
+    def get(self):
+        return np.array([self.v])
+
+
 class _Spec:
     batched_capable = True
 
-    def __init__(self, eps, tail=False):
+    def __init__(self, eps, tail=False, nan_first=False):
         pop = _Population()
         self.t = GEN
         self.param_names = [f"p{k}" for k in range(D)]
@@ -98,6 +106,11 @@ class _Spec:
         self.x0vec = torch.ones(D, dtype=torch.float64)
         self.eps = eps
         self.weight_scale = 1.0
+        if nan_first:
+            # QuantileEpsilon's device threshold when its select left the
+            # quantile undecided (a knot in a > 2048-key tie run): NaN
+            nan = float("nan")
+            self.eps_device = (torch.tensor([nan], dtype=torch.float64), 1.0, _Fut(nan))
         self.prior_kind = None
         self.prior_params = None
 
@@ -130,6 +143,12 @@ def _install_cpu_doubles(monkeypatch_like):
         idx[:k] = torch.from_numpy(acc[:k])
         return idx, torch.tensor([len(acc)])
 
+    def round_keep(counts, need, rank):
+        # abc_round_keep on the host (its kernel is tested on the GPU)
+        from pyabc_amd.sampler import distributed as dd
+        return torch.tensor([int(dd.cutoff(counts.numpy(), need)[rank])])
+
+    monkeypatch_like(g, "round_keep", round_keep)
     monkeypatch_like(g, "pnorm", pnorm)
     monkeypatch_like(g, "pnorm_accept", pnorm_accept)
     monkeypatch_like(g, "require_device", lambda: torch.device("cpu"))
@@ -155,7 +174,9 @@ class _FusedRound:
                                            np.full(D, 0.5), SEED, GEN, lo)
         return th, lp, anc, x, oracle.pnorm(x, np.ones(D))
 
-    def run(self, lo, B, eps, cap, filter=True, rec_x=None):
+    def run(self, lo, B, eps, cap, filter=True, rec_x=None, eps_dev=None, eps_scale=1.0):
+        if eps_dev is not None:
+            eps = float(eps_dev[0]) * eps_scale
         *_, x, d = self._rows(lo, B)
         acc = np.nonzero(d <= eps)[0]
         idx = torch.zeros(max(int(cap), 1), dtype=torch.int64)
@@ -194,21 +215,24 @@ class _FusedRound:
             ctypes.memmove(ptr, r.ctypes.data, r.nbytes)
 
 
-def _run(n, eps, batch, record, fused=False):
+def _run(n, eps, batch, record, fused=False, nan_first=False):
     """fused: False (staged distance + compaction), True (fused rounds) or
-    "tail" (staged rounds with the accept tail)."""
+    "tail" (staged rounds with the accept tail); nan_first: the first fused
+    round gets an undecided (NaN) device threshold."""
     from pyabc_amd.sampler import BatchedGPUSampler
     s = BatchedGPUSampler(batch_size=batch, seed=SEED, fused=fused is True)
     if fused is True:
         s._fused_round = lambda spec, seed, gen, dev: _FusedRound(spec)
     s.sample_factory.record_rejected = record
-    sample = s.sample_until_n_accepted(n, _Spec(eps, tail=fused == "tail"))
+    sample = s.sample_until_n_accepted(n, _Spec(eps, tail=fused == "tail",
+                                                nan_first=nan_first))
     c = sample._cols
     rec = sample._recorded
     return dict(theta=c.theta.numpy(), w=c.weights.numpy(),
                 d=c.distances.numpy(), x=c.sum_stats.numpy(),
                 n_eval=np.array(s.nr_evaluations_),
                 rounds=np.array(s.last_stats["rounds"]),
+                reruns=np.array(s.last_stats.get("quantile_reruns", 0)),
                 rec=(rec.numpy() if rec is not None else np.zeros(0)))
 
 
@@ -225,13 +249,13 @@ def _count_collectives():
     return calls
 
 
-def _worker(rank, ws, port, out_dir, n, eps, batch, record, fused=False):
+def _worker(rank, ws, port, out_dir, n, eps, batch, record, fused=False, nan_first=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
         _install_cpu_doubles(setattr)
         calls = _count_collectives()
-        res = _run(n, eps, batch, record, fused)
+        res = _run(n, eps, batch, record, fused, nan_first)
         res["collectives"] = np.array(calls["n"])
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), **res)
     finally:
@@ -270,6 +294,36 @@ def test_sharded_sampler_matches_single_rank(monkeypatch, n, batch, record, ws, 
                 np.testing.assert_array_equal(got["rec"], ref["rec"])
     # the cutoff keeps exactly the first n accepted in global index order
     assert np.all(ref["d"] <= eps)
+
+
+@pytest.mark.parametrize("n,batch,record", [(300, 256, True), (37, 64, False)])
+def test_sharded_fused_quantile_rerun(monkeypatch, n, batch, record):
+    """The fused loop's first round at an undecided (NaN) device quantile
+    (batched.py: the round accepts nothing and the same candidates run again
+    at the host value): 1 and 2 ranks equal the staged loop -- population,
+    evaluations, recorded rows -- with one re-run counted
+    (last_stats["quantile_reruns"]) and its count gather the only extra
+    collective."""
+    eps, ws = 1.6, 2
+    _install_cpu_doubles(monkeypatch.setattr)
+    ref = _run(n, eps, batch * ws, record, True, nan_first=True)
+    staged = _run(n, eps, batch * ws, record, False)
+    assert int(ref["reruns"]) == 1
+    for k in ("theta", "w", "d", "x", "n_eval", "rec"):
+        np.testing.assert_array_equal(ref[k], staged[k], err_msg=k)
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_worker, args=(ws, _free_port(), tmp, n, eps, batch,
+                                          record, True, True),
+                           nprocs=ws, join=True, start_method="spawn")
+        for rank in range(ws):
+            got = dict(np.load(os.path.join(tmp, f"r{rank}.npz")))
+            assert int(got["reruns"]) == 1
+            assert int(got["n_eval"]) == int(ref["n_eval"])
+            assert int(got["collectives"]) == int(got["rounds"]) + 2 + int(record)
+            for k in ("theta", "w", "d", "x"):
+                np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+            if record:
+                np.testing.assert_array_equal(got["rec"], ref["rec"])
 
 
 def _collective_worker(rank, ws, port, out_dir):

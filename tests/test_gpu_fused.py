@@ -334,6 +334,24 @@ def test_regen_device_sized(dev):
             assert bool((o[n:] == 7).all())
 
 
+def test_round_keep_vs_cutoff(dev):
+    """abc_round_keep (the multi-rank cutoff on the device) against the
+    host's dd.cutoff: ranks 1..8, counts with zeros, need below / at / above
+    the total."""
+    from pyabc_amd import gpu
+    from pyabc_amd.sampler import distributed as dd
+    rng = np.random.default_rng(9)
+    for ws in (1, 2, 3, 8):
+        for _ in range(20):
+            counts = rng.integers(0, 50, ws) * rng.integers(0, 2, ws)
+            tot = int(counts.sum())
+            for need in (0, 1, max(tot // 2, 1), tot, tot + 7):
+                c = torch.as_tensor(counts, dtype=torch.int64, device=dev)
+                want = dd.cutoff(counts, need)
+                got = [int(gpu.round_keep(c, need, r).cpu()) for r in range(ws)]
+                assert got == list(want), (counts, need)
+
+
 def test_fused_vs_oracle_replay(dev):
     """Accept set against the numpy oracle's replay of the same streams
     (theta, x to 1e-12; masks equal away from |d - eps| < 1e-12)."""
@@ -411,6 +429,57 @@ def test_sampler_fused_equals_staged(dev, adaptive, local, max_fused, S, filt, d
             if filt == 1.0:
                 assert abc.sampler.last_stats.get("filtered_rounds", 0) > 0
     (_, p0, n0, e0), (_, p1, n1, e1) = runs
+    assert n0 == n1 and e0 == e1
+    for a, b in zip(p0, p1):
+        assert torch.equal(a.theta, b.theta)
+        assert torch.equal(a.weights, b.weights)
+        assert torch.equal(a.distances, b.distances)
+        assert torch.equal(a.sum_stats, b.sum_stats)
+
+
+def unit_scale(data, x_0=None):
+    """An adaptive distance's scale that keeps every weight at 1 (host scale
+    function): record_rejected on, distances unchanged."""
+    return 1.0
+
+
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_sampler_fused_quantile_rerun(dev, adaptive):
+    """Every candidate's statistics are 0 (a = 0, sigma = 0), so every
+    distance is the same and QuantileEpsilon's knots sit in a tie run of
+    4000 equal keys: the device select leaves the quantile undecided (NaN),
+    each generation's first fused round runs at the NaN threshold, accepts
+    nothing and is re-run at the host value (batched.py,
+    last_stats["quantile_reruns"]).  The fused sampler's populations,
+    weights, epsilons and evaluation counts equal the staged sampler's bit
+    for bit -- also with record_rejected on (an adaptive distance whose
+    scale keeps the weights at 1)."""
+    import pyabc_amd as pa
+    d, S = 4, 10
+    names = [f"p{k}" for k in range(d)]
+    keys = [f"y{k}" for k in range(S)]
+    runs = []
+    for fused in (False, True):
+        model = pa.LinearGaussianModel(names, keys, src=[k % d for k in range(S)],
+                                       a=np.zeros(S), sigma=np.zeros(S))
+        prior = pa.Distribution(**{n: pa.RV("norm", 0, 1) for n in names})
+        dist = (pa.AdaptivePNormDistance(p=2, scale_function=unit_scale) if adaptive
+                else pa.PNormDistance(p=2))
+        sampler = pa.BatchedGPUSampler(seed=5, fused=fused)
+        np.random.seed(3)
+        abc = pa.ABCSMC(model, prior, dist, population_size=4000,
+                        transitions=pa.MultivariateNormalTransition(),
+                        eps=pa.QuantileEpsilon(alpha=0.5), sampler=sampler)
+        abc.new("sqlite://", {k: 0.5 for k in keys})
+        h = abc.run(max_nr_populations=3)
+        if fused:
+            st = abc.sampler.last_stats
+            assert st.get("fused") and st["quantile_reruns"] == 1
+        assert abc.sampler.sample_factory.record_rejected == adaptive
+        pops = [h.get_population_device(t) for t in range(h.max_t + 1)]
+        runs.append((pops, [g["n_sim"] for g in abc.generation_log],
+                     [g["eps"] for g in abc.generation_log]))
+    (p0, n0, e0), (p1, n1, e1) = runs
     assert n0 == n1 and e0 == e1
     for a, b in zip(p0, p1):
         assert torch.equal(a.theta, b.theta)
