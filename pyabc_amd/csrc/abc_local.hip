@@ -1214,7 +1214,7 @@ int launch_fit(const double* X, const double* w, int64_t N, int64_t nq,
     half8* img = cv.take<half8>((size_t)(nsteps + DM_SB) * mm_nt<D>() * 64);
     double* part16 = cv.take<double>((size_t)RS16 * 16 * mm_nt<D>() * (size_t)N);
     double* cenm = cv.take<double>((size_t)NM * N);
-    float* drows = cv.take<float>((size_t)(nsteps + DM_SB) * DM_RSTEP);
+    float* drows = cv.take<float>((size_t)(nsteps + DM_SB) * dm_rstep<D>());
     if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "local_fit: workspace too small");
     ABC_HIP(hipMemsetAsync(bnd, 0, sizeof(unsigned long long) * (1 + D), s));
     ABC_HIP(hipMemsetAsync(flag, 0, 2 * sizeof(int), s));
@@ -1617,7 +1617,7 @@ extern "C" size_t abc_local_fit_workspace(int64_t N, int d) {
     size_only<half8>(off, (size_t)((nsteps + DM_SB) * nt * 64));
     size_only<double>(off, (size_t)mm_chunks(n1, nsteps) * 16 * nt * (size_t)n1);
     size_only<double>(off, nm * (size_t)n1);
-    size_only<float>(off, (size_t)(nsteps + DM_SB) * DM_RSTEP);
+    size_only<float>(off, (size_t)(nsteps + DM_SB) * dm_rstep<5>());
   }
   return off + 256;
 }

@@ -10,10 +10,13 @@
 // features] product of mm_moments_kernel (same exact 11-bit limb image of
 // F, same fp64 flushes, same mm_finish_kernel), with two changes that
 // matter at k = N/4, where every row of every wave has members:
-//  * the membership key is s^ = n^_n + sum_q y^_jq (-2 y^_nq) + n^_j on the
-//    centred fp32 rows of knn_prep_kernel (D fma + 1 add per pair instead of
-//    D sub + D fma; any evaluation order is inside kn_bound), decided
-//    against the fp32 cuts of v* and settled exactly in fp64 between them;
+//  * the membership key is the k-NN select's s^ = n^_j + n^_n - 2 y^_j . y^_n
+//    on the same centred fp32 features, formed by v_mfma_f32_16x16x4_f32
+//    (the select's k-ordered chain, so kn_bound covers it) from a row
+//    fragment image in the step's k-slot order: 2 x KB MFMAs per 32-row step
+//    where the VALU spent D fma + 1 add per pair (round 5: 21.6 VALU
+//    lane-instructions per pair); the keys are decided against the fp32 cuts
+//    of v* and settled exactly in fp64 between them;
 //  * both operand streams reach LDS by global_load_lds (16 B per lane, no
 //    staging registers), double-buffered per DM_SB 32-row steps, so the
 //    wave's registers go to its 2 x 7 accumulator tiles.
@@ -22,13 +25,17 @@ constexpr int DM_G = 1;                    // particle tiles per wave
 constexpr int DM_T = DM_W * 64;
 constexpr int DM_PB = DM_W * DM_G * 16;    // particles per block
 constexpr int DM_SB = 2;                   // 32-row steps per LDS stage
-constexpr int DM_ROWF = 8;                 // floats per staged row: y^ (D <= 7), n^
-// rows image: per 32-row step 32 rows of DM_ROWF floats with 4 pad floats
-// after every 8 rows, so the 4 lane groups (rows 8 kq + u) read 4 different
-// bank quads of the staged copy (unpadded, the rows lay 64 words apart: one
-// bank quad, a 4-way conflict on every row read)
-constexpr int DM_RSTEP = 32 * DM_ROWF + 16;     // floats per 32-row step
-__host__ __device__ constexpr int dm_row_off(int r) { return r * DM_ROWF + (r >> 3) * 4; }
+// Row fragments of one 32-row step: 2 tiles h x KB k-blocks x 64 lanes
+// (floats); lane l of (h, kb) holds feature 4 kb + (l >> 4) of the step's
+// row dm_row(h, l & 15), features [y^ (D), n^, 1, 0...] (rows >= N: n^ =
+// +inf, the rest 0).  The MFMA returns tile h's keys at lane l for rows
+// dm_row(h, 4 (l >> 4) + r), r < 4 -- with dm_row(h, i) = 8 (i >> 2) +
+// (i & 3) + 4 h those are rows 8 (l >> 4) + 4 h + r: the k-slots of the
+// moments MFMA's A fragment (lane l: rows 8 (l >> 4) + u, u < 8), so the
+// keys become the fragment without a lane exchange.  Reads are one float per
+// lane at consecutive addresses (no bank conflicts).
+template <int D> constexpr int dm_rstep() { return 2 * kn_kb<D>() * 64; }
+__host__ __device__ constexpr int dm_row(int h, int i) { return 8 * (i >> 2) + (i & 3) + 4 * h; }
 
 __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(
@@ -36,29 +43,33 @@ __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
       (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// rows [y^_0 .. y^_{D-1}, n^, 0...] per row (rows >= N: n^ = +inf, key +inf)
+// the row fragment image (one thread per row; rows past N key +inf)
 template <int D>
 __global__ __launch_bounds__(256) void knn_rows_kernel(const double* __restrict__ X, int64_t N,
                                                        int64_t nrows,
                                                        const double* __restrict__ cen,
                                                        float* __restrict__ rows) {
+  constexpr int KB = kn_kb<D>();
   const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= nrows) return;
-  float* dst = rows + (j >> 5) * DM_RSTEP + dm_row_off((int)(j & 31));
-  float f[DM_ROWF];
+  const int r = (int)(j & 31);
+  const int h = (r >> 2) & 1, i = 4 * (r >> 3) + (r & 3);   // dm_row(h, i) == r
+  float* dst = rows + (j >> 5) * dm_rstep<D>() + h * KB * 64 + i;
+  float f[4 * KB];
 #pragma unroll
-  for (int k = 0; k < DM_ROWF; ++k) f[k] = 0.0f;
+  for (int k = 0; k < 4 * KB; ++k) f[k] = 0.0f;
   if (j < N) {
     float y[D];
     const float n = kn_feat<D>(X, j, cen, y);
 #pragma unroll
     for (int q = 0; q < D; ++q) f[q] = y[q];
     f[D] = n;
+    f[D + 1] = 1.0f;
   } else {
     f[D] = INFINITY;
   }
 #pragma unroll
-  for (int k = 0; k < DM_ROWF; ++k) dst[k] = f[k];
+  for (int k = 0; k < 4 * KB; ++k) dst[(k >> 2) * 64 + 16 * (k & 3)] = f[k];
 }
 
 // DEFER (the deferred collect, see knn_select_kernel): sel_v / sel_jcut hold
@@ -78,12 +89,13 @@ __global__ __launch_bounds__(DM_T) void knn_dense_kernel(
     const unsigned long long* __restrict__ sel_v, const long long* __restrict__ sel_jcut,
     const long long* __restrict__ sel_rank0, double* __restrict__ part,
     int* __restrict__ qcnt, int* __restrict__ qidx, int* __restrict__ cbelow) {
-  static_assert(D + 1 <= DM_ROWF, "staged row holds y^ and n^");
+  constexpr int KB = kn_kb<D>();
+  constexpr int RSTEP = dm_rstep<D>();
   constexpr int NT = mm_nt<D>(), NCP = 16 * NT;
   constexpr int BP = DM_SB * NT * 64;              // B pieces (16 B) per stage
-  constexpr int RP = DM_SB * DM_RSTEP / 4;         // row pieces per stage
+  constexpr int RP = DM_SB * RSTEP / 4;            // row pieces per stage
   constexpr int SP = BP + RP;
-  static_assert(BP % 64 == 0 && DM_RSTEP % 4 == 0, "B stream: whole wave-instructions");
+  static_assert(BP % 64 == 0 && RSTEP % 4 == 0, "B stream: whole wave-instructions");
   constexpr int PW = ((SP + 63) / 64 + DM_W - 1) / DM_W;  // wave-instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char stage[2][SP * 16];
   __shared__ int s_qn[DEFER ? DM_PB : 1], s_q[DEFER ? DM_PB * DQ_L : 1];
@@ -101,16 +113,26 @@ __global__ __launch_bounds__(DM_T) void knn_dense_kernel(
   const KnBound Bd = kn_bound<D>(*R2p);
   const float zc = kn_cut_above(0.0, Bd);
 
-  // the lane's particle in each tile: -2 y^_n, n^_n and the fp32 cuts of v*
-  float m2y[DM_G][D], nn[DM_G], cin[DM_G], cout[DM_G];
+  // the lane's particle in each tile: its key features (the B operand of
+  // the key MFMA: feature 4 kb + (lane >> 4) of [-2 y^_n, 1, n^_n]) and the
+  // fp32 cuts of v*
+  float bfr[DM_G][KB], cin[DM_G], cout[DM_G];
 #pragma unroll
   for (int g = 0; g < DM_G; ++g) {
     const int64_t pn = p0 + 16 * g + (lane & 15);
     const int64_t pe = pn < N ? pn : N - 1;
     float y[D];
-    nn[g] = kn_feat<D>(X, pe, cen, y);
+    const float nn = kn_feat<D>(X, pe, cen, y);
 #pragma unroll
-    for (int q = 0; q < D; ++q) m2y[g][q] = -2.0f * y[q];
+    for (int kb = 0; kb < KB; ++kb) {
+      const int k = 4 * kb + (lane >> 4);
+      float v = 0.0f;
+#pragma unroll
+      for (int q = 0; q < D; ++q) if (k == q) v = -2.0f * y[q];
+      if (k == D) v = 1.0f;
+      if (k == D + 1) v = nn;
+      bfr[g][kb] = v;
+    }
     if constexpr (DEFER) {
       cin[g] = kn_cut_below(__longlong_as_double((long long)sel_v[pe]), Bd);
       cout[g] = kn_cut_above(__longlong_as_double(sel_jcut[pe]), Bd);
@@ -153,7 +175,7 @@ __global__ __launch_bounds__(DM_T) void knn_dense_kernel(
   // padded by DM_SB steps past nsteps, so a partial last stage loads safely)
   auto issue = [&](int buf, int64_t sb) {
     const char* bsrc = reinterpret_cast<const char*>(img + sb * NT * 64);
-    const char* rsrc = reinterpret_cast<const char*>(rows + sb * DM_RSTEP);
+    const char* rsrc = reinterpret_cast<const char*>(rows + sb * RSTEP);
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
       const int wi = wv * PW + i;              // wave-instruction index (uniform)
@@ -174,21 +196,25 @@ __global__ __launch_bounds__(DM_T) void knn_dense_kernel(
     const int nk = (int)((s1 - sb) < DM_SB ? (s1 - sb) : DM_SB);
     for (int k = 0; k < nk; ++k) {
       half8 a[DM_G];
-      uint32_t openm = 0u, inm = 0u;   // bit 8 g + u: pair (tile g, row u)
-      // rows one at a time (not unrolled: the 8 rows' features would
-      // otherwise be loaded up front and cost the occupancy)
-#pragma unroll 2
-      for (int u = 0; u < 8; ++u) {
-        const float* rf = rs + k * DM_RSTEP + dm_row_off(8 * kq + u);
-        const f32x4 r0 = *reinterpret_cast<const f32x4*>(rf);
-        const f32x4 r1 = *reinterpret_cast<const f32x4*>(rf + 4);
-        float y[8] = {r0[0], r0[1], r0[2], r0[3], r1[0], r1[1], r1[2], r1[3]};
+      uint32_t openm = 0u, inm = 0u;   // bit 8 g + u: pair (tile g, row 8 kq + u)
+      // the step's keys: tile h gives rows 8 kq + 4 h + r (r < 4)
+      const float* rf = rs + k * RSTEP + lane;
+      float af[2][KB];
 #pragma unroll
-        for (int g = 0; g < DM_G; ++g) {
-          float sk = nn[g];
+      for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int q = 0; q < D; ++q) sk = __builtin_fmaf(y[q], m2y[g][q], sk);
-          sk += y[D];
+        for (int kb = 0; kb < KB; ++kb) af[h][kb] = rf[(h * KB + kb) * 64];
+#pragma unroll
+      for (int g = 0; g < DM_G; ++g) {
+        knf4 c[2] = {knf4{0.f, 0.f, 0.f, 0.f}, knf4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            c[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[h][kb], bfr[g][kb], c[h], 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float sk = c[u >> 2][u & 3];
           const bool in = sk < cin[g] && sk > zc;
           openm |= (!in && !(sk > cout[g])) ? (1u << (8 * g + u)) : 0u;
           inm |= in ? (1u << (8 * g + u)) : 0u;
