@@ -419,6 +419,8 @@ int abc_importance_weights(const double* prior_logpdf,
  * the knots lie in more than 2048 points of one 2^-24 slice of the key span
  * (ties by the thousand) it writes NaN: the caller then runs
  * abc_weighted_quantile_sorted (full stable radix sort, always decided).
+ * abc_weighted_quantile's workspace is zero before its first call (e.g.
+ * hipMemset at allocation) and every call leaves its control block zero.
  * abc_sort_pairs_f64: stable LSD radix sort of fp64 keys carrying fp64
  * values. */
 size_t abc_sort_pairs_workspace(int64_t N);

@@ -13,7 +13,8 @@
 // fixed-point integers (w * 2^(62 - ceil log2 N) / max w, truncated), so the
 // histograms' sums are exact integers, independent of any order -- the search
 // is deterministic -- and each bin's cumulative weight is known to within N
-// units.  Four kernels (plus one memset of the control block); each
+// units.  Four kernels (the control block is left zeroed for the next
+// call, no memset); each
 // single-block step runs in the last block of the multi-block kernel before
 // it (device-scope fence + counter), so there is no one-block launch:
 //   1. range: min / max key and max weight (integer max atomics);
@@ -65,7 +66,8 @@ __device__ __forceinline__ double qval(u64 k) {
   return __longlong_as_double((long long)b);
 }
 
-// per-call control block, zeroed by the launcher's one memset: the global
+// per-call control block, zero when a call starts (the workspace is zeroed
+// once; the gather's last block resets it): the global
 // key range (kmin stored complemented, so zero is the identity of the max
 // atomics), the last-block counters of the three multi-block stages, the
 // fixed-point total and the list counter
@@ -171,26 +173,6 @@ __global__ __launch_bounds__(WQ_T) void wq_range_kernel(const double* __restrict
   }
 }
 
-// Last-block hand-over.  Everything one stage hands to its last block is
-// written by agent-scope atomics (histogram adds, list / partial-sum stores
-// through __hip_atomic_store) and read there by agent-scope atomic loads, so
-// no L2 write-back is needed per block: each wave waits for its own memory
-// operations to complete, the block's counter is bumped once, and the block
-// that brings it to the grid size runs the stage's tail (pick / final) after
-// one acquire fence.  The single-block kernels and their launch gaps go.
-__device__ __forceinline__ bool wq_last_block(unsigned int* done) {
-  __shared__ int s_last;
-  __builtin_amdgcn_s_waitcnt(0);   // this wave's atomics / stores completed
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return false;
-  __atomic_thread_fence(__ATOMIC_ACQUIRE);
-  return true;
-}
-
 template <class T>
 __device__ __forceinline__ void st_agent(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -198,6 +180,44 @@ __device__ __forceinline__ void st_agent(T* p, T v) {
 template <class T>
 __device__ __forceinline__ T ld_agent(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Last-block hand-over.  Everything one stage hands to its last block is
+// written by agent-scope atomics (histogram adds, list / partial-sum stores
+// through __hip_atomic_store) and read there by agent-scope atomic loads, so
+// no L2 write-back is needed per block: each wave waits for its own memory
+// operations to complete, the block's counter is bumped once, and the block
+// that brings it to the grid size runs the stage's tail (pick / final) after
+// one acquire fence.  The single-block kernels and their launch gaps go.
+// The counter's bump is a release (one per block: the block's writes,
+// ordered before it by the barrier, happen-before the last block's reads)
+// and the last block's acquire pairs with it, as the HIP / LLVM memory model
+// requires on a multi-XCD part.
+__device__ __forceinline__ bool wq_last_block(unsigned int* done) {
+  __shared__ int s_last;
+  __builtin_amdgcn_s_waitcnt(0);   // this wave's atomics / stores completed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+             gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return true;
+}
+
+// the control block back to zero for the next call (the gather's last block,
+// after every stage has read it): no memset per call
+__device__ __forceinline__ void wq_reset(WqCtl* ctl) {
+  if (threadIdx.x == 0) {
+    st_agent(&ctl->nkmin, 0ull);
+    st_agent(&ctl->kmax, 0ull);
+    st_agent(&ctl->wmax, 0ull);
+    st_agent(&ctl->tot, 0ull);
+    st_agent(&ctl->list_n, 0u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st_agent(&ctl->done[i], 0u);
+  }
 }
 
 __device__ __forceinline__ void seg_keys(u64 lo, u64 hi, int sh, int b1, int b2, u64& slo,
@@ -453,6 +473,7 @@ __global__ __launch_bounds__(WQ_T) void wq_gather_final_kernel(
     }
   }
   if (!wq_last_block(&ctl->done[2])) return;
+  wq_reset(ctl);
   const int nsum = gridDim.x;
   __shared__ u64 skey[WQ_CAP];
   __shared__ int sidx[WQ_CAP];
@@ -592,7 +613,7 @@ extern "C" size_t abc_weighted_quantile_workspace(int64_t N) {
   return off + 256;
 }
 
-// Launches: one memset (the control block), range, level-1 histogram (its
+// Launches: range, level-1 histogram (its
 // last block picks), level-2 histogram (exits at once when level 1 fits; its
 // last block picks), gather (its last block sorts the list and
 // interpolates).  No single-block kernel.
@@ -616,7 +637,6 @@ extern "C" int abc_weighted_quantile(const double* points, const double* w, int6
   double* lw = cv.take<double>(WQ_CAP);
   double* psum = cv.take<double>((size_t)2 * nb);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "quantile: carve");
-  ABC_HIP(hipMemsetAsync(ctl, 0, sizeof(WqCtl), s));
   hipLaunchKernelGGL(wq_range_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, ctl,
                      ghc, ghw);
   ABC_LAUNCHED();

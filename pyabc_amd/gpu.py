@@ -62,8 +62,9 @@ def workspace(nbytes, slot="main"):
     buf = _ws.get(key)
     nbytes = max(int(nbytes), 256)
     if buf is None or buf.numel() < nbytes:
-        # zero-filled once: abc_candidates_round's tile ticket counter lives
-        # in its first bytes, and every round leaves it zero
+        # zero-filled once: abc_candidates_round's tile ticket counter and
+        # abc_weighted_quantile's control block live in their slots' first
+        # bytes, and every call leaves them zero
         buf = torch.zeros(int(nbytes * 1.25) + 256, dtype=torch.uint8,
                           device=f"cuda:{dev}")
         _ws[key] = buf
@@ -569,7 +570,8 @@ def weighted_quantile(points, w, alpha, sorted_path=False):
     q = torch.empty(1, dtype=F64, device=points.device)
     name = "abc_weighted_quantile_sorted" if sorted_path else "abc_weighted_quantile"
     nb = nat.query(name + "_workspace", N)
-    ws = workspace(nb, "sort")
+    # the select's own slot: its control block stays zero between calls
+    ws = workspace(nb, "sort" if sorted_path else "quantile")
     nat.call(name, p(points), p(w), N, float(alpha), p(q), p(ws), ws.numel(), stream_ptr())
     return q
 
