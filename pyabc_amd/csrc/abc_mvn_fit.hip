@@ -19,8 +19,8 @@
 // off-diagonal is below 2^-53 sqrt(|a_pp a_qq|)), eigenpairs sorted by
 // decreasing eigenvalue, the whitening U (kept columns scaled by 1/sqrt(s),
 // cut ones zero -- so the MFMA image can be packed at rank d before the
-// host knows the rank), and L L^T = cov by a semidefinite Cholesky (pivots
-// at or below the cut-off give zero columns).  stats = [rank, log pdet,
+// host knows the rank), and L L^T = cov from the eigen factor (QR of
+// (V diag(sqrt s))^T, as the host's psd_whitening).  stats = [rank, log pdet,
 // support tol, -log max w, bandwidth, min s, max s, ok].
 #include "abc_common.h"
 
@@ -251,27 +251,48 @@ __global__ __launch_bounds__(FT) void mvn_fit_kernel(const double* __restrict__ 
     stats[6] = mx;
     stats[7] = (nan || mn < -cut) ? 0.0 : 1.0;
   }
-  // ---- L L^T = cov, lower; pivots <= cut give zero columns
+  // ---- L L^T = cov, lower: from the eigen factor B = V diag(sqrt(max(s, 0)))
+  // (B B^T = cov for any PSD cov, the host's psd_whitening): Householder QR
+  // of B^T = Q R, L = R^T with the rows of R signed so diag(L) >= 0.  An
+  // unpivoted semidefinite Cholesky zeroing pivots at or below the cut-off
+  // left off-diagonal terms up to sqrt(cut c_ii) out of L L^T for a direction
+  // whose variance sits near the cut.
+  for (int e = t; e < d * d; e += FT) {
+    const int k = e / d, i = e % d;
+    C[k][i] = V[i][k] * sqrt(fmax(lam[k], 0.0));   // C = B^T
+  }
+  __syncthreads();
   for (int j = 0; j < d; ++j) {
     if (t == 0) {
-      const double s = C[j][j];
-      const double ljj = s > cut ? sqrt(s) : 0.0;
-      C[j][j] = ljj;
-      s_piv = ljj;
+      double nrm = 0.0;
+      for (int i = j; i < d; ++i) nrm += C[i][j] * C[i][j];
+      nrm = sqrt(nrm);
+      const double x0 = C[j][j];
+      const double alpha = x0 >= 0.0 ? -nrm : nrm;
+      // the reflector v = x - alpha e_1 into lam (the eigenvalues are in C)
+      double vn = 0.0;
+      for (int i = j; i < d; ++i) {
+        const double v = (i == j) ? x0 - alpha : C[i][j];
+        lam[i] = v;                                   // lam: the reflector
+        vn += v * v;
+      }
+      s_piv = vn;                                     // |v|^2 (0: nothing to do)
     }
     __syncthreads();
-    const double ljj = s_piv;
-    for (int i = j + 1 + t; i < d; i += FT) C[i][j] = ljj > 0.0 ? C[i][j] / ljj : 0.0;
-    __syncthreads();
-    for (int e = t; e < (d - j - 1) * (d - j - 1); e += FT) {
-      const int i = j + 1 + e / (d - j - 1), k = j + 1 + e % (d - j - 1);
-      if (k <= i) C[i][k] -= C[i][j] * C[k][j];
+    const double vn = s_piv;
+    if (vn > 0.0) {
+      for (int k = j + t; k < d; k += FT) {
+        double dot = 0.0;
+        for (int i = j; i < d; ++i) dot += lam[i] * C[i][k];
+        const double f = 2.0 * dot / vn;
+        for (int i = j; i < d; ++i) C[i][k] -= f * lam[i];
+      }
     }
     __syncthreads();
   }
   for (int e = t; e < d * d; e += FT) {
     const int i = e / d, j = e % d;
-    L[e] = j <= i ? C[i][j] : 0.0;
+    L[e] = j <= i ? (C[j][j] < 0.0 ? -C[j][i] : C[j][i]) : 0.0;
   }
 }
 

@@ -604,7 +604,10 @@ class ABCSMC:
                 logger.info(f"Acceptance rate: {pop_size} / {n_sim} = "
                             f"{rate:.4e}, ESS={ess:.4e}.")
             pending.append(log_ess)
-            if not hasattr(self.sampler, "on_density_queued"):
+            # a generation callback sees this generation's log complete (its
+            # ESS read here, not deferred behind the next density)
+            if not hasattr(self.sampler, "on_density_queued") or \
+                    self.generation_callback is not None:
                 flush()
             if self.generation_callback is not None:
                 self.generation_callback(t)
