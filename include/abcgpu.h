@@ -416,8 +416,8 @@ int abc_importance_weights(const double* prior_logpdf,
  * points sorted ascending, ties by index), found by a weighted MSD select
  * (fixed-point bin weights, a few hundred points sorted around the knots;
  * abc_quantile.hip), written to *q (device double).  Weights >= 0.  When
- * the knots lie in more than 2048 points of one 2^-24 slice of the key span
- * (ties by the thousand) it writes NaN: the caller then runs
+ * the knots lie in more than 2048 points of one narrow slice of the key span
+ * (2^-23 of it or less; ties by the thousand) it writes NaN: the caller then runs
  * abc_weighted_quantile_sorted (full stable radix sort, always decided).
  * abc_weighted_quantile's workspace is zero before its first call (e.g.
  * hipMemset at allocation) and every call leaves its control block zero.

@@ -34,10 +34,16 @@
 //      points before it), forms the cumulative weights from the
 //      sum below, xp and np.interp's rules (quantile_pick semantics: clamps,
 //      exact knot hit, NaN fallbacks).
+// Up to 2^20 points (c3's population) the same stages run in ONE launch on a
+// resident grid, the points held in registers and the stages handed on by
+// counters and flags instead of kernel boundaries (wq_onepass_kernel below:
+// 0.045 vs 0.069 ms at 1e6).
 // A segment that still holds more than WQ_CAP points after level 2 (ties by
 // the thousand at the knots, e.g. discrete distances) is not decided here:
 // *q = NaN, and the host (gpu.weighted_quantile's readers) reruns the exact
 // sort-based abc_weighted_quantile_sorted on the same inputs.
+#include <type_traits>
+
 #include "abc_common.h"
 
 namespace abc {
@@ -69,8 +75,10 @@ __device__ __forceinline__ double qval(u64 k) {
 // per-call control block, zero when a call starts (the workspace is zeroed
 // once; the gather's last block resets it): the global
 // key range (kmin stored complemented, so zero is the identity of the max
-// atomics), the last-block counters of the three multi-block stages, the
-// fixed-point total and the list counter
+// atomics), the last-block counters of the three multi-block stages (the
+// one-launch path: done[0] its arrival counter, done[1] its hand-off flag),
+// the fixed-point total and the list counter; pad != 0 marks a one-launch
+// call whose wait timed out
 struct WqCtl {
   u64 nkmin, kmax, wmax;
   unsigned int done[4];
@@ -234,12 +242,13 @@ __device__ __forceinline__ void seg_keys(u64 lo, u64 hi, int sh, int b1, int b2,
 // certainly below the target to the first whose interval lies certainly
 // above it (the knots j and j + 1 lie between them, inclusive).  Block
 // reductions by wave shuffles (no same-address LDS atomics).
+// The level-1 pick also returns the input's fixed-point total (tot_out),
+// which level 2 takes as tot_in.
 template <int BITS>
-__device__ void wq_pick_block(int64_t N, double alpha, const WqCtl* ctl,
-                              const unsigned int* ghc, const u64* ghw, u64 lo, u64 hi,
-                              u64 base_w, long long base_c, bool level1, WqCtl* ctl_w,
-                              WqDesc* out) {
-  constexpr int NB = 1 << BITS, PER = NB / WQ_T;
+__device__ void wq_pick_block(int64_t N, double alpha, const unsigned int* ghc,
+                              const u64* ghw, u64 lo, u64 hi, u64 base_w, long long base_c,
+                              bool level1, double tot_in, u64* tot_out, WqDesc* out) {
+  constexpr int NB = 1 << BITS, PER = NB >= WQ_T ? NB / WQ_T : 1;
   __shared__ u64 s_w[WQ_T / 64];
   __shared__ long long s_c[WQ_T / 64];
   __shared__ int s_i[4][WQ_T / 64];
@@ -252,8 +261,9 @@ __device__ void wq_pick_block(int64_t N, double alpha, const WqCtl* ctl,
   long long sc = 0;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    c[i] = ld_agent(&ghc[t * PER + i]);
-    wsm[i] = ld_agent(&ghw[t * PER + i]);
+    const bool has = NB >= WQ_T || t < NB;   // fewer bins than threads: the rest hold 0
+    c[i] = has ? ld_agent(&ghc[t * PER + i]) : 0u;
+    wsm[i] = has ? ld_agent(&ghw[t * PER + i]) : 0ull;
     sw += wsm[i];
     sc += c[i];
   }
@@ -276,7 +286,7 @@ __device__ void wq_pick_block(int64_t N, double alpha, const WqCtl* ctl,
   }
   // the whole input's fixed-point total: summed at level 1 and kept in the
   // control block for level 2
-  const double tot_fx = level1 ? (double)tw : __longlong_as_double((long long)ctl->tot);
+  const double tot_fx = level1 ? (double)tw : tot_in;
   const double target = alpha * tot_fx;
   const double margin = (double)N + ldexp(tot_fx, -48) + 4096.0;
   ow += base_w;
@@ -339,7 +349,7 @@ __device__ void wq_pick_block(int64_t N, double alpha, const WqCtl* ctl,
     d.ok = d.count <= (level1 ? WQ_REFINE : WQ_CAP) ? 1 : 0;
     d.done = 0;
     *out = d;
-    if (level1) ctl_w->tot = (u64)__double_as_longlong((double)tw);
+    if (level1) *tot_out = (u64)__double_as_longlong((double)tw);
   }
 }
 
@@ -389,8 +399,10 @@ __global__ __launch_bounds__(WQ_T) void wq_hist_kernel(
     }
   }
   if (!wq_last_block(&ctl->done[LEVEL - 1])) return;
-  wq_pick_block<BITS>(N, alpha, ctl, ghc, ghw, lo, hi, prev ? prev->base_w : 0ull,
-                      prev ? prev->below : 0, LEVEL == 1, ctl, desc + (LEVEL - 1));
+  wq_pick_block<BITS>(N, alpha, ghc, ghw, lo, hi, prev ? prev->base_w : 0ull,
+                      prev ? prev->below : 0, LEVEL == 1,
+                      LEVEL == 1 ? 0.0 : __longlong_as_double((long long)ctl->tot), &ctl->tot,
+                      desc + (LEVEL - 1));
 }
 
 // ---- 7. final ---------------------------------------------------------------
@@ -425,72 +437,56 @@ __device__ __forceinline__ bool kless(u64 ka, int ia, u64 kb, int ib) {
   return ka < kb || (ka == kb && ia < ib);
 }
 
-// ---- 4./5. gather the segment + the fp64 sums, final in the last block -----
-__global__ __launch_bounds__(WQ_T) void wq_gather_final_kernel(
-    const double* __restrict__ x, const double* __restrict__ w, int64_t N, int64_t chunk,
-    double alpha, WqCtl* __restrict__ ctl, const WqDesc* __restrict__ desc,
-    u64* __restrict__ gkey, int* __restrict__ gidx, double* __restrict__ gw,
-    double* __restrict__ psum, double* __restrict__ q) {
-  __shared__ double sh[WQ_T / 64];
-  // the level-1 segment when it fits, else level 2's
-  const WqDesc D = desc[0].ok ? desc[0] : desc[1];
-  {
-    const int64_t b0 = (int64_t)blockIdx.x * chunk;
-    const int64_t b1 = b0 + chunk < N ? b0 + chunk : N;
-    double below = 0.0, all = 0.0;
-    for (int64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += WQ_U * WQ_T) {
-      double xv[WQ_U], wv[WQ_U];
-#pragma unroll
-      for (int u = 0; u < WQ_U; ++u) {
-        const int64_t i = i0 + (int64_t)u * WQ_T;
-        xv[u] = i < b1 ? x[i] : 0.0;
-        wv[u] = i < b1 ? w[i] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < WQ_U; ++u) {
-      const int64_t i = i0 + (int64_t)u * WQ_T;
-      if (i >= b1) continue;
-      const u64 k = qkey(xv[u]);
-      const double wi = wval(wv[u]);
-      all += wi;
-      if (k < D.lo) below += wi;
-      else if (D.ok && k <= D.hi) {
-        const unsigned int pos = atomicAdd(&ctl->list_n, 1u);
-        if (pos < (unsigned int)WQ_CAP) {
-          st_agent(&gkey[pos], k);
-          st_agent(&gidx[pos], (int)i);
-          st_agent(&gw[pos], wi);
-        }
-      }
-      }
-    }
-    auto add = [](double a, double b) { return a + b; };
-    below = block_reduce(below, sh, add);
-    all = block_reduce(all, sh, add);
-    if (threadIdx.x == 0) {
-      st_agent(&psum[2 * blockIdx.x], below);
-      st_agent(&psum[2 * blockIdx.x + 1], all);
-    }
-  }
-  if (!wq_last_block(&ctl->done[2])) return;
-  wq_reset(ctl);
-  const int nsum = gridDim.x;
-  __shared__ u64 skey[WQ_CAP];
-  __shared__ int sidx[WQ_CAP];
-  __shared__ double sw[WQ_CAP];
-  __shared__ Knot kn[WQ_CAP];
+// ---- the final (one block) ------------------------------------------------------
+// The gather blocks' fp64 sums, the segment's list sorted by (key, index),
+// the cumulative weights and np.interp's rules.
+struct WqFinalLds {
+  u64 skey[WQ_CAP];
+  int sidx[WQ_CAP];
+  double sw[WQ_CAP];
+  Knot kn[WQ_CAP];
+  int srank[WQ_CAP];
+};
+
+__device__ void wq_final(const WqDesc D, int64_t N, double alpha, int nsum,
+                         const double* psum, const u64* gkey, const int* gidx, const double* gw,
+                         double* q, WqFinalLds& L) {
+  u64* skey = L.skey;
+  int* sidx = L.sidx;
+  double* sw = L.sw;
+  Knot* kn = L.kn;
   __shared__ double dsh[WQ_FT / 64];
   const int t = threadIdx.x;
   if (!D.ok) {   // the knots sit in more than WQ_CAP points (ties): not decided
     if (t == 0) *q = NAN;
     return;
   }
-  // the gather blocks' fp64 sums: a fixed tree (lanes, then waves in order)
+  const int m = (int)D.count;
+  // the gather blocks' fp64 sums and the listed points: all loads in flight
+  // together, then the sums by a fixed tree (lanes, then waves in order)
   __shared__ double s_bt[2][WQ_FT / 64];
   __shared__ double s_below, s_total;
   {
     double bl = t < nsum ? ld_agent(&psum[2 * t]) : 0.0;
     double al = t < nsum ? ld_agent(&psum[2 * t + 1]) : 0.0;
+    constexpr int PT = WQ_CAP / WQ_FT;
+    u64 lk[PT];
+    int li[PT];
+    double lw[PT];
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const int e = t + q * WQ_FT;
+      if (e < m) {
+        lk[q] = ld_agent(&gkey[e]);
+        li[q] = ld_agent(&gidx[e]);
+        lw[q] = ld_agent(&gw[e]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const int e = t + q * WQ_FT;
+      if (e < m) { skey[e] = lk[q]; sidx[e] = li[q]; sw[e] = lw[q]; }
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       bl += __shfl_xor(bl, o, 64);
@@ -507,13 +503,6 @@ __global__ __launch_bounds__(WQ_T) void wq_gather_final_kernel(
     __syncthreads();
   }
   const double below = s_below, total = s_total;
-  const int m = (int)D.count;
-  for (int i = t; i < m; i += WQ_FT) {
-    skey[i] = ld_agent(&gkey[i]);
-    sidx[i] = ld_agent(&gidx[i]);
-    sw[i] = ld_agent(&gw[i]);
-  }
-  __syncthreads();
   // rank sort by (key, index) -- the stable order of the reference's sort:
   // each listed point counts the points before it (LDS broadcast reads, no
   // dependent stages; up to WQ_REFINE points the count is split over
@@ -522,7 +511,7 @@ __global__ __launch_bounds__(WQ_T) void wq_gather_final_kernel(
   // so the order -- and the fixed-order prefix below -- never depends on the
   // list's (atomic) fill order.
   {
-    __shared__ int srank[WQ_CAP];
+    int* srank = L.srank;
     const int G = m <= WQ_REFINE ? WQ_FT / WQ_REFINE : 1;
     const int per_g = WQ_FT / G, g = t / per_g, e0 = t % per_g;
     const int jn = (m + G - 1) / G, jlo = g * jn, jhi = min(m, jlo + jn);
@@ -589,6 +578,362 @@ __global__ __launch_bounds__(WQ_T) void wq_gather_final_kernel(
   }
 }
 
+
+// ---- 4./5. gather the segment + the fp64 sums, final in the last block -----
+__global__ __launch_bounds__(WQ_T) void wq_gather_final_kernel(
+    const double* __restrict__ x, const double* __restrict__ w, int64_t N, int64_t chunk,
+    double alpha, WqCtl* __restrict__ ctl, const WqDesc* __restrict__ desc,
+    u64* __restrict__ gkey, int* __restrict__ gidx, double* __restrict__ gw,
+    double* __restrict__ psum, double* __restrict__ q) {
+  __shared__ double sh[WQ_T / 64];
+  // the level-1 segment when it fits, else level 2's
+  const WqDesc D = desc[0].ok ? desc[0] : desc[1];
+  {
+    const int64_t b0 = (int64_t)blockIdx.x * chunk;
+    const int64_t b1 = b0 + chunk < N ? b0 + chunk : N;
+    double below = 0.0, all = 0.0;
+    for (int64_t i0 = b0 + threadIdx.x; i0 < b1; i0 += WQ_U * WQ_T) {
+      double xv[WQ_U], wv[WQ_U];
+#pragma unroll
+      for (int u = 0; u < WQ_U; ++u) {
+        const int64_t i = i0 + (int64_t)u * WQ_T;
+        xv[u] = i < b1 ? x[i] : 0.0;
+        wv[u] = i < b1 ? w[i] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < WQ_U; ++u) {
+      const int64_t i = i0 + (int64_t)u * WQ_T;
+      if (i >= b1) continue;
+      const u64 k = qkey(xv[u]);
+      const double wi = wval(wv[u]);
+      all += wi;
+      if (k < D.lo) below += wi;
+      else if (D.ok && k <= D.hi) {
+        const unsigned int pos = atomicAdd(&ctl->list_n, 1u);
+        if (pos < (unsigned int)WQ_CAP) {
+          st_agent(&gkey[pos], k);
+          st_agent(&gidx[pos], (int)i);
+          st_agent(&gw[pos], wi);
+        }
+      }
+      }
+    }
+    auto add = [](double a, double b) { return a + b; };
+    below = block_reduce(below, sh, add);
+    all = block_reduce(all, sh, add);
+    if (threadIdx.x == 0) {
+      st_agent(&psum[2 * blockIdx.x], below);
+      st_agent(&psum[2 * blockIdx.x + 1], all);
+    }
+  }
+  if (!wq_last_block(&ctl->done[2])) return;
+  wq_reset(ctl);
+  __shared__ WqFinalLds L;
+  wq_final(D, N, alpha, (int)gridDim.x, psum, gkey, gidx, gw, q, L);
+}
+
+// ---- one launch: every stage in one resident grid ---------------------------
+// Up to WQ_ONE_MAX points (c3's 1e6) each thread holds its WQ_U points in
+// registers from the first read: the range, both histogram levels and the
+// gather run on them, the stages separated by grid-wide hand-offs instead of
+// kernel boundaries (the grid -- at most WQ_MAXB blocks, one per CU -- is
+// checked against the device's resident capacity before launch, so every
+// block runs at once).  A hand-off: every block bumps an arrival counter;
+// the block that brings it to the grid size runs the stage's tail alone (the
+// level's pick), publishes its result with agent-scope stores and raises a
+// flag; the others wait on the flag.  Level 1 bins on 256 bins (not 2048 as
+// the four-launch path): the flush of each block's LDS histogram into the
+// global one is one integer atomic per non-empty bin and block, and with
+// ~250 blocks those atomics on a few KB dominated the level (measured:
+// 28 us at 2048 bins, profiles/r06_quantile_onepass.log); level 2 then
+// resolves the wider segment (4096 bins over its few thousand points).
+// A third level (4096 bins) resolves spans whose points crowd into a tiny
+// part of the key range.
+// Deterministic (integer histograms, fixed-order fp64 sums); the segment
+// differs from the four-launch path's, so the fp64 sum below it -- and q --
+// may differ from that path's in the last bits (both within the 1e-12 bar).
+constexpr int64_t WQ_ONE_MAX = (int64_t)WQ_MAXB * WQ_U * WQ_T;
+constexpr int WQ_BITS1_ONE = 8;
+constexpr int WQ_ONE_LEVELS = 3;   // 256 x 4096 x 4096 bins over the key span at most
+constexpr unsigned int WQ_SPIN_MAX = 1u << 18;   // 10-300 ms of polls: a hang guard only
+
+union WqOneLds {
+  struct { unsigned int cnt[WQ_NB]; u64 ws[WQ_NB]; } h;
+  WqFinalLds f;
+};
+
+// Hand-off counters and flags (a zeroed workspace region, one 256-B line
+// each so that no two share a memory channel's queue): blocks arrive on the
+// counter of their group (block index mod 8), the last of a group on the top
+// counter, and the last there is the last block; it raises one flag per
+// group, which the group's blocks poll.  One counter for every block cost
+// ~12 us per hand-off at 245 blocks (the arrivals and polls on one address
+// are served one after another), the groups ~3 us.
+// The key range and the weight maximum go the same way: one (~key min, key
+// max, weight max) slot per group, read by every block after hand-off 1 (the
+// same three addresses for every block cost ~5 us more).
+constexpr int WQ_HS_STRIDE = 64;                 // u32 per line
+constexpr int WQ_HS_TOP = 8, WQ_HS_FLAG = 9;     // line indices
+constexpr int WQ_HS_RANGE = 17;                  // 8 lines: u64 ~kmin, kmax, wmax
+constexpr int WQ_HS_LINES = WQ_HS_RANGE + 8;
+
+// Arrival k (1, 2, ...): true in the block that arrives last.  Everything a
+// stage hands on is written by agent-scope atomics and stores (performed at
+// the agent's coherence point, past the XCD's L2), complete (s_waitcnt)
+// before the block arrives, and read after the wait with agent-scope loads,
+// which the workgroup barrier after the wait keeps behind it.  So the
+// counters and flags need no release / acquire of their own -- an
+// agent-scope release writes back the XCD's whole L2 (one per block per
+// hand-off measured as slow as the contended counter).
+__device__ bool wq_arrive(unsigned int* hs, unsigned int k) {
+  __shared__ int s_last;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int g = blockIdx.x & 7u, ng = (gridDim.x - g + 7u) >> 3;
+    const unsigned int groups = gridDim.x < 8u ? gridDim.x : 8u;
+    int last = 0;
+    if (__hip_atomic_fetch_add(&hs[g * WQ_HS_STRIDE], 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT) == k * ng - 1u)
+      last = __hip_atomic_fetch_add(&hs[WQ_HS_TOP * WQ_HS_STRIDE], 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == k * groups - 1u;
+    s_last = last;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+// the last block's result is out: raise every group's flag to k
+__device__ void wq_release(unsigned int* hs, unsigned int k) {
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x < (gridDim.x < 8u ? gridDim.x : 8u))
+    st_agent(&hs[(WQ_HS_FLAG + threadIdx.x) * WQ_HS_STRIDE], k);
+}
+// wait for flag k.  A wait that outlasts WQ_SPIN_MAX polls (the grid was not
+// resident after all) returns false: the caller leaves q NaN, the host's
+// exact path then answers, and the control block stays poisoned for the
+// calls after.
+__device__ bool wq_wait(unsigned int* hs, unsigned int k) {
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    const unsigned int* f = &hs[(WQ_HS_FLAG + (blockIdx.x & 7u)) * WQ_HS_STRIDE];
+    int ok = 1;
+    for (unsigned int it = 0; ld_agent(f) < k; ++it) {
+      if (it >= WQ_SPIN_MAX) { ok = 0; break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+__device__ __forceinline__ void wq_poison(WqCtl* ctl, double* q) {
+  if (threadIdx.x == 0) {
+    st_agent(&ctl->pad, 1u);
+    st_agent(q, (double)NAN);
+  }
+}
+
+__device__ __forceinline__ void st_desc(WqDesc* g, const WqDesc& d) {
+  st_agent(&g->lo, d.lo);
+  st_agent(&g->hi, d.hi);
+  st_agent(&g->base_w, d.base_w);
+  st_agent(&g->count, d.count);
+  st_agent(&g->below, d.below);
+  st_agent(&g->ok, d.ok);
+}
+__device__ __forceinline__ WqDesc ld_desc(const WqDesc* g) {
+  WqDesc d;
+  d.lo = ld_agent(&g->lo);
+  d.hi = ld_agent(&g->hi);
+  d.base_w = ld_agent(&g->base_w);
+  d.count = ld_agent(&g->count);
+  d.below = ld_agent(&g->below);
+  d.ok = ld_agent(&g->ok);
+  d.done = 0;
+  return d;
+}
+
+__global__ __launch_bounds__(WQ_T) void wq_onepass_kernel(
+    const double* __restrict__ x, const double* __restrict__ w, int64_t N, int64_t chunk,
+    double alpha, WqCtl* __restrict__ ctl, unsigned int* __restrict__ hs,
+    WqDesc* __restrict__ gdesc, unsigned int* __restrict__ ghc, u64* __restrict__ ghw,
+    u64* __restrict__ gkey,
+    int* __restrict__ gidx, double* __restrict__ gw, double* __restrict__ psum,
+    double* __restrict__ q) {
+  __shared__ WqOneLds L;
+  __shared__ double shd[WQ_T / 64];
+  __shared__ WqDesc sD;
+  __shared__ u64 s_tot;
+  if (ld_agent(&ctl->pad)) {   // an earlier call's wait timed out
+    if (blockIdx.x == 0 && threadIdx.x == 0) *q = NAN;
+    return;
+  }
+  const int t = threadIdx.x;
+  // every level's global histogram to zero (added into after hand-off 1)
+  for (int e = blockIdx.x * WQ_T + t; e < WQ_ONE_LEVELS * WQ_NB; e += gridDim.x * WQ_T) {
+    st_agent(&ghc[e], 0u);
+    st_agent(&ghw[e], 0ull);
+  }
+  const int64_t b0 = (int64_t)blockIdx.x * chunk;
+  const int64_t b1 = b0 + chunk < N ? b0 + chunk : N;
+  u64 kv[WQ_U];
+  double wv[WQ_U];
+  bool in[WQ_U];
+  u64 mn = ~0ull, mx = 0ull, wm = 0ull;
+  double all = 0.0;
+#pragma unroll
+  for (int u = 0; u < WQ_U; ++u) {
+    const int64_t i = b0 + t + (int64_t)u * WQ_T;
+    in[u] = i < b1;
+    kv[u] = in[u] ? qkey(x[i]) : ~0ull;
+    wv[u] = in[u] ? wval(w[i]) : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < WQ_U; ++u) {
+    if (!in[u]) continue;
+    mn = kv[u] < mn ? kv[u] : mn;
+    mx = kv[u] > mx ? kv[u] : mx;
+    const u64 wb = (u64)__double_as_longlong(wv[u]);   // >= 0: bits order like values
+    wm = wb > wm ? wb : wm;
+    all += wv[u];
+  }
+  auto add = [](double a, double b) { return a + b; };
+  {
+    // the four block reductions in one pass (~kmin, kmax, wmax by max; the
+    // weight sum by the same fixed tree as block_reduce)
+    u64 nmn = ~mn;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const u64 a = __shfl_xor(nmn, o, 64), b = __shfl_xor(mx, o, 64),
+                c = __shfl_xor(wm, o, 64);
+      nmn = a > nmn ? a : nmn;
+      mx = b > mx ? b : mx;
+      wm = c > wm ? c : wm;
+      all += __shfl_xor(all, o, 64);
+    }
+    __shared__ u64 s_r[3][WQ_T / 64];
+    if ((t & 63) == 0) {
+      s_r[0][t >> 6] = nmn; s_r[1][t >> 6] = mx; s_r[2][t >> 6] = wm; shd[t >> 6] = all;
+    }
+    __syncthreads();
+    if (t == 0) {
+      double a = shd[0];
+      for (int i = 1; i < WQ_T / 64; ++i) {
+        nmn = s_r[0][i] > nmn ? s_r[0][i] : nmn;
+        mx = s_r[1][i] > mx ? s_r[1][i] : mx;
+        wm = s_r[2][i] > wm ? s_r[2][i] : wm;
+        a += shd[i];
+      }
+      unsigned long long* r = reinterpret_cast<unsigned long long*>(
+          &hs[(WQ_HS_RANGE + (blockIdx.x & 7u)) * WQ_HS_STRIDE]);
+      atomicMax(&r[0], (unsigned long long)nmn);
+      atomicMax(&r[1], (unsigned long long)mx);
+      atomicMax(&r[2], (unsigned long long)wm);
+      st_agent(&psum[2 * blockIdx.x + 1], a);
+    }
+  }
+  if (wq_arrive(hs, 1)) wq_release(hs, 1);
+  if (!wq_wait(hs, 1)) { wq_poison(ctl, q); return; }
+
+  __shared__ Range s_range;
+  if (t < 64) {   // the groups' slots (zero = the identity of the max)
+    const unsigned int groups = gridDim.x < 8u ? gridDim.x : 8u;
+    const u64* r = reinterpret_cast<const u64*>(&hs[(WQ_HS_RANGE + (t & 7)) * WQ_HS_STRIDE]);
+    u64 a = 0ull, b = 0ull, c = 0ull;
+    if (t < (int)groups) { a = ld_agent(&r[0]); b = ld_agent(&r[1]); c = ld_agent(&r[2]); }
+#pragma unroll
+    for (int o = 4; o > 0; o >>= 1) {
+      const u64 a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64), c2 = __shfl_xor(c, o, 64);
+      a = a2 > a ? a2 : a;
+      b = b2 > b ? b2 : b;
+      c = c2 > c ? c2 : c;
+    }
+    if (t == 0) {
+      const double wmax = __longlong_as_double((long long)c);
+      s_range = Range{~a, b, wmax > 0.0 ? ldexp(1.0, 62 - lg_ceil(N)) / wmax : 0.0};
+    }
+  }
+  __syncthreads();
+  const Range R = s_range;
+  // one histogram level over [lo, hi] into the level's global bins
+  auto level = [&](auto bits_c, u64 lo, u64 hi, unsigned int* gc, u64* gws) {
+    constexpr int BITS = decltype(bits_c)::value, NB = 1 << BITS;
+    for (int b = t; b < NB; b += WQ_T) { L.h.cnt[b] = 0u; L.h.ws[b] = 0ull; }
+    const int sh = span_shift<BITS>(lo, hi);
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < WQ_U; ++u) {
+      if (!in[u] || kv[u] < lo || kv[u] > hi) continue;
+      const int bin = (int)((kv[u] - lo) >> sh);
+      atomicAdd(&L.h.cnt[bin], 1u);
+      atomicAdd(&L.h.ws[bin], wfix(wv[u], R.S));
+    }
+    __syncthreads();
+    for (int b = t; b < NB; b += WQ_T) {
+      if (L.h.cnt[b]) {
+        atomicAdd(&gc[b], L.h.cnt[b]);
+        atomicAdd(reinterpret_cast<unsigned long long*>(&gws[b]),
+                  (unsigned long long)L.h.ws[b]);
+      }
+    }
+  };
+  level(std::integral_constant<int, WQ_BITS1_ONE>{}, R.kmin, R.kmax, ghc, ghw);
+  unsigned int k = 2;
+  if (wq_arrive(hs, k)) {
+    wq_pick_block<WQ_BITS1_ONE>(N, alpha, ghc, ghw, R.kmin, R.kmax, 0ull, 0, true, 0.0,
+                                &s_tot, &sD);
+    __syncthreads();
+    if (t == 0) {
+      st_desc(&gdesc[0], sD);
+      st_agent(&ctl->tot, s_tot);
+    }
+    wq_release(hs, k);
+  }
+  if (!wq_wait(hs, k)) { wq_poison(ctl, q); return; }
+  WqDesc D = ld_desc(&gdesc[0]);
+  // levels 2.. on 4096 bins while the segment holds more than WQ_CAP points
+  // (the same decision in every block)
+  for (int lev = 1; !D.ok && lev < WQ_ONE_LEVELS; ++lev) {
+    level(std::integral_constant<int, WQ_BITS>{}, D.lo, D.hi, ghc + lev * WQ_NB,
+          ghw + lev * WQ_NB);
+    ++k;
+    if (wq_arrive(hs, k)) {
+      wq_pick_block<WQ_BITS>(N, alpha, ghc + lev * WQ_NB, ghw + lev * WQ_NB, D.lo, D.hi,
+                             D.base_w, D.below, false,
+                             __longlong_as_double((long long)ld_agent(&ctl->tot)), nullptr, &sD);
+      __syncthreads();
+      if (t == 0) st_desc(&gdesc[lev & 1], sD);
+      wq_release(hs, k);
+    }
+    if (!wq_wait(hs, k)) { wq_poison(ctl, q); return; }
+    D = ld_desc(&gdesc[lev & 1]);
+  }
+  // gather: the segment's points into the list, the fp64 sum below it
+  double below = 0.0;
+#pragma unroll
+  for (int u = 0; u < WQ_U; ++u) {
+    if (!in[u]) continue;
+    if (kv[u] < D.lo) below += wv[u];
+    else if (D.ok && kv[u] <= D.hi) {
+      const unsigned int pos = atomicAdd(&ctl->list_n, 1u);
+      if (pos < (unsigned int)WQ_CAP) {
+        st_agent(&gkey[pos], kv[u]);
+        st_agent(&gidx[pos], (int)(b0 + t + (int64_t)u * WQ_T));
+        st_agent(&gw[pos], wv[u]);
+      }
+    }
+  }
+  below = block_reduce(below, shd, add);
+  if (t == 0) st_agent(&psum[2 * blockIdx.x], below);
+  if (!wq_arrive(hs, k + 1)) return;
+  // every block is past its last wait: the counters and flags back to zero
+  wq_reset(ctl);
+  if (t < WQ_HS_LINES * 8) st_agent(&hs[(t >> 3) * WQ_HS_STRIDE + (t & 7)], 0u);
+  wq_final(D, N, alpha, (int)gridDim.x, psum, gkey, gidx, gw, q, L.f);
+}
+
 int wq_blocks(int64_t N) {
   const int64_t b = ceil_div(N, 4096);
   return (int)(b < 1 ? 1 : (b > WQ_MAXB ? WQ_MAXB : b));
@@ -603,8 +948,9 @@ extern "C" size_t abc_weighted_quantile_workspace(int64_t N) {
   const int nb = wq_blocks(N > 0 ? N : 1);
   size_t off = 0;
   size_only<WqCtl>(off, 1);
-  size_only<unsigned int>(off, (size_t)2 * WQ_NB);
-  size_only<u64>(off, (size_t)2 * WQ_NB);
+  size_only<unsigned int>(off, (size_t)WQ_HS_LINES * WQ_HS_STRIDE);
+  size_only<unsigned int>(off, (size_t)WQ_ONE_LEVELS * WQ_NB);
+  size_only<u64>(off, (size_t)WQ_ONE_LEVELS * WQ_NB);
   size_only<WqDesc>(off, 2);
   size_only<u64>(off, WQ_CAP);
   size_only<int>(off, WQ_CAP);
@@ -629,14 +975,22 @@ extern "C" int abc_weighted_quantile(const double* points, const double* w, int6
   const int64_t chunk = ceil_div(N, nb);
   Carver cv(ws, ws_bytes);
   WqCtl* ctl = cv.take<WqCtl>(1);
-  unsigned int* ghc = cv.take<unsigned int>((size_t)2 * WQ_NB);   // level 1 | level 2
-  u64* ghw = cv.take<u64>((size_t)2 * WQ_NB);
+  unsigned int* hs = cv.take<unsigned int>((size_t)WQ_HS_LINES * WQ_HS_STRIDE);
+  // levels 1 | 2 (| 3: the one-launch path)
+  unsigned int* ghc = cv.take<unsigned int>((size_t)WQ_ONE_LEVELS * WQ_NB);
+  u64* ghw = cv.take<u64>((size_t)WQ_ONE_LEVELS * WQ_NB);
   WqDesc* desc = cv.take<WqDesc>(2);
   u64* lkey = cv.take<u64>(WQ_CAP);
   int* lidx = cv.take<int>(WQ_CAP);
   double* lw = cv.take<double>(WQ_CAP);
   double* psum = cv.take<double>((size_t)2 * nb);
   if (!cv.ok) return set_error(ABC_ERR_WORKSPACE, "quantile: carve");
+  if (N <= WQ_ONE_MAX && nb <= resident_blocks(wq_onepass_kernel, WQ_T, 0)) {
+    hipLaunchKernelGGL(wq_onepass_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk,
+                       alpha, ctl, hs, desc, ghc, ghw, lkey, lidx, lw, psum, q);
+    ABC_LAUNCHED();
+    return ABC_OK;
+  }
   hipLaunchKernelGGL(wq_range_kernel, dim3(nb), dim3(WQ_T), 0, s, points, w, N, chunk, ctl,
                      ghc, ghw);
   ABC_LAUNCHED();

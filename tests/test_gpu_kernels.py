@@ -490,20 +490,25 @@ def test_weighted_quantile_golden(dev):
 
 
 @pytest.mark.parametrize("case", ["normal", "skewed_w", "heavy_ties", "one_value",
-                                  "two_spikes", "zero_w", "big", "discrete", "tiny"])
+                                  "two_spikes", "zero_w", "big", "one_max", "dense_core",
+                                  "crowded", "discrete", "tiny"])
 def test_weighted_quantile_select(dev, case):
     """The weighted MSD select (abc_quantile.hip) against the oracle's stable
     sort + cumsum + interp (weighted_statistics.py:27-43): continuous data,
     skewed weights, ties by the thousand (the final block's refinement), one
     value for every point (the run summary), two spikes straddling the
-    quantile, zero weights, N = 2e6, integer-valued distances, N <= 3; alpha
+    quantile, zero weights, N = 2e6 (four launches), N = 2^20 (the one-launch
+    path's largest grid), half the points in 1e-4 of the range (the
+    one-launch path's third level), the bulk crowded next to two extreme
+    points (the segment keeps its lone neighbours, no level narrows it: left
+    to the sorted path), integer-valued distances, N <= 3; alpha
     at 0, 1, at a knot and between knots.  1e-12 relative.  Continuous data
     is decided by the select itself; knots inside ties by the thousand leave
     NaN and are resolved on the sort-based kernel (gpu.resolve_quantile)."""
     import zlib
     from pyabc_amd import gpu
     rng = np.random.default_rng(zlib.crc32(case.encode()))
-    N = {"big": 2_000_000, "tiny": 3}.get(case, 200_003)
+    N = {"big": 2_000_000, "one_max": 1 << 20, "tiny": 3}.get(case, 200_003)
     pts = rng.gamma(2.0, 1.5, N)
     w = rng.uniform(0.5, 1.5, N)
     if case == "skewed_w":
@@ -516,12 +521,18 @@ def test_weighted_quantile_select(dev, case):
         pts = np.where(rng.uniform(size=N) < 0.5, 1.0, np.nextafter(1.0, 2.0))
     elif case == "zero_w":
         w[rng.uniform(size=N) < 0.4] = 0.0
+    elif case == "dense_core":
+        pts = np.where(rng.uniform(size=N) < 0.5, 1.0 + rng.uniform(size=N),
+                       1.5 + 1e-4 * rng.uniform(size=N))
+    elif case == "crowded":
+        pts = 1.0 + 1e-3 * rng.uniform(size=N)
+        pts[7], pts[N // 2] = 1e-300, 1e300
     elif case == "discrete":
         pts = rng.integers(0, 40, N).astype(np.float64)
     w = w / w.sum()
     order = np.argsort(pts, kind="stable")
     knot = float(((np.cumsum(w[order]) - 0.5 * w[order]))[N // 3])
-    decided = case in ("normal", "skewed_w", "zero_w", "big", "tiny")
+    decided = case in ("normal", "skewed_w", "zero_w", "big", "one_max", "dense_core", "tiny")
     P, W = T(pts), T(w)
     for a in (0.0, 0.1, 0.5, knot, 0.9, 1.0):
         raw = float(gpu.weighted_quantile(P, W, a).cpu()[0])
