@@ -77,7 +77,7 @@ def normal_pairs(x0, x1):
     f32 = np.float32
     a = np.asarray(x0, dtype=np.uint32).astype(np.uint64)
     b = np.asarray(x1, dtype=np.uint32).astype(np.uint64)
-    m1 = a | np.uint64(1)                 # u1 = m1 2^-32 (32 bits)
+    m1 = a | np.uint64(1)                 # u1 = m1 2^-32 (32 bits; 41 below 2^-23)
     yi = np.uint64(1 << 32) - m1
     # series branch: u1 > 1 - 2^-8
     y = yi.astype(np.float32) * f32(2.0 ** -32)
@@ -86,9 +86,11 @@ def normal_pairs(x0, x1):
     z = z * y + f32(0.5)
     z = z * y + f32(1.0)
     v_series = z * y
-    # table branch
-    e = (np.frexp(m1.astype(np.float64))[1] - 1).astype(np.uint64)
-    t = (m1 << (np.uint64(31) - e)) & np.uint64(0xFFFFFFFF)
+    # table branch; u1 < 2^-23 (a < 2^9): 41 bits, b's 9 low bits below a's
+    ext = a < np.uint64(512)
+    mt = np.where(ext, (a << np.uint64(9)) | (b & np.uint64(511)) | np.uint64(1), m1)
+    e = (np.frexp(mt.astype(np.float64))[1] - 1).astype(np.uint64)
+    t = (mt << (np.uint64(31) - e)) & np.uint64(0xFFFFFFFF)
     i = ((t >> np.uint64(24)) & np.uint64(127)).astype(np.int64)
     delta = (t & np.uint64(0xFFFFFF)).astype(np.float32) * f32(2.0 ** -31)
     r = delta * T["inv"][i]
@@ -96,7 +98,7 @@ def normal_pairs(x0, x1):
     p = p * r - f32(0.5)
     p = p * r + f32(1.0)
     p = p * r
-    k = (np.uint64(32) - e).astype(np.float32)
+    k = (np.where(ext, np.uint64(41), np.uint64(32)) - e).astype(np.float32)
     LN2_HI, LN2_LO = f32(float.fromhex("0x1.62e4p-1")), f32(float.fromhex("0x1.7f7d1cp-20"))
     v_table = (k * LN2_HI - T["hi"][i]) + ((k * LN2_LO - T["lo"][i]) - p)
     v = np.where(yi < np.uint64(1 << 24), v_series, v_table).astype(np.float32)

@@ -128,9 +128,12 @@ __device__ __forceinline__ void stage_bm_tab(float* lds) {
 }
 
 // Box-Muller: n0 = R cos(2 pi u2), n1 = R sin(2 pi u2), R = sqrt(-2 ln u1),
-// u1 = m1 2^-32 with m1 the whole 32-bit word made odd (so u1 >= 2^-32 and
-// R <= sqrt(64 ln 2) = 6.66: the normals are cut at |n| < 6.66, mass
-// 2.7e-11 per normal), u2 = m2 2^-24 (m2 odd, 24 bits: the angle).  The
+// u1 = m1 2^-32 with m1 the whole 32-bit word a made odd, u2 = m2 2^-24 (m2
+// odd, the top 23 bits of b: the angle).  Below 2^-23 (a < 2^9) u1 takes
+// the 9 low bits of b, which the angle leaves unused, as 9 more bits: u1 =
+// m1' 2^-41, m1' = (a << 9 | b & 511) made odd.  So u1 >= 2^-41 and R <=
+// sqrt(82 ln 2) = 7.54: P(R > 7.54) = 2^-41, a normal's cut mass ~5e-14
+// (32 bits alone cut at 6.66, mass 2.7e-11).  The
 // transform is evaluated in fp32 with only correctly rounded operations in a
 // fixed order (no contraction; sqrt_rn; 4 KB of tables), so that
 // oracle/philox.py normal_pairs replays it bit for bit in numpy float32:
@@ -165,8 +168,11 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, double& n0,
     z = z * y + 1.0f;
     v = z * y;
   } else {
-    const int e = 31 - __clz((int)m1);               // floor(log2 m1), 0..31
-    const uint32_t t = m1 << (31 - e);               // leading one at bit 31
+    // u1 < 2^-23: 41 bits, the 9 low bits of b below a's (m1' < 2^18)
+    const bool ext = a < 512u;
+    const uint32_t mt = ext ? ((a << 9) | (b & 511u) | 1u) : m1;
+    const int e = 31 - __clz((int)mt);               // floor(log2 m), 0..31
+    const uint32_t t = mt << (31 - e);               // leading one at bit 31
     const int i = (int)((t >> 24) & 127u);
     const float delta = (float)(t & 0xFFFFFFu) * 0x1p-31f;
     const float* lg = tab + BM_TAB_LOG + 4 * i;      // (INV_C, LN_HI, LN_LO, 0)
@@ -175,7 +181,7 @@ __device__ __forceinline__ void box_muller(uint32_t a, uint32_t b, double& n0,
     p = p * r - 0.5f;
     p = p * r + 1.0f;
     p = p * r;                                       // log1p(r)
-    const float k = (float)(32 - e);
+    const float k = (float)((ext ? 41 : 32) - e);    // k LN2_HI exact (<= 23 bits)
     v = (k * LN2_HI - lg[1]) + ((k * LN2_LO - lg[2]) - p);
   }
   const float R = sqrt_rn(2.0f * v);

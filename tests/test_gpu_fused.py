@@ -494,7 +494,7 @@ def test_box_muller_accuracy(dev):
     normals equal the oracle's float32 replay (oracle/philox.py
     normal_pairs) BIT FOR BIT, and are within 4 fp32 ulp of R of an 80-bit
     long-double evaluation of R cos / R sin, R = sqrt(-2 ln u1), u1 = (a | 1)
-    2^-32 (32-bit u1: normals reach 6.66)."""
+    2^-32, below 2^-23 ((a << 9 | b & 511) | 1) 2^-41 (normals reach 7.54)."""
     from pyabc_amd import gpu
     from oracle.philox import normal_pairs, philox4x32_10
     B, S = 1 << 20, 4
@@ -508,9 +508,12 @@ def test_box_muller_accuracy(dev):
         ref = np.stack(normal_pairs(r[:, 2 * h], r[:, 2 * h + 1]), 1)
         np.testing.assert_array_equal(x[:, 2 * h:2 * h + 2], ref)
         rr = r.astype(np.uint64)
-        m1 = (rr[:, 2 * h] | np.uint64(1)).astype(ld)
-        m2 = ((rr[:, 2 * h + 1] >> np.uint64(9)) * 2 + 1).astype(ld)
-        R = np.sqrt(-2 * np.log(m1 * ld(2.0) ** -32))
+        a, b = rr[:, 2 * h], rr[:, 2 * h + 1]
+        u1 = np.where(a < np.uint64(512),
+                      ((a << np.uint64(9)) | (b & np.uint64(511)) | np.uint64(1)).astype(ld)
+                      * ld(2.0) ** -41, (a | np.uint64(1)).astype(ld) * ld(2.0) ** -32)
+        m2 = ((b >> np.uint64(9)) * 2 + 1).astype(ld)
+        R = np.sqrt(-2 * np.log(u1))
         ang = ld("3.14159265358979323846264338327950288") * m2 * ld(2.0) ** -23
         exact = np.stack([(R * np.cos(ang)).astype(np.float64),
                           (R * np.sin(ang)).astype(np.float64)], 1)

@@ -159,28 +159,37 @@ def test_box_muller_replay_accuracy_and_tail():
     """oracle.normal_pairs -- the bit-for-bit replay of the device transform
     (abc_common.h box_muller; tests/test_gpu_fused.py pins device == oracle)
     -- is within 4 fp32 ulp of R of a long-double R cos / R sin on 2M random
-    words plus the edges (u1 = 2^-32, u1 next to the series branch at
-    1 - 2^-8, u1 -> 1), and its largest radius is sqrt(-2 ln 2^-32) = 6.66,
-    so the normals are cut at |n| < 6.66 (mass 2 Phi(-6.66) = 2.7e-11)."""
+    words plus the edges (u1 = 2^-41, the 41-bit u1 below 2^-23 and the
+    32-bit one above, u1 next to the series branch at 1 - 2^-8, u1 -> 1),
+    and its largest radius is sqrt(-2 ln 2^-41) = 7.54: P(R > 7.54) =
+    2^-41 (32 bits alone: 6.66, 2^-32)."""
     rng = np.random.default_rng(3)
     a = rng.integers(0, 2 ** 32, 1 << 21, dtype=np.uint64)
     b = rng.integers(0, 2 ** 32, 1 << 21, dtype=np.uint64)
-    edge = np.array([0, 1, 2, 3, 2 ** 24 - 1, 2 ** 32 - 2 ** 24 - 1, 2 ** 32 - 2 ** 24,
-                     2 ** 32 - 2 ** 24 + 1, 2 ** 32 - 3, 2 ** 32 - 1], dtype=np.uint64)
+    edge = np.array([0, 1, 2, 3, 511, 512, 513, 2 ** 24 - 1, 2 ** 32 - 2 ** 24 - 1,
+                     2 ** 32 - 2 ** 24, 2 ** 32 - 2 ** 24 + 1, 2 ** 32 - 3, 2 ** 32 - 1],
+                    dtype=np.uint64)
     a = np.concatenate([edge, a])
-    b = np.concatenate([rng.integers(0, 2 ** 32, len(edge), dtype=np.uint64), b])
+    eb = rng.integers(0, 2 ** 32, len(edge), dtype=np.uint64)
+    eb[0] &= np.uint64(0xFFFFFE00)          # a = 0 with b's 9 low bits 0: u1 = 2^-41
+    b = np.concatenate([eb, b])
     n0, n1 = oracle.normal_pairs(a.astype(np.uint32), b.astype(np.uint32))
     ld = np.longdouble
-    m1 = (a | np.uint64(1)).astype(ld)
+    ext = a < np.uint64(512)
+    u1 = np.where(ext, ((a << np.uint64(9)) | (b & np.uint64(511)) | np.uint64(1)).astype(ld)
+                  * ld(2.0) ** -41, (a | np.uint64(1)).astype(ld) * ld(2.0) ** -32)
     m2 = ((b >> np.uint64(9)) * 2 + 1).astype(ld)
-    R = np.sqrt(-2 * np.log(m1 * ld(2.0) ** -32))
+    R = np.sqrt(-2 * np.log(u1))
     ang = ld("3.14159265358979323846264338327950288") * m2 * ld(2.0) ** -23
     for got, ex in ((n0, R * np.cos(ang)), (n1, R * np.sin(ang))):
         ulp = np.abs(got - ex.astype(np.float64)) / \
             np.spacing(R.astype(np.float32)).astype(np.float64)
         assert ulp.max() <= 4, ulp.max()
     r0 = float(np.hypot(n0[0], n1[0]))
-    assert abs(r0 - np.sqrt(64 * np.log(2))) < 1e-5 and r0 > 6.66
+    assert abs(r0 - np.sqrt(82 * np.log(2))) < 1e-5 and r0 > 7.53
+    # the 32-bit branch above 2^-23 is unchanged: a = 512 is its smallest u1
+    r512 = float(np.hypot(n0[5], n1[5]))
+    assert abs(r512 - np.sqrt(-2 * np.log(513 * 2.0 ** -32))) < 1e-5
 
 
 # ---- bootstrapped KDE CV (cv/bootstrap.py, golden from the reference) -----
