@@ -27,7 +27,7 @@ def main():
     for n, d in rows.items():
         if key and key not in n:
             continue
-        print(f"{d.get('VGPRs', '?'):>4} vgpr  spill {d.get('VGPRs Spill', '?'):>3}  "
+        print(f"{d.get('VGPRs', '?'):>4} vgpr {d.get('TotalSGPRs', '?'):>4} sgpr lds {d.get('LDS Size [bytes/block]', '?'):>6}  spill {d.get('VGPRs Spill', '?'):>3}  "
               f"occ {d.get('Occupancy [waves/SIMD]', '?'):>2}  {n[:110]}")
 
 
