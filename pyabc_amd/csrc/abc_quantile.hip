@@ -682,9 +682,11 @@ constexpr int WQ_HS_LINES = WQ_HS_RANGE + 8;
 // the agent's coherence point, past the XCD's L2), complete (s_waitcnt)
 // before the block arrives, and read after the wait with agent-scope loads,
 // which the workgroup barrier after the wait keeps behind it.  So the
-// counters and flags need no release / acquire of their own -- an
-// agent-scope release writes back the XCD's whole L2 (one per block per
-// hand-off measured as slow as the contended counter).
+// counters and flags need no release / acquire of their own: with them
+// (acq_rel arrivals, release flags, acquire polls and fence) a call takes
+// 0.174 instead of 0.044 ms at 1e6 -- every agent-scope release writes back
+// the XCD's L2 and every acquire invalidates it
+// (profiles/r06_quantile_release_ab.log).
 __device__ bool wq_arrive(unsigned int* hs, unsigned int k) {
   __shared__ int s_last;
   __builtin_amdgcn_s_waitcnt(0);
