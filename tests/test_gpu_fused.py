@@ -522,6 +522,29 @@ def test_box_muller_accuracy(dev):
         assert ulp.max() <= 4, ulp.max()
 
 
+def test_box_muller_tail_words(dev):
+    """The 41-bit u1 branch (first word < 2^9: u1 takes the angle word's 9
+    low bits) on the device: simulator draws at Philox indices whose u1 word
+    is below 512 (found by scanning oracle.philox4x32_10 for seed 5,
+    generation 6, the simulator slot) equal the oracle replay bit for bit,
+    and their radius lies beyond the 2^-23 edge (sqrt(46 ln 2) = 5.64)."""
+    from pyabc_amd import gpu
+    from oracle.philox import normal_pairs, philox4x32_10
+    hits = [4877494, 8440393, 12144803, 20704936, 22109970, 22722510]
+    S = 4
+    for h in hits:
+        r = philox4x32_10(np.array([h], dtype=np.uint64), 0x40000000, 6, 5)[0]
+        assert r[0] < 512 or r[2] < 512
+        th = torch.zeros((1, 1), dtype=torch.float64, device=dev)
+        x = gpu.simulate_linear_gaussian(th, T(np.zeros(S), torch.int32), T(np.zeros(S)),
+                                         T(np.ones(S)), 5, 6, h).cpu().numpy()[0]
+        for q in (0, 2):
+            n0, n1 = normal_pairs(r[q:q + 1], r[q + 1:q + 2])
+            np.testing.assert_array_equal(x[q:q + 2], [n0[0], n1[0]])
+            if r[q] < 512:
+                assert np.hypot(n0[0], n1[0]) > np.sqrt(46 * np.log(2)) - 1e-6
+
+
 @pytest.mark.parametrize("mode,d", [("mvn", 10), ("mvn", 3), ("local", 5), ("prior", 10),
                                     ("mvn", 7), ("mvn", 20)])
 def test_proposal_only_round_equals_propose(dev, mode, d):
