@@ -554,9 +554,9 @@ constexpr int LAZY_KT = 4;
 // Attempt 0 is the accepted proposal for EVERY candidate whose first LAZY_KT
 // coordinates lie in the support, when the support box of every coordinate
 // k >= LAZY_KT contains the whole range theta_k can take:
-//   |theta_k| <= max_jk |X_jk| + 7 sum_q |L_kq|
-// (every Box-Muller normal has |n| <= sqrt(2 * 32 ln 2) < 6.67; a relative
-// margin covers the roundings).  Also the early-reject statistics 0..3 must
+//   |theta_k| <= max_jk |X_jk| + 7.6 sum_q |L_kq|
+// (every Box-Muller normal has |n| <= sqrt(2 * 41 ln 2) < 7.54, the 41-bit
+// u1 of box_muller; a relative margin covers the roundings).  Also the early-reject statistics 0..3 must
 // read theta_src with src < LAZY_KT.  Decided per block from its LDS
 // constants (thread 0; the caller synchronises before C.lazy is read).
 template <int D, int MODE>
@@ -572,7 +572,7 @@ __device__ __forceinline__ bool lazy_filter_ok(const BlockConsts& C, const Propo
     for (int k = LAZY_KT; k < D; ++k) {
       double ls = 0.0;
       for (int q = 0; q <= k; ++q) ls += fabs(C.LT[q * D + k]);
-      const double b = (xm + 7.0 * ls) * 1.000001 + 1e-300;
+      const double b = (xm + 7.6 * ls) * 1.000001 + 1e-300;
       ok = ok && (C.box[2 * k] <= -b) && (b <= C.box[2 * k + 1]);  // NaN: false
     }
     return ok;
