@@ -353,6 +353,104 @@ __device__ void wq_pick_block(int64_t N, double alpha, const unsigned int* ghc,
   }
 }
 
+// The same pick by one wave (wave 0 of the block; the other waves do not
+// take part) for levels of at most 256 bins (4 per lane): the scans and
+// reductions are shuffles only -- no block barrier, no LDS -- and every
+// decision is the block version's (same prefix sums, same rules).
+template <int BITS>
+__device__ void wq_pick_wave(int64_t N, double alpha, const unsigned int* ghc,
+                             const u64* ghw, u64 lo, u64 hi, u64 base_w, long long base_c,
+                             bool level1, double tot_in, u64* tot_out, WqDesc* out) {
+  constexpr int NB = 1 << BITS, PER = NB / 64;
+  static_assert(NB % 64 == 0 && PER <= 4, "wave pick: 64 .. 256 bins");
+  const int lane = threadIdx.x & 63;
+  unsigned int c[PER];
+  u64 wsm[PER];
+  u64 sw = 0ull;
+  long long sc = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    c[i] = ld_agent(&ghc[lane * PER + i]);
+    wsm[i] = ld_agent(&ghw[lane * PER + i]);
+    sw += wsm[i];
+    sc += c[i];
+  }
+  u64 iw = sw;
+  long long ic = sc;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u64 a = __shfl_up(iw, o, 64);
+    const long long b = __shfl_up(ic, o, 64);
+    if (lane >= o) { iw += a; ic += b; }
+  }
+  const u64 tw = __shfl(iw, 63, 64);
+  u64 ow = iw - sw;
+  const long long oc = ic - sc;
+  const double tot_fx = level1 ? (double)tw : tot_in;
+  const double target = alpha * tot_fx;
+  const double margin = (double)N + ldexp(tot_fx, -48) + 4096.0;
+  ow += base_w;
+  int cb1 = -1, cb2 = NB, first = NB, last = -1;
+  {
+    u64 pw = ow;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int b = lane * PER + i;
+      if (c[i]) {
+        first = min(first, b);
+        last = max(last, b);
+        if ((double)(pw + wsm[i]) + margin <= target) cb1 = max(cb1, b);
+        if ((double)pw - margin > target) cb2 = min(cb2, b);
+      }
+      pw += wsm[i];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cb1 = max(cb1, __shfl_xor(cb1, o, 64));
+    cb2 = min(cb2, __shfl_xor(cb2, o, 64));
+    first = min(first, __shfl_xor(first, o, 64));
+    last = max(last, __shfl_xor(last, o, 64));
+  }
+  int b1 = cb1 >= 0 ? cb1 : first;
+  int b2 = cb2 < NB ? cb2 : last;
+  if (b1 >= NB) b1 = 0;
+  if (b2 < b1) b2 = b1;
+  // the prefix at b1 and the end of b2: held by one lane each, summed over
+  // the wave (every other lane adds zero)
+  u64 bw = 0ull;
+  long long bc = 0, ec = 0;
+  {
+    u64 pw = ow;
+    long long pc = oc;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int b = lane * PER + i;
+      if (b == b1) { bw = pw; bc = pc; }
+      if (b == b2) ec = pc + c[i];
+      pw += wsm[i];
+      pc += c[i];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    bw += __shfl_xor(bw, o, 64);
+    bc += __shfl_xor(bc, o, 64);
+    ec += __shfl_xor(ec, o, 64);
+  }
+  if (lane == 0) {
+    WqDesc d;
+    seg_keys(lo, hi, span_shift<BITS>(lo, hi), b1, b2, d.lo, d.hi);
+    d.base_w = bw;
+    d.below = base_c + bc;
+    d.count = ec - bc;
+    d.ok = d.count <= (level1 ? WQ_REFINE : WQ_CAP) ? 1 : 0;
+    d.done = 0;
+    *out = d;
+    if (level1) *tot_out = (u64)__double_as_longlong((double)tw);
+  }
+}
+
 // ---- 2./3. histogram of one level + its pick --------------------------------
 // level 1: the whole key range; level 2: the level-1 segment (every block
 // exits when the level-1 segment fits).  The block's LDS histogram goes into
@@ -884,8 +982,9 @@ __global__ __launch_bounds__(WQ_T) void wq_onepass_kernel(
   level(std::integral_constant<int, WQ_BITS1_ONE>{}, R.kmin, R.kmax, ghc, ghw);
   unsigned int k = 2;
   if (wq_arrive(hs, k)) {
-    wq_pick_block<WQ_BITS1_ONE>(N, alpha, ghc, ghw, R.kmin, R.kmax, 0ull, 0, true, 0.0,
-                                &s_tot, &sD);
+    if (t < 64)
+      wq_pick_wave<WQ_BITS1_ONE>(N, alpha, ghc, ghw, R.kmin, R.kmax, 0ull, 0, true, 0.0,
+                                 &s_tot, &sD);
     __syncthreads();
     if (t == 0) {
       st_desc(&gdesc[0], sD);
