@@ -20,9 +20,10 @@
 //      smallest key, dropped like indices[n, 1:]);
 //   3. the members (key < v*, or key == v* and index < j*, minus rank 0)
 //      compacted in index order;
-//   4. the moments sum lw, lw^2, lw delta, lw delta delta^T over the members
-//      in that order, chunks of rows staged in LDS, each thread owning a few
-//      of the 2 + d + d(d+1)/2 sums (deterministic);
+//   4. the moments sum lw, lw^2, lw delta, then (a second sweep) lw (delta -
+//      m)(delta - m)^T with the weighted mean m, over the members in that
+//      order, chunks of rows staged in LDS, each thread owning a few of the
+//      2 + d + d(d+1)/2 sums (deterministic);
 //   5. thread 0: np.cov of the offsets, the fix-ups, LU (partial pivoting;
 //      det and inverse from the same factors, as abc_local.hip), Cholesky.
 // pdf: one thread per candidate, population rows (inverse, row, log w -
@@ -106,6 +107,7 @@ __global__ __launch_bounds__(WT) void local_wide_fit_kernel(WideFitArgs A) {
   __shared__ double a_lu_l[BIG ? 1 : WD_MAX * (WD_MAX + 1)];
   __shared__ double cov_l[BIG ? 1 : WD_MAX * (WD_MAX + 1)];
   __shared__ int perm_l[BIG ? 1 : WD_MAX];
+  __shared__ double mean_l[BIG ? 1 : WD_MAX];
   double* bg = BIG ? A.big + (int64_t)blockIdx.x * wide_big_doubles(d) : nullptr;
   double* xn = BIG ? bg : xn_l;
   double* mom = BIG ? bg + d : mom_l;
@@ -197,13 +199,21 @@ __global__ __launch_bounds__(WT) void local_wide_fit_kernel(WideFitArgs A) {
     const int64_t nmem = s_nmem;
     // 4. moments over the members, one chunk of rows at a time; each thread
     // owns the sums f = t + e WT (16 per pass; more passes above d = 89, each
-    // streaming the members again)
+    // streaming the members again).  Two sweeps, as np.cov's own two passes
+    // (average, then the products of the centred offsets): first lw, lw^2
+    // and lw delta, then lw (delta - m)(delta - m)^T with the weighted mean m
+    // -- the one-sweep form E[dd^T] - m m^T cancelled when the neighbourhood
+    // sits off its particle (4e-11 relative at d = 80,
+    // profiles/r06_d80_weight_bound_probe.log).
     const int cs = d + 1;                  // chunk row stride
     double* chunk = chunk_l;
-    for (int f0 = 0; f0 < nm; f0 += 16 * WT) {
+    double* mean = BIG ? xsol : mean_l;    // (xsol is free until step 5)
+    for (int sweep = 0; sweep < 2; ++sweep) {
+    const int fa = sweep == 0 ? 0 : 2 + d, fb = sweep == 0 ? 2 + d : nm;
+    for (int f0 = fa; f0 < fb; f0 += 16 * WT) {
       double acc[16];
       int ea[16], eb[16];
-      const int rem = nm - f0;
+      const int rem = fb - f0;
       const int per = (rem + WT - 1) / WT < 16 ? (rem + WT - 1) / WT : 16;
       for (int e = 0; e < per; ++e) {
         acc[e] = 0.0;
@@ -226,12 +236,14 @@ __global__ __launch_bounds__(WT) void local_wide_fit_kernel(WideFitArgs A) {
         for (int e = t; e < rows * cs; e += WT) {
           const int r = e / cs, q = e - r * cs;
           const int64_t j = mem[c0 + r];
-          chunk[r * cs + q] = q < d ? A.X[j * d + q] - xn[q] : A.w[j];
+          chunk[r * cs + q] = q < d ? (sweep == 0 ? A.X[j * d + q] - xn[q]
+                                                  : (A.X[j * d + q] - xn[q]) - mean[q])
+                                    : A.w[j];
         }
         __syncthreads();
         for (int e = 0; e < per; ++e) {
           const int f = f0 + t + e * WT;
-          if (f >= nm) break;
+          if (f >= fb) break;
           double sm = acc[e];
           if (f == 0) {
             for (int r = 0; r < rows; ++r) sm += chunk[r * cs + d];
@@ -251,10 +263,15 @@ __global__ __launch_bounds__(WT) void local_wide_fit_kernel(WideFitArgs A) {
       }
       for (int e = 0; e < per; ++e) {
         const int f = f0 + t + e * WT;
-        if (f < nm) mom[f] = acc[e];
+        if (f < fb) mom[f] = acc[e];
       }
     }
     __syncthreads();
+    if (sweep == 0) {
+      for (int q = t; q < d; q += WT) mean[q] = mom[2 + q] / mom[0];
+      __syncthreads();
+    }
+    }
     // 5. covariance, fix-ups, factorisations (thread 0)
     if (t == 0) {
       if (N == 1) {
@@ -271,7 +288,8 @@ __global__ __launch_bounds__(WT) void local_wide_fit_kernel(WideFitArgs A) {
         int f = 2 + d;
         for (int a = 0; a < d; ++a)
           for (int b = a; b < d; ++b, ++f) {
-            const double v = (mom[f] / sw - (mom[2 + a] / sw) * (mom[2 + b] / sw)) / (1.0 - sa2);
+            // (mom[f]: the centred products of the second sweep)
+            const double v = (mom[f] / sw) / (1.0 - sa2);
             cov[(a) * ld + (b)] = v;
             cov[(b) * ld + (a)] = v;
           }
