@@ -35,6 +35,22 @@ def normals(index, slot0, n, generation, seed):
     return out
 
 
+def perturbation_normals(index, slot0, n, generation, seed, anc_words):
+    """The n perturbation normals of one attempt (pyabc_amd/csrc/
+    abc_candidate.h perturb_words): normals 0, 1 from the ancestor draw's
+    unused words 2, 3 (anc_words [B, 4]); normals 2 q' + 2, 2 q' + 3 from half
+    q' & 1 of slot slot0 + q' // 2."""
+    index = np.asarray(index, dtype=np.uint64)
+    out = np.empty((len(index), n))
+    a0, a1 = normal_pairs(anc_words[:, 2], anc_words[:, 3])
+    out[:, 0] = a0
+    if n > 1:
+        out[:, 1] = a1
+    if n > 2:
+        out[:, 2:] = normals(index, slot0, n - 2, generation, seed)
+    return out
+
+
 def prior_logpdf(theta, kinds, params):
     """Product prior in log space with scipy's closed-support pdfs."""
     theta = np.atleast_2d(theta)
@@ -98,7 +114,7 @@ def propose_mvn(X, w, L, seed, generation, idx0, B, kinds=None, params=None,
         r = philox4x32_10(ii, s0, generation, seed)
         u = uniform53(r[:, 0], r[:, 1])
         j = np.minimum(np.searchsorted(cdf, u * total, side="right"), N - 1)
-        n = normals(ii, s0 + SLOT_PERTURB, d, generation, seed)
+        n = perturbation_normals(ii, s0 + SLOT_PERTURB, d, generation, seed, r)
         if per_particle:
             th = X[j] + np.einsum("bkq,bq->bk", np.asarray(L)[j], n)
         else:

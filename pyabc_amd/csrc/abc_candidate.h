@@ -24,7 +24,7 @@ namespace abc {
 constexpr double LOG_SQRT_2PI = 0.91893853320467274178;
 constexpr uint32_t SLOTS_PER_ATTEMPT = 65536;
 constexpr uint32_t SLOT_ANCESTOR = 0;
-constexpr uint32_t SLOT_PERTURB = 1;     // 4 normals per slot
+constexpr uint32_t SLOT_PERTURB = 1;     // 4 normals per slot (after the first two)
 constexpr uint32_t SLOT_PRIOR = 32;      // + 512 k + iteration
 constexpr uint32_t SLOT_SIM = 0x40000000u;
 
@@ -36,6 +36,25 @@ __device__ __forceinline__ void normals4(uint64_t g, uint32_t slot, uint32_t gen
   u32x4 r = philox(g, slot, gen, seed);
   box_muller(r.x, r.y, n[0], n[1], tab);
   if (need > 2) box_muller(r.z, r.w, n[2], n[3], tab);
+}
+
+// Words of perturbation pair p (normals 2 p, 2 p + 1) of one attempt: pair 0
+// takes the ancestor draw's unused second pair (its uniform53 reads x, y);
+// pair p >= 1 half (p - 1) & 1 of slot SLOT_PERTURB + (p - 1) / 2, whose
+// Philox call the caller makes when (p - 1) is even (into r).  A d = 9 or 10
+// proposal then needs 2 perturbation calls instead of 3.
+__device__ __forceinline__ void perturb_words(int p, const u32x4& anc, u32x4& r, uint64_t g,
+                                              uint32_t s0, uint32_t gen, uint64_t seed,
+                                              uint32_t& wa, uint32_t& wb) {
+  if (p == 0) {
+    wa = anc.z;
+    wb = anc.w;
+    return;
+  }
+  const int p1 = p - 1;
+  if ((p1 & 1) == 0) r = philox(g, s0 + SLOT_PERTURB + (uint32_t)(p1 >> 1), gen, seed);
+  wa = (p1 & 1) ? r.z : r.x;
+  wb = (p1 & 1) ? r.w : r.y;
 }
 
 // ---- priors (scipy.stats pdf conventions, closed support [a, b]) ----------
@@ -485,8 +504,9 @@ __device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockCon
       // the ancestor's guide bracket is loaded first and the perturbation
       // L n (independent of j) is computed while those loads are in flight;
       // the search and the X_j row come after: theta_k = X_jk + (L n)_k
-      u32x4 r = philox(g, s0 + SLOT_ANCESTOR, A.gen, A.seed);
-      const double target = uniform53(r.x, r.y) * total;
+      const u32x4 ra = philox(g, s0 + SLOT_ANCESTOR, A.gen, A.seed);
+      u32x4 r = ra;
+      const double target = uniform53(ra.x, ra.y) * total;
       AncestorBracket br;
       if (TABLE) {
         const int64_t kt = anc_bin(target, C.inv_step, A.G);
@@ -507,9 +527,10 @@ __device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockCon
       // column q only reaches rows k >= q: with D known the pair loop is
       // unrolled and the upper triangle's multiply-adds vanish
       auto pair = [&](int q) {
-        if ((q & 3) == 0) r = philox(g, s0 + SLOT_PERTURB + (uint32_t)(q >> 2), A.gen, A.seed);
+        uint32_t wa, wb;
+        perturb_words(q >> 1, ra, r, g, s0, A.gen, A.seed, wa, wb);
         double n0, n1;
-        box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1, C.bmt);
+        box_muller(wa, wb, n0, n1, C.bmt);
         const bool two = q + 1 < d;
 #pragma unroll
         for (int k = 0; k < (D > 0 ? D : d); ++k) {
@@ -543,8 +564,9 @@ __device__ __forceinline__ int propose_one(const ProposalArgs& A, const BlockCon
 
 // ---- the lazy early-reject head ---------------------------------------------
 // With a lower-triangular L, theta_k depends on normals 0..k only, so the
-// first LAZY_KT coordinates of attempt 0 need one perturbation Philox call
-// and two Box-Muller pairs instead of all d.  lazy_head_group (below)
+// first LAZY_KT coordinates of attempt 0 need the ancestor draw's second
+// pair, one perturbation Philox call and two Box-Muller pairs instead of
+// all d.  lazy_head_group (below)
 // evaluates exactly those coordinates with propose_one's operations in
 // propose_one's order (same streams, same fma chain, same X_j + (L n)_k), so
 // they are the bits propose_one produces whenever attempt 0 is the accepted
@@ -695,10 +717,13 @@ __device__ __forceinline__ void lazy_head_group(const ProposalArgs& A, const Sim
   const double* box = C.box + oz;
   double target[CG];
   int32_t glo[CG], ghi[CG];
+  uint32_t az[CG], aw[CG];   // the ancestor draw's second pair: normals 0, 1
 #pragma unroll
   for (int c = 0; c < CG; ++c) {
     const u32x4 r = philox(g[c], SLOT_ANCESTOR, A.gen, A.seed);
     target[c] = uniform53(r.x, r.y) * C.total;
+    az[c] = r.z;
+    aw[c] = r.w;
     const int64_t kt = anc_bin(target[c], C.inv_step, A.G);
     glo[c] = A.bguide[kt];
     ghi[c] = A.bguide[kt + 1];
@@ -711,8 +736,9 @@ __device__ __forceinline__ void lazy_head_group(const ProposalArgs& A, const Sim
     const u32x4 r = philox(g[c], SLOT_PERTURB, A.gen, A.seed);
 #pragma unroll
     for (int q = 0; q < KT; q += 2) {
+      // (perturb_words: pair 0 from the ancestor draw, pair 1 from x, y)
       double n0, n1;
-      box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1, C.bmt);
+      box_muller(q == 0 ? az[c] : r.x, q == 0 ? aw[c] : r.y, n0, n1, C.bmt);
 #pragma unroll
       for (int k = 0; k < KT; ++k) {
         if (k >= q) th[c][k] = fma(LT[q * D + k], n0, th[c][k]);

@@ -72,15 +72,17 @@ __global__ __launch_bounds__(256) void propose_wide_kernel(
         th[k] = prior_draw1(A.kind[k], A.params + 4 * k, g, s0 + SLOT_PRIOR + 512u * k, A.gen,
                             A.seed);
     } else {
-      u32x4 r = philox(g, s0 + SLOT_ANCESTOR, A.gen, A.seed);
-      const double target = uniform53(r.x, r.y) * total;
+      const u32x4 ra = philox(g, s0 + SLOT_ANCESTOR, A.gen, A.seed);
+      u32x4 r = ra;
+      const double target = uniform53(ra.x, ra.y) * total;
       j = ancestor_search(A.cdf, A.guide, A.N, total, target);
       const double* Lj = MODE == PROP_LOCAL ? A.L + j * d * d : A.L;
       for (int k = 0; k < d; ++k) th[k] = 0.0;
       for (int q = 0; q < d; q += 2) {
-        if ((q & 3) == 0) r = philox(g, s0 + SLOT_PERTURB + (uint32_t)(q >> 2), A.gen, A.seed);
+        uint32_t wa, wb;
+        perturb_words(q >> 1, ra, r, g, s0, A.gen, A.seed, wa, wb);
         double n0, n1;
-        box_muller((q & 2) ? r.z : r.x, (q & 2) ? r.w : r.y, n0, n1);
+        box_muller(wa, wb, n0, n1);
         const bool two = q + 1 < d;
         for (int k = q; k < d; ++k) {
           th[k] = fma(Lj[k * d + q], n0, th[k]);
